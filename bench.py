@@ -1,0 +1,93 @@
+#!/usr/bin/env python3
+"""Headline benchmark: whole-node output tokens/s (+ p50 per-token latency) of Llama-2-7B
+layer-sharded over N MI355X GPUs (BASELINE.json).
+
+    python bench.py --gpus N --steps K --warmup W
+    (N > 1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+             --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...)
+
+Workload (synthetic prompts, random-init bf16 weights of the exact Llama-2-7B architecture,
+generated on each device - no checkpoints are available offline):
+  * rank r owns a contiguous layer range chosen by the master scheduler (rank 0 also holds
+    the embedding, rank N-1 the final norm + lm_head), one process per GPU;
+  * M = N micro-batches of B sequences each are in flight in the pipeline (B per GPU is
+    fixed -> weak scaling); every sequence was prefilled with a P-token prompt first;
+  * one timed "step" = every in-flight sequence produces one new token (greedy, fused
+    lm_head+argmax on device); hidden states move stage->stage with RCCL send/recv over
+    xGMI, token ids return last->first the same way.
+  * W untimed warm-up steps, then exactly K timed steps bracketed by barrier +
+    torch.cuda.synchronize(); the max over ranks is reported by rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+BASELINE_TOK_S = None  # BASELINE.json "published" is empty: no reference number to divide by
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=64)
+    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--model", default="llama2-7b")
+    ap.add_argument("--batch", type=int, default=16, help="sequences per micro-batch (per GPU)")
+    ap.add_argument("--prompt-len", type=int, default=128)
+    ap.add_argument("--max-seq", type=int, default=1024)
+    ap.add_argument("--microbatches", type=int, default=0, help="0 = one per pipeline stage")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--json-out", default="")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if a.gpus != world and world != 1:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    if a.gpus > 1 and world == 1:
+        raise SystemExit("multi-GPU runs must be launched with torch.distributed.run (one rank per GPU)")
+    from llm_sharding_amd.parallel.pipeline import run_decode_benchmark
+    res = run_decode_benchmark(model=a.model, n_gpus=a.gpus, steps=a.steps, warmup=a.warmup,
+                               batch=a.batch, prompt_len=a.prompt_len, max_seq=a.max_seq,
+                               microbatches=a.microbatches, seed=a.seed, use_graph=not a.no_graph)
+    if res is None:  # non-zero ranks
+        return
+    line = {
+        "metric": "output_tokens_per_sec_whole_node",
+        "value": round(res["tok_s"], 2),
+        "unit": "tokens/s",
+        "n_gpus": a.gpus,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(res["ms_per_step"], 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": (round(res["tok_s"] / BASELINE_TOK_S, 3) if BASELINE_TOK_S else None),
+        "dtype": "bf16",
+        "data": "synthetic prompts, random-init weights (Llama-2-7B architecture)",
+        "config": {"model": res["model_name"], "global_batch": res["global_batch"],
+                   "seq_len": a.prompt_len + a.warmup + a.steps,
+                   "parallelism": f"pp{a.gpus}", "microbatches": res["microbatches"],
+                   "batch_per_microbatch": a.batch, "prompt_len": a.prompt_len},
+        "p50_tpot_ms": round(res["p50_tpot_ms"], 4),
+        "p90_tpot_ms": round(res["p90_tpot_ms"], 4),
+        "ttft_ms": round(res["ttft_ms"], 3),
+        "reference_anecdote_tok_s": 4.3,
+    }
+    print(json.dumps(line), flush=True)
+    if a.json_out:
+        with open(a.json_out, "w") as f:
+            json.dump(line, f)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,106 @@
+#!/usr/bin/env python3
+"""In-tree native build for llm_sharding_amd.
+
+Produces (git-ignored, but they travel to the GPU box with the gpurun snapshot):
+  llm_sharding_amd/_native/liblsa_kernels.so   HIP kernels for gfx950 (hipcc, -O3)
+  llm_sharding_amd/_native/liblsa_comm.so      C++ TCP transport (epoll, framed) - no GPU
+
+Incremental: an object is rebuilt only when its source or any header in csrc/ is newer.
+Usage: python csrc/build.py [--force] [-j N] [--arch gfx950]
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import glob
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "csrc")
+OUT = os.path.join(ROOT, "llm_sharding_amd", "_native")
+OBJ = os.path.join(ROOT, "build", "obj")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+
+
+def _hipcc() -> str:
+    p = os.path.join(ROCM, "bin", "hipcc")
+    return p if os.path.exists(p) else (shutil.which("hipcc") or "hipcc")
+
+
+def _newest_header() -> float:
+    hs = glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True)
+    return max((os.path.getmtime(h) for h in hs), default=0.0)
+
+
+def _stale(src: str, obj: str, hdr_mtime: float) -> bool:
+    if not os.path.exists(obj):
+        return True
+    t = os.path.getmtime(obj)
+    return t < os.path.getmtime(src) or t < hdr_mtime
+
+
+def _run(cmd: list) -> None:
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"build failed: {' '.join(cmd)}\n{r.stdout}")
+    if r.stdout.strip():
+        sys.stderr.write(r.stdout)
+
+
+def build(force: bool = False, jobs: int = 8, arch: str = "gfx950", verbose: bool = True) -> dict:
+    os.makedirs(OUT, exist_ok=True)
+    os.makedirs(OBJ, exist_ok=True)
+    hdr = _newest_header()
+    hipcc = _hipcc()
+    kernel_srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
+    comm_srcs = sorted(glob.glob(os.path.join(CSRC, "comm", "*.cpp")))
+    hip_flags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={arch}", "-Wall",
+                 "-Wno-unused-function", "-munsafe-fp-atomics"]
+    jobs_list = []
+    kobjs = []
+    for s in kernel_srcs:
+        o = os.path.join(OBJ, os.path.basename(s) + ".o")
+        kobjs.append(o)
+        if force or _stale(s, o, hdr):
+            jobs_list.append([hipcc, *hip_flags, "-c", s, "-o", o])
+    cobjs = []
+    cxx = shutil.which("g++") or "g++"
+    for s in comm_srcs:
+        o = os.path.join(OBJ, os.path.basename(s) + ".o")
+        cobjs.append(o)
+        if force or _stale(s, o, hdr):
+            jobs_list.append([cxx, "-O2", "-std=c++17", "-fPIC", "-Wall", "-c", s, "-o", o])
+    if verbose and jobs_list:
+        print(f"[build] compiling {len(jobs_list)} translation unit(s) for {arch}", file=sys.stderr)
+    with cf.ThreadPoolExecutor(max(1, jobs)) as ex:
+        list(ex.map(_run, jobs_list))
+    out = {}
+    klib = os.path.join(OUT, "liblsa_kernels.so")
+    if kobjs and (force or not os.path.exists(klib) or
+                  os.path.getmtime(klib) < max(os.path.getmtime(o) for o in kobjs)):
+        _run([hipcc, "-shared", "-fPIC", f"--offload-arch={arch}", *kobjs, "-o", klib])
+    out["kernels"] = klib
+    clib = os.path.join(OUT, "liblsa_comm.so")
+    if cobjs and (force or not os.path.exists(clib) or
+                  os.path.getmtime(clib) < max(os.path.getmtime(o) for o in cobjs)):
+        _run([cxx, "-shared", "-fPIC", *cobjs, "-o", clib, "-lpthread"])
+    out["comm"] = clib
+    return out
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", "--jobs", type=int, default=min(8, os.cpu_count() or 4))
+    ap.add_argument("--arch", default=os.environ.get("PYTORCH_ROCM_ARCH", "gfx950"))
+    a = ap.parse_args()
+    res = build(a.force, a.jobs, a.arch)
+    for k, v in res.items():
+        print(f"{k}: {v}")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,245 @@
+// Attention over the static KV cache.
+//
+// The reference runs HF eager attention (matmul -> fp32 softmax -> matmul, GQA via
+// repeat_kv) on a DynamicCache grown by torch.cat every step (SURVEY.md §2.3 K6/K7,
+// /root/reference/utils/shard_loader.py:66-74). Here:
+//
+//  attn_split_kernel  flash-decoding: grid (nsplit, n_kv, rows). One workgroup streams one
+//                     contiguous chunk of a (slot, kv-head)'s keys ONCE for the whole GQA
+//                     group of query heads (no repeat_kv copies). K/V rows go straight to
+//                     VGPRs (16 B/lane, HD/8 lanes per key), scores and the online softmax
+//                     run in fp32 in the exp2 domain. Row m attends keys [0, kvlen(m)):
+//                     kvlen = pos+1 (causal; decode and prefill alike) unless an explicit
+//                     kv_len array is given (the reference's unmasked prefill, Q1).
+//                     The split count is fixed per launch (graph-capturable); the chunk is
+//                     derived on-device from the current length, so empty splits exit.
+//  attn_combine_kernel merges the per-split (o, lse) partials -> bf16 [rows][n_heads*HD].
+#include "common.h"
+
+namespace {
+
+constexpr int ATT_WAVES = 4;
+constexpr int ATT_THR = ATT_WAVES * LSA_WAVE;
+constexpr float NEG_BIG = -1e30f;
+
+template <int HD, int G>
+__global__ __launch_bounds__(ATT_THR) void attn_split_kernel(
+    const bf16_raw* __restrict__ q, int ldq, const bf16_raw* __restrict__ kc,
+    const bf16_raw* __restrict__ vc, const int* __restrict__ slot, const int* __restrict__ pos,
+    const int* __restrict__ kv_len, int n_heads, int n_kv, int t_max, float scale_log2,
+    int nsplit, int min_chunk, float* __restrict__ part_o, float* __restrict__ part_lse) {
+  constexpr int LPK = HD / 8;          // lanes per key row (8 bf16 = 16 B per lane)
+  constexpr int KPW = LSA_WAVE / LPK;  // keys per wave-instruction
+  constexpr int KPI = KPW * ATT_WAVES; // keys per workgroup iteration
+  constexpr int U = 4;                 // iterations in flight per wave
+
+  __shared__ float s_m[ATT_WAVES][G];
+  __shared__ float s_l[ATT_WAVES][G];
+  __shared__ float s_o[ATT_WAVES][G][HD];
+
+  const int split = blockIdx.x, kvh = blockIdx.y, row = blockIdx.z;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int grp = lane / LPK, li = lane % LPK;
+
+  int T = kv_len ? kv_len[row] : pos[row] + 1;
+  T = T > t_max ? t_max : T;  // never read past the static cache
+  int chunk = (T + nsplit - 1) / nsplit;
+  chunk = chunk < min_chunk ? min_chunk : chunk;
+  chunk = (chunk + KPI - 1) / KPI * KPI;
+  const int k0 = split * chunk;
+  const int k1 = min(T, k0 + chunk);
+  const size_t pbase = ((size_t)row * n_heads + (size_t)kvh * G) * nsplit + split;
+  if (k0 >= k1) {
+    if (tid < G) part_lse[pbase + (size_t)tid * nsplit] = -INFINITY;
+    return;
+  }
+
+  float qf[G][8];
+#pragma unroll
+  for (int r = 0; r < G; ++r) {
+    unpack8(ld16(q + (size_t)row * ldq + (size_t)(kvh * G + r) * HD + li * 8), qf[r]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) qf[r][j] *= scale_log2;
+  }
+
+  const size_t cbase = ((size_t)slot[row] * n_kv + kvh) * (size_t)t_max * HD;
+  const bf16_raw* kb = kc + cbase + li * 8;
+  const bf16_raw* vb = vc + cbase + li * 8;
+
+  float mx[G], l[G], o[G][8];
+#pragma unroll
+  for (int r = 0; r < G; ++r) {
+    mx[r] = NEG_BIG;
+    l[r] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[r][j] = 0.f;
+  }
+
+  // loop bound is wave-uniform (the 16-lane key groups of a wave shuffle only internally)
+  for (int base = k0 + w * KPW; base < k1; base += KPI * U) {
+    u32x4_t kr[U], vr[U];
+    bool valid[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int key = base + grp + u * KPI;
+      valid[u] = key < k1;
+      const int kk = valid[u] ? key : k0;
+      kr[u] = ld16(kb + (size_t)kk * HD);
+      vr[u] = ld16(vb + (size_t)kk * HD);
+    }
+    float s[G][U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float kf[8];
+      unpack8(kr[u], kf);
+#pragma unroll
+      for (int r = 0; r < G; ++r) {
+        float d = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d += qf[r][j] * kf[j];
+#pragma unroll
+        for (int off = LPK / 2; off > 0; off >>= 1) d += __shfl_xor(d, off, 64);
+        s[r][u] = valid[u] ? d : NEG_BIG;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < G; ++r) {
+      float bm = s[r][0];
+#pragma unroll
+      for (int u = 1; u < U; ++u) bm = fmaxf(bm, s[r][u]);
+      const float mn = fmaxf(mx[r], bm);
+      const float alpha = exp2f(mx[r] - mn);
+      mx[r] = mn;
+      l[r] *= alpha;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[r][j] *= alpha;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const float p = valid[u] ? exp2f(s[r][u] - mn) : 0.f;
+        l[r] += p;
+        float vf[8];
+        unpack8(vr[u], vf);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[r][j] += p * vf[j];
+      }
+    }
+  }
+
+  // merge the KPW key-groups of this wave (same li, different grp)
+#pragma unroll
+  for (int off = LPK; off < LSA_WAVE; off <<= 1) {
+#pragma unroll
+    for (int r = 0; r < G; ++r) {
+      const float mo = __shfl_xor(mx[r], off, 64);
+      const float lo = __shfl_xor(l[r], off, 64);
+      const float mn = fmaxf(mx[r], mo);
+      const float a = exp2f(mx[r] - mn), b = exp2f(mo - mn);
+      l[r] = l[r] * a + lo * b;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[r][j] = o[r][j] * a + __shfl_xor(o[r][j], off, 64) * b;
+      mx[r] = mn;
+    }
+  }
+  if (grp == 0) {
+#pragma unroll
+    for (int r = 0; r < G; ++r) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s_o[w][r][li * 8 + j] = o[r][j];
+      if (li == 0) {
+        s_m[w][r] = mx[r];
+        s_l[w][r] = l[r];
+      }
+    }
+  }
+  __syncthreads();
+  for (int e = tid; e < G * HD; e += ATT_THR) {
+    const int r = e / HD, d = e - r * HD;
+    float mm = s_m[0][r];
+#pragma unroll
+    for (int i = 1; i < ATT_WAVES; ++i) mm = fmaxf(mm, s_m[i][r]);
+    float ls = 0.f, os = 0.f;
+#pragma unroll
+    for (int i = 0; i < ATT_WAVES; ++i) {
+      const float a = exp2f(s_m[i][r] - mm);
+      ls += s_l[i][r] * a;
+      os += s_o[i][r][d] * a;
+    }
+    const size_t pi = pbase + (size_t)r * nsplit;
+    part_o[pi * HD + d] = os / ls;
+    if (d == 0) part_lse[pi] = mm + log2f(ls);
+  }
+}
+
+template <int HD>
+__global__ __launch_bounds__(HD) void attn_combine_kernel(const float* __restrict__ part_o,
+                                                          const float* __restrict__ part_lse,
+                                                          int n_heads, int nsplit,
+                                                          bf16_raw* __restrict__ out, int ldo) {
+  const int h = blockIdx.x, row = blockIdx.y, d = threadIdx.x;
+  const size_t pb = ((size_t)row * n_heads + h) * nsplit;
+  float mm = -INFINITY;
+  for (int s = 0; s < nsplit; ++s) mm = fmaxf(mm, part_lse[pb + s]);
+  float ws = 0.f, acc = 0.f;
+  for (int s = 0; s < nsplit; ++s) {
+    const float lse = part_lse[pb + s];
+    if (lse == -INFINITY) continue;
+    const float wgt = exp2f(lse - mm);
+    ws += wgt;
+    acc += wgt * part_o[(pb + s) * HD + d];
+  }
+  out[(size_t)row * ldo + (size_t)h * HD + d] = f2bf(acc / ws);
+}
+
+template <int HD, int G>
+int launch_split(const bf16_raw* q, int ldq, const bf16_raw* kc, const bf16_raw* vc, const int* slot,
+                 const int* pos, const int* kv_len, int rows, int n_heads, int n_kv, int t_max,
+                 float scale_log2, int nsplit, int min_chunk, float* po, float* pl, hipStream_t s) {
+  dim3 grid(nsplit, n_kv, rows);
+  attn_split_kernel<HD, G><<<grid, ATT_THR, 0, s>>>(q, ldq, kc, vc, slot, pos, kv_len, n_heads, n_kv,
+                                                     t_max, scale_log2, nsplit, min_chunk, po, pl);
+  LSA_CHECK_LAUNCH();
+  return LSA_OK;
+}
+
+template <int HD>
+int dispatch_g(int g, const bf16_raw* q, int ldq, const bf16_raw* kc, const bf16_raw* vc,
+               const int* slot, const int* pos, const int* kv_len, int rows, int n_heads, int n_kv,
+               int t_max, float sl2, int nsplit, int min_chunk, float* po, float* pl, hipStream_t s) {
+#define LSA_G(GG) \
+  case GG: return launch_split<HD, GG>(q, ldq, kc, vc, slot, pos, kv_len, rows, n_heads, n_kv, t_max, sl2, nsplit, min_chunk, po, pl, s);
+  switch (g) {
+    LSA_G(1) LSA_G(2) LSA_G(3) LSA_G(4) LSA_G(6) LSA_G(8)
+    default: return LSA_UNSUPPORTED;
+  }
+#undef LSA_G
+}
+
+}  // namespace
+
+extern "C" int lsa_attn_decode(const void* q, int ldq, const void* k_cache, const void* v_cache,
+                               const int* slot, const int* pos, const int* kv_len, int rows,
+                               int n_heads, int n_kv, int head_dim, int t_max, float scale,
+                               int nsplit, int min_chunk, float* part_o, float* part_lse,
+                               void* out, int ldo, hipStream_t stream) {
+  if (rows < 1 || n_heads % n_kv || nsplit < 1 || min_chunk < 1) return LSA_BAD_SHAPE;
+  const int g = n_heads / n_kv;
+  const float sl2 = scale * 1.4426950408889634f;
+  const bf16_raw* qq = static_cast<const bf16_raw*>(q);
+  const bf16_raw* kc = static_cast<const bf16_raw*>(k_cache);
+  const bf16_raw* vc = static_cast<const bf16_raw*>(v_cache);
+  int rc;
+  if (head_dim == 128)
+    rc = dispatch_g<128>(g, qq, ldq, kc, vc, slot, pos, kv_len, rows, n_heads, n_kv, t_max, sl2, nsplit, min_chunk, part_o, part_lse, stream);
+  else if (head_dim == 64)
+    rc = dispatch_g<64>(g, qq, ldq, kc, vc, slot, pos, kv_len, rows, n_heads, n_kv, t_max, sl2, nsplit, min_chunk, part_o, part_lse, stream);
+  else
+    return LSA_UNSUPPORTED;
+  if (rc != LSA_OK) return rc;
+  dim3 grid(n_heads, rows);
+  if (head_dim == 128)
+    attn_combine_kernel<128><<<grid, 128, 0, stream>>>(part_o, part_lse, n_heads, nsplit, static_cast<bf16_raw*>(out), ldo);
+  else
+    attn_combine_kernel<64><<<grid, 64, 0, stream>>>(part_o, part_lse, n_heads, nsplit, static_cast<bf16_raw*>(out), ldo);
+  LSA_CHECK_LAUNCH();
+  return LSA_OK;
+}

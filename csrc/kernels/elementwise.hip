@@ -1,0 +1,120 @@
+// Small bandwidth-bound kernels of the stage forward, all vectorised 16 B/lane
+// (cdna_hip_programming.md Guideline 13):
+//   lsa_embed        nn.Embedding row gather (reference node_worker.py:215,302)
+//   lsa_rmsnorm      standalone RMSNorm (prefill path; decode fuses it into the GEMV)
+//   lsa_argmax_finalize  decode the fused-argmax keys -> token ids, reset the keys, append to
+//                    the device-side history and advance the per-row positions. This keeps
+//                    the whole autoregressive step on the device (no .item() host sync per
+//                    token as in node_worker.py:287) so it can be captured in a hipGraph.
+#include "common.h"
+
+namespace {
+
+__global__ __launch_bounds__(256) void embed_kernel(const int* __restrict__ ids,
+                                                    const bf16_raw* __restrict__ table, int H,
+                                                    bf16_raw* __restrict__ out, int ldo) {
+  const int row = blockIdx.x;
+  const int id = ids[row];
+  const bf16_raw* src = table + (size_t)id * H;
+  bf16_raw* dst = out + (size_t)row * ldo;
+  for (int c = threadIdx.x; c < (H >> 3); c += blockDim.x) st16(dst + c * 8, ld16(src + c * 8));
+}
+
+__global__ __launch_bounds__(256) void rmsnorm_kernel(const bf16_raw* __restrict__ x, int ldx,
+                                                      const bf16_raw* __restrict__ w, int H,
+                                                      float eps, bf16_raw* __restrict__ out,
+                                                      int ldo) {
+  __shared__ float s_part[4];
+  const int row = blockIdx.x, tid = threadIdx.x;
+  const bf16_raw* xr = x + (size_t)row * ldx;
+  float s = 0.f;
+  for (int c = tid; c < (H >> 3); c += 256) {
+    float f[8];
+    unpack8(ld16(xr + c * 8), f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += f[j] * f[j];
+  }
+  s = wave_sum(s);
+  if ((tid & 63) == 0) s_part[tid >> 6] = s;
+  __syncthreads();
+  const float rs = rsqrtf((s_part[0] + s_part[1] + s_part[2] + s_part[3]) / (float)H + eps);
+  bf16_raw* orow = out + (size_t)row * ldo;
+  for (int c = tid; c < (H >> 3); c += 256) {
+    float f[8], g[8];
+    unpack8(ld16(xr + c * 8), f);
+    unpack8(ld16(w + c * 8), g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = f[j] * rs * g[j];
+    st16(orow + c * 8, pack8(f));
+  }
+}
+
+// One workgroup; rows <= 1024.
+__global__ void argmax_finalize_kernel(unsigned long long* __restrict__ keys, int rows,
+                                       int* __restrict__ tokens, int* __restrict__ pos,
+                                       int pos_inc, int* __restrict__ history, int hist_stride,
+                                       int hist_len, int* __restrict__ step_ctr) {
+  const int r = threadIdx.x;
+  int step = 0;
+  if (step_ctr) step = *step_ctr;
+  __syncthreads();
+  if (r < rows) {
+    const unsigned long long k = keys[r];
+    const int tok = (int)argmax_key_index(k);
+    keys[r] = 0ull;
+    tokens[r] = tok;
+    if (pos) pos[r] += pos_inc;
+    if (history && step < hist_len) history[(size_t)step * hist_stride + r] = tok;
+  }
+  if (r == 0 && step_ctr) *step_ctr = step + 1;
+}
+
+}  // namespace
+
+extern "C" int lsa_embed(const int* ids, int rows, const void* table, int H, void* out, int ldo,
+                         hipStream_t stream) {
+  if (rows < 1 || H % 8) return LSA_BAD_SHAPE;
+  embed_kernel<<<rows, 256, 0, stream>>>(ids, static_cast<const bf16_raw*>(table), H,
+                                        static_cast<bf16_raw*>(out), ldo);
+  LSA_CHECK_LAUNCH();
+  return LSA_OK;
+}
+
+extern "C" int lsa_rmsnorm(const void* x, int ldx, const void* w, int rows, int H, float eps,
+                           void* out, int ldo, hipStream_t stream) {
+  if (rows < 1 || H % 8) return LSA_BAD_SHAPE;
+  rmsnorm_kernel<<<rows, 256, 0, stream>>>(static_cast<const bf16_raw*>(x), ldx,
+                                          static_cast<const bf16_raw*>(w), H, eps,
+                                          static_cast<bf16_raw*>(out), ldo);
+  LSA_CHECK_LAUNCH();
+  return LSA_OK;
+}
+
+extern "C" int lsa_argmax_finalize(unsigned long long* keys, int rows, int* tokens, int* pos,
+                                   int pos_inc, int* history, int hist_stride, int hist_len,
+                                   int* step_ctr, hipStream_t stream) {
+  if (rows < 1 || rows > 1024) return LSA_BAD_SHAPE;
+  const int thr = ((rows + 63) / 64) * 64;
+  argmax_finalize_kernel<<<1, thr, 0, stream>>>(keys, rows, tokens, pos, pos_inc, history,
+                                               hist_stride, hist_len, step_ctr);
+  LSA_CHECK_LAUNCH();
+  return LSA_OK;
+}
+
+namespace {
+__global__ void pos_advance_kernel(int* __restrict__ pos, int rows, int inc) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < rows) pos[r] += inc;
+}
+}  // namespace
+
+// Device-side position counters of a pipeline stage (its KV length per row) - advanced inside
+// the captured decode graph, so replays never need host-side re-capture.
+extern "C" int lsa_pos_advance(int* pos, int rows, int inc, hipStream_t stream) {
+  if (rows < 1) return LSA_BAD_SHAPE;
+  pos_advance_kernel<<<(rows + 255) / 256, 256, 0, stream>>>(pos, rows, inc);
+  LSA_CHECK_LAUNCH();
+  return LSA_OK;
+}
+
+extern "C" int lsa_version() { return 1; }

@@ -1,0 +1,199 @@
+"""Model configuration for the Llama decoder family served by this engine.
+
+The reference reads hyper-parameters from the HF ``config.json`` stored inside the shard
+folder (``/root/reference/utils/node_worker.py:88`` -> ``LlamaConfig.from_pretrained``).
+We parse the same file ourselves (no transformers dependency on the hot path) and provide
+presets for the models the reference is configured with:
+
+* Llama-2-7B  (``/root/reference/utils/node_worker.py:564``, ``inference.py:11``)
+* Llama-3.2-3B-Instruct (``/root/reference/start_node.py:14``, 28 layers: ``node_profiler.py:1207``)
+* Llama-2-70B (BASELINE.json config 4)
+
+plus tiny configs used by the CPU test-suite.
+"""
+from __future__ import annotations
+
+import dataclasses
+import json
+import math
+import os
+from typing import Any, Optional
+
+
+@dataclasses.dataclass
+class LlamaConfig:
+    hidden_size: int = 4096
+    intermediate_size: int = 11008
+    num_hidden_layers: int = 32
+    num_attention_heads: int = 32
+    num_key_value_heads: int = 32
+    head_dim: int = 128
+    vocab_size: int = 32000
+    max_position_embeddings: int = 4096
+    rms_norm_eps: float = 1e-5
+    rope_theta: float = 10000.0
+    rope_scaling: Optional[dict] = None
+    tie_word_embeddings: bool = False
+    bos_token_id: int = 1
+    eos_token_id: Any = 2
+    model_type: str = "llama"
+    name: str = "llama"
+
+    # ------------------------------------------------------------------ derived
+    @property
+    def q_size(self) -> int:
+        return self.num_attention_heads * self.head_dim
+
+    @property
+    def kv_size(self) -> int:
+        return self.num_key_value_heads * self.head_dim
+
+    @property
+    def qkv_size(self) -> int:
+        return self.q_size + 2 * self.kv_size
+
+    @property
+    def gqa_group(self) -> int:
+        return self.num_attention_heads // self.num_key_value_heads
+
+    @property
+    def eos_ids(self) -> list:
+        e = self.eos_token_id
+        if e is None:
+            return []
+        return list(e) if isinstance(e, (list, tuple)) else [int(e)]
+
+    def layer_param_count(self) -> int:
+        H, I = self.hidden_size, self.intermediate_size
+        return H * self.qkv_size + self.q_size * H + 3 * H * I + 2 * H
+
+    def layer_bytes(self, elem_bytes: int = 2) -> int:
+        return self.layer_param_count() * elem_bytes
+
+    def kv_bytes_per_token_per_layer(self, elem_bytes: int = 2) -> int:
+        return 2 * self.kv_size * elem_bytes
+
+    def validate(self) -> None:
+        if self.num_attention_heads % self.num_key_value_heads:
+            raise ValueError("num_attention_heads must be a multiple of num_key_value_heads")
+        if self.head_dim % 16:
+            raise ValueError("head_dim must be a multiple of 16")
+
+    # ------------------------------------------------------------------ IO
+    @classmethod
+    def from_dict(cls, d: dict) -> "LlamaConfig":
+        fields = {f.name for f in dataclasses.fields(cls)}
+        kw = {k: v for k, v in d.items() if k in fields}
+        if "num_key_value_heads" not in d or d.get("num_key_value_heads") is None:
+            kw["num_key_value_heads"] = d.get("num_attention_heads", cls.num_attention_heads)
+        if "head_dim" not in d or d.get("head_dim") is None:
+            kw["head_dim"] = d.get("hidden_size", cls.hidden_size) // d.get(
+                "num_attention_heads", cls.num_attention_heads)
+        if "_name_or_path" in d and "name" not in d:
+            kw["name"] = os.path.basename(str(d["_name_or_path"]).rstrip("/")) or "llama"
+        cfg = cls(**kw)
+        cfg.validate()
+        return cfg
+
+    @classmethod
+    def from_pretrained(cls, path: str) -> "LlamaConfig":
+        """Same entry point name as HF's ``LlamaConfig.from_pretrained`` (reads ``config.json``)."""
+        p = os.path.join(path, "config.json") if os.path.isdir(path) else path
+        with open(p, "r") as f:
+            d = json.load(f)
+        if "name" not in d:
+            d["name"] = os.path.basename(os.path.dirname(os.path.abspath(p)))
+        return cls.from_dict(d)
+
+    def to_dict(self) -> dict:
+        d = dataclasses.asdict(self)
+        d["architectures"] = ["LlamaForCausalLM"]
+        d["torch_dtype"] = "bfloat16"
+        return d
+
+    def save_pretrained(self, path: str) -> None:
+        os.makedirs(path, exist_ok=True)
+        with open(os.path.join(path, "config.json"), "w") as f:
+            json.dump(self.to_dict(), f, indent=2)
+
+
+# ---------------------------------------------------------------------- presets
+def llama2_7b() -> LlamaConfig:
+    return LlamaConfig(name="Llama-2-7b-chat-hf")
+
+
+def llama2_13b() -> LlamaConfig:
+    return LlamaConfig(hidden_size=5120, intermediate_size=13824, num_hidden_layers=40,
+                       num_attention_heads=40, num_key_value_heads=40, name="Llama-2-13b-chat-hf")
+
+
+def llama2_70b() -> LlamaConfig:
+    return LlamaConfig(hidden_size=8192, intermediate_size=28672, num_hidden_layers=80,
+                       num_attention_heads=64, num_key_value_heads=8, name="Llama-2-70b-chat-hf")
+
+
+def llama32_3b() -> LlamaConfig:
+    return LlamaConfig(hidden_size=3072, intermediate_size=8192, num_hidden_layers=28,
+                       num_attention_heads=24, num_key_value_heads=8, head_dim=128,
+                       vocab_size=128256, max_position_embeddings=131072, rms_norm_eps=1e-5,
+                       rope_theta=500000.0,
+                       rope_scaling={"rope_type": "llama3", "factor": 32.0,
+                                     "low_freq_factor": 1.0, "high_freq_factor": 4.0,
+                                     "original_max_position_embeddings": 8192},
+                       tie_word_embeddings=True, bos_token_id=128000,
+                       eos_token_id=[128001, 128008, 128009], name="Llama-3___2-3B-Instruct")
+
+
+def tiny(layers: int = 4, hidden: int = 256, heads: int = 4, kv_heads: int = 2,
+         head_dim: int = 64, inter: int = 512, vocab: int = 512, llama3: bool = False) -> LlamaConfig:
+    """Small config for CPU tests (shapes respect every kernel's tiling constraints)."""
+    cfg = LlamaConfig(hidden_size=hidden, intermediate_size=inter, num_hidden_layers=layers,
+                      num_attention_heads=heads, num_key_value_heads=kv_heads, head_dim=head_dim,
+                      vocab_size=vocab, max_position_embeddings=2048, name="tiny-llama",
+                      bos_token_id=1, eos_token_id=2)
+    if llama3:
+        cfg.rope_theta = 500000.0
+        cfg.rope_scaling = {"rope_type": "llama3", "factor": 8.0, "low_freq_factor": 1.0,
+                            "high_freq_factor": 4.0, "original_max_position_embeddings": 256}
+    return cfg
+
+
+PRESETS = {
+    "llama2-7b": llama2_7b,
+    "llama2-13b": llama2_13b,
+    "llama2-70b": llama2_70b,
+    "llama3.2-3b": llama32_3b,
+    "tiny": tiny,
+}
+
+
+def get_preset(name: str) -> LlamaConfig:
+    key = name.lower().replace("_", "-")
+    if key not in PRESETS:
+        raise KeyError(f"unknown model preset {name!r}; known: {sorted(PRESETS)}")
+    return PRESETS[key]()
+
+
+def dtype_suffix(dtype) -> str:
+    """Shard-folder suffix: ``str(dtype).split('.')[-1]`` (reference ``model_sharder.py:24``)."""
+    return str(dtype).split(".")[-1]
+
+
+def ceil_div(a: int, b: int) -> int:
+    return -(-a // b)
+
+
+def round_up(a: int, b: int) -> int:
+    return ceil_div(a, b) * b
+
+
+def human_bytes(n: float) -> str:
+    for unit in ("B", "KiB", "MiB", "GiB", "TiB"):
+        if abs(n) < 1024 or unit == "TiB":
+            return f"{n:.2f} {unit}"
+        n /= 1024
+    return f"{n:.2f} TiB"
+
+
+__all__ = ["LlamaConfig", "llama2_7b", "llama2_13b", "llama2_70b", "llama32_3b", "tiny",
+           "get_preset", "dtype_suffix", "ceil_div", "round_up", "human_bytes", "math"]

@@ -1,0 +1,189 @@
+"""ctypes bindings for the in-tree HIP kernel library (``_native/liblsa_kernels.so``).
+
+Every wrapper takes torch tensors that live on the current ROCm device, checks the shapes the
+kernel's grid assumes (a bad shape must never reach the GPU: an out-of-bounds wave can reset
+the whole node), and launches on ``torch.cuda.current_stream()`` so that the launches are
+captured by ``torch.cuda.graph`` (hipGraph) like any other stream work.
+
+The library is loaded AFTER ``import torch`` so that its ``libamdhip64.so.7`` dependency
+resolves (by soname) to the HIP runtime torch already loaded: one runtime, shared streams.
+If the library is missing on a machine with a GPU we raise - there is no silent fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import torch
+
+NATIVE_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_native")
+KERNELS_SO = os.path.join(NATIVE_DIR, "liblsa_kernels.so")
+
+EPI_STORE, EPI_RESID, EPI_SWIGLU, EPI_QKV, EPI_ARGMAX = range(5)
+_STATUS = {0: "ok", 1: "bad shape", 2: "unsupported", 3: "launch failed"}
+
+
+class EpiArgs(ctypes.Structure):
+    _fields_ = [
+        ("out", ctypes.c_void_p), ("resid", ctypes.c_void_p), ("k_cache", ctypes.c_void_p),
+        ("v_cache", ctypes.c_void_p), ("slot", ctypes.c_void_p), ("pos", ctypes.c_void_p),
+        ("cos_t", ctypes.c_void_p), ("sin_t", ctypes.c_void_p), ("keys", ctypes.c_void_p),
+        ("ldo", ctypes.c_int), ("ldr", ctypes.c_int), ("n_heads", ctypes.c_int),
+        ("n_kv", ctypes.c_int), ("head_dim", ctypes.c_int), ("t_max", ctypes.c_int),
+        ("col_offset", ctypes.c_int), ("pad_", ctypes.c_int),
+    ]
+
+
+_lib = None
+
+
+def available() -> bool:
+    return os.path.exists(KERNELS_SO)
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(KERNELS_SO):
+        raise RuntimeError(
+            f"HIP kernel library not built: {KERNELS_SO} missing. Run `python csrc/build.py` "
+            "(or __graft_entry__.build()).")
+    L = ctypes.CDLL(KERNELS_SO, mode=ctypes.RTLD_GLOBAL)
+    vp, i, f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+    L.lsa_gemv.argtypes = [vp, i, vp, vp, i, i, i, vp, f, i, ctypes.POINTER(EpiArgs), i, vp]
+    L.lsa_gemm.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(EpiArgs), i, vp]
+    L.lsa_attn_decode.argtypes = [vp, i, vp, vp, vp, vp, vp, i, i, i, i, i, f, i, i, vp, vp, vp, i, vp]
+    L.lsa_embed.argtypes = [vp, i, vp, i, vp, i, vp]
+    L.lsa_rmsnorm.argtypes = [vp, i, vp, i, i, f, vp, i, vp]
+    L.lsa_argmax_finalize.argtypes = [vp, i, vp, vp, i, vp, i, i, vp, vp]
+    L.lsa_pos_advance.argtypes = [vp, i, i, vp]
+    for name in ("lsa_gemv", "lsa_gemm", "lsa_attn_decode", "lsa_embed", "lsa_rmsnorm",
+                 "lsa_argmax_finalize", "lsa_pos_advance", "lsa_version"):
+        getattr(L, name).restype = ctypes.c_int
+    _lib = L
+    return L
+
+
+def _p(t: Optional[torch.Tensor]):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"{what}: {_STATUS.get(rc, rc)}")
+
+
+def _req(cond: bool, msg: str) -> None:
+    if not cond:
+        raise ValueError(msg)
+
+
+def _is_bf16_cuda(*ts) -> bool:
+    return all(t is None or (t.is_cuda and t.dtype == torch.bfloat16) for t in ts)
+
+
+def make_epi(out=None, resid=None, k_cache=None, v_cache=None, slot=None, pos=None, cos=None,
+             sin=None, keys=None, ldo=0, ldr=0, n_heads=0, n_kv=0, head_dim=0, t_max=0,
+             col_offset=0) -> EpiArgs:
+    return EpiArgs(_p(out), _p(resid), _p(k_cache), _p(v_cache), _p(slot), _p(pos), _p(cos), _p(sin),
+                   _p(keys), ldo, ldr, n_heads, n_kv, head_dim, t_max, col_offset, 0)
+
+
+# ------------------------------------------------------------------------------ projections
+def gemv(x: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep: EpiArgs,
+         norm_w: Optional[torch.Tensor] = None, eps: float = 1e-5,
+         a_rows: Optional[torch.Tensor] = None, tn: int = 0) -> None:
+    """Decode projection, M <= 16 rows. ``wp`` is ``pack_b(W)``, W: [N, K]."""
+    from .packing import pick_tn
+    _req(1 <= M <= 16, f"gemv supports 1..16 rows, got {M}")
+    _req(_is_bf16_cuda(x, wp, norm_w), "gemv: bf16 cuda tensors required")
+    _req(wp.numel() == N * K and N % 16 == 0 and K % 32 == 0, "gemv: packed weight shape")
+    _req(x.dim() == 2 and x.shape[1] >= K and x.stride(1) == 1, "gemv: x must be [rows, >=K] row-major")
+    if a_rows is None:
+        _req(x.shape[0] >= M, "gemv: x has fewer rows than M")
+    else:
+        _req(a_rows.dtype == torch.int32 and a_rows.is_cuda and a_rows.numel() >= M, "gemv: a_rows")
+    if norm_w is not None:
+        _req(norm_w.numel() == K, "gemv: norm weight size")
+    if tn == 0:
+        tn = pick_tn(N // 16, need_even=(epi == EPI_SWIGLU))
+    rc = lib().lsa_gemv(_p(x), x.stride(0), _p(a_rows), _p(wp), M, N, K, _p(norm_w), float(eps), epi,
+                        ctypes.byref(ep), tn, _stream())
+    _check(rc, "lsa_gemv")
+
+
+def gemm(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep: EpiArgs,
+         tn: int = 2) -> None:
+    """Prefill projection (any M). N must be a multiple of 64*tn, K of 64."""
+    _req(_is_bf16_cuda(a, wp), "gemm: bf16 cuda tensors required")
+    _req(wp.numel() == N * K and K % 64 == 0, "gemm: packed weight shape")
+    _req(a.dim() == 2 and a.shape[0] >= M and a.shape[1] >= K and a.stride(1) == 1, "gemm: A shape")
+    if N % (64 * tn):
+        tn = 1
+    _req(N % (64 * tn) == 0, f"gemm: N={N} not a multiple of {64 * tn}")
+    _req(not (epi == EPI_SWIGLU and tn != 2), "gemm: SwiGLU needs N % 128 == 0")
+    rc = lib().lsa_gemm(_p(a), a.stride(0), _p(wp), M, N, K, epi, ctypes.byref(ep), tn, _stream())
+    _check(rc, "lsa_gemm")
+
+
+# ------------------------------------------------------------------------------ attention
+def attn(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, slot: torch.Tensor,
+         pos: torch.Tensor, rows: int, n_heads: int, n_kv: int, head_dim: int, nsplit: int,
+         part_o: torch.Tensor, part_lse: torch.Tensor, out: torch.Tensor,
+         kv_len: Optional[torch.Tensor] = None, min_chunk: int = 64,
+         scale: Optional[float] = None) -> None:
+    """Split-KV attention of ``rows`` query rows against the static cache + combine."""
+    _req(_is_bf16_cuda(q, k_cache, v_cache, out), "attn: bf16 cuda tensors")
+    _req(k_cache.dim() == 4 and k_cache.shape == v_cache.shape, "attn: cache [slots, n_kv, T, hd]")
+    _req(k_cache.shape[1] == n_kv and k_cache.shape[3] == head_dim, "attn: cache dims")
+    _req(q.shape[0] >= rows and q.shape[1] >= n_heads * head_dim, "attn: q shape")
+    _req(part_o.numel() >= rows * n_heads * nsplit * head_dim and part_lse.numel() >= rows * n_heads * nsplit,
+         "attn: workspace too small")
+    _req(part_o.dtype == torch.float32 and part_lse.dtype == torch.float32, "attn: fp32 workspace")
+    _req(slot.dtype == torch.int32 and pos.dtype == torch.int32, "attn: int32 slot/pos")
+    t_max = k_cache.shape[2]
+    sc = head_dim ** -0.5 if scale is None else scale
+    rc = lib().lsa_attn_decode(_p(q), q.stride(0), _p(k_cache), _p(v_cache), _p(slot), _p(pos), _p(kv_len),
+                               rows, n_heads, n_kv, head_dim, t_max, float(sc), nsplit, min_chunk,
+                               _p(part_o), _p(part_lse), _p(out), out.stride(0), _stream())
+    _check(rc, "lsa_attn_decode")
+
+
+# ------------------------------------------------------------------------------ elementwise
+def embed(ids: torch.Tensor, table: torch.Tensor, out: torch.Tensor, rows: Optional[int] = None) -> None:
+    rows = ids.numel() if rows is None else rows
+    _req(ids.dtype == torch.int32 and ids.is_cuda, "embed: int32 ids")
+    _req(_is_bf16_cuda(table, out) and out.shape[1] >= table.shape[1], "embed: shapes")
+    rc = lib().lsa_embed(_p(ids), rows, _p(table), table.shape[1], _p(out), out.stride(0), _stream())
+    _check(rc, "lsa_embed")
+
+
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, rows: int, eps: float) -> None:
+    H = w.numel()
+    _req(_is_bf16_cuda(x, w, out), "rmsnorm: bf16 cuda tensors")
+    rc = lib().lsa_rmsnorm(_p(x), x.stride(0), _p(w), rows, H, float(eps), _p(out), out.stride(0), _stream())
+    _check(rc, "lsa_rmsnorm")
+
+
+def argmax_finalize(keys: torch.Tensor, rows: int, tokens: torch.Tensor, pos: Optional[torch.Tensor] = None,
+                    pos_inc: int = 1, history: Optional[torch.Tensor] = None,
+                    step_ctr: Optional[torch.Tensor] = None) -> None:
+    _req(keys.dtype == torch.int64 and tokens.dtype == torch.int32, "argmax_finalize: dtypes")
+    hs = history.stride(0) if history is not None else 0
+    hl = history.shape[0] if history is not None else 0
+    if history is not None:
+        _req(history.dtype == torch.int32 and history.shape[1] >= rows, "argmax_finalize: history shape")
+    rc = lib().lsa_argmax_finalize(_p(keys), rows, _p(tokens), _p(pos), pos_inc, _p(history), hs, hl,
+                                   _p(step_ctr), _stream())
+    _check(rc, "lsa_argmax_finalize")
+
+
+def pos_advance(pos: torch.Tensor, rows: int, inc: int = 1) -> None:
+    rc = lib().lsa_pos_advance(_p(pos), rows, inc, _stream())
+    _check(rc, "lsa_pos_advance")

@@ -1,0 +1,283 @@
+"""Micro-batched pipeline-parallel decode over RCCL (one process per GPU).
+
+The reference chain passes ONE token around the ring at a time: stage i receives a pickled
+``next_state_info`` over ZMQ, runs its layers, pushes the result on (SURVEY.md §3.2,
+``/root/reference/utils/node_worker.py:493-559``), so at most 1/N of the devices ever work.
+
+Here each rank is one stage (a contiguous layer range from the master scheduler, resident on
+its own MI355X). M micro-batches of B sequences are in flight; for every (step, micro-batch)
+a rank:
+
+    irecv(hidden | token ids)  ->  stream-wait  ->  replay the micro-batch's hipGraph
+    (layers [+ embed] [+ final-norm/lm_head/argmax])  ->  isend(hidden | token ids)
+
+The RCCL p2p ops run on the NCCL stream and are ordered against the compute stream by
+events (no host synchronisation per token); the host only throttles its run-ahead to two
+steps. Hidden states go rank r -> r+1 over xGMI, token ids go last -> 0 (the ring back-edge,
+``receive_next_token`` with the embedding co-located on the first stage).
+"""
+from __future__ import annotations
+
+import os
+import time
+from typing import Optional
+
+import torch
+
+from ..config import get_preset
+from ..runtime.engine import DecodeGraph, RandomSource, StageEngine
+from .scheduler import plan_stages
+
+
+def _percentile(xs, q):
+    if not xs:
+        return float("nan")
+    s = sorted(xs)
+    k = (len(s) - 1) * q
+    lo, hi = int(k), min(int(k) + 1, len(s) - 1)
+    return s[lo] + (s[hi] - s[lo]) * (k - lo)
+
+
+class PipelineStage:
+    """One rank's share of a pipelined decode: engine + per-micro-batch graphs and buffers."""
+
+    def __init__(self, cfg, rank: int, world: int, start: int, end: int, device, batch: int,
+                 microbatches: int, max_seq: int, source, use_graph: bool = True,
+                 max_prefill_rows: int = 2048):
+        self.cfg, self.rank, self.world = cfg, rank, world
+        self.first, self.last = rank == 0, rank == world - 1
+        self.B, self.M = batch, microbatches
+        self.device = torch.device(device)
+        self.use_graph = use_graph
+        self.eng = StageEngine(cfg, start, end, device, torch.bfloat16, has_embed=self.first,
+                               has_head=self.last, source=source, max_slots=batch * microbatches,
+                               max_seq=max_seq, max_prefill_rows=max(max_prefill_rows, batch))
+        H = cfg.hidden_size
+        self.h_out = [torch.zeros((batch, H), dtype=torch.bfloat16, device=self.device) for _ in range(microbatches)]
+        self.tok_out = [torch.zeros(batch, dtype=torch.int32, device=self.device) for _ in range(microbatches)]
+        self.graphs: list = []
+        self.send_works: dict = {}
+        self.tokens_ready = [True] * microbatches  # stage 0: next-step token ids are in place
+
+    # ---------------------------------------------------------------- p2p helpers
+    def _send(self, t: torch.Tensor, dst: int, key):
+        import torch.distributed as dist
+        w = dist.isend(t, dst)
+        self.send_works[key] = w
+
+    def _wait_send(self, key):
+        w = self.send_works.pop(key, None)
+        if w is not None:
+            w.wait()
+
+    @staticmethod
+    def _recv(t: torch.Tensor, src: int):
+        import torch.distributed as dist
+        dist.irecv(t, src).wait()
+
+    # ---------------------------------------------------------------- prefill
+    def slots(self, mb: int) -> list:
+        return list(range(mb * self.B, (mb + 1) * self.B))
+
+    def prefill(self, prompts: Optional[torch.Tensor], prompt_len: int) -> Optional[list]:
+        """Prefill every micro-batch through the pipeline. ``prompts``: [M, B, P] int (rank 0).
+        Returns (on rank 0) the first generated token per micro-batch ([B] int32 tensors)."""
+        eng, B, P, H = self.eng, self.B, prompt_len, self.cfg.hidden_size
+        firsts = []
+        for mb in range(self.M):
+            sl = self.slots(mb)
+            slot, pos = eng.prefill_rows(sl, [P] * B)
+            if self.first:
+                h = eng.embed(prompts[mb].reshape(-1).to(self.device))
+            else:
+                h = torch.empty((B * P, H), dtype=torch.bfloat16, device=self.device)
+                self._recv(h, self.rank - 1)
+            h = eng.forward(h, slot, pos)
+            eng.advance(sl, [P] * B)
+            if self.last:
+                tok = eng.head(h, [i * P + P - 1 for i in range(B)]).to(torch.int32)
+                if self.world > 1:
+                    self._send(tok, 0, ("pf", mb))
+                    self._wait_send(("pf", mb))
+                else:
+                    firsts.append(tok)
+            else:
+                hs = h.clone()
+                self._send(hs, self.rank + 1, ("pf", mb))
+                self._wait_send(("pf", mb))
+            if self.first and self.world > 1:
+                tok = torch.empty(B, dtype=torch.int32, device=self.device)
+                self._recv(tok, self.world - 1)
+                firsts.append(tok)
+        return firsts if self.first else None
+
+    # ---------------------------------------------------------------- decode
+    def build_graphs(self, first_tokens: Optional[list], history_len: int) -> None:
+        mode = "full" if self.world == 1 else ("first" if self.first else ("last" if self.last else "mid"))
+        self.mode = mode
+        self.graphs = []
+        for mb in range(self.M):
+            g = DecodeGraph(self.eng, self.B, mode, slots=self.slots(mb),
+                            history_len=history_len if self.last else 0)
+            if first_tokens is not None and mode in ("full", "first"):
+                g.tokens.copy_(first_tokens[mb])
+            if self.use_graph:
+                g.capture()
+            self.graphs.append(g)
+
+    def _run_mb(self, g: DecodeGraph):
+        if self.use_graph:
+            g.replay()
+        else:
+            g._body()
+
+    def step(self, s: int, events: Optional[list] = None) -> None:
+        """One decode step for every micro-batch (the host never blocks on the GPU here)."""
+        for mb, g in enumerate(self.graphs):
+            if self.world > 1:
+                if self.first:
+                    if not self.tokens_ready[mb]:
+                        self._recv(g.tokens, self.world - 1)
+                    self.tokens_ready[mb] = False
+                else:
+                    self._recv(g.h_in, self.rank - 1)
+            self._run_mb(g)
+            if events is not None:
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record()
+                events.append((s, mb, ev))
+            if self.world > 1:
+                if self.last:
+                    # the next replay rewrites g.tokens: send from a private copy, reused only
+                    # after the previous send of this micro-batch completed
+                    self._wait_send(("tok", mb))
+                    self.tok_out[mb].copy_(g.tokens)
+                    self._send(self.tok_out[mb], 0, ("tok", mb))
+                else:
+                    self._wait_send(("h", mb))
+                    self.h_out[mb].copy_(g.out_hidden)
+                    self._send(self.h_out[mb], self.rank + 1, ("h", mb))
+
+    def drain(self):
+        """End of a phase: stage 0 collects the token ids the last stage produced in the final
+        step (the ring back-edge), then every outstanding send is waited for."""
+        if self.world > 1 and self.first:
+            for mb, g in enumerate(self.graphs):
+                if not self.tokens_ready[mb]:
+                    self._recv(g.tokens, self.world - 1)
+                    self.tokens_ready[mb] = True
+        for k in list(self.send_works):
+            self._wait_send(k)
+
+
+def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int = 64, warmup: int = 8,
+                         batch: int = 16, prompt_len: int = 128, max_seq: int = 1024,
+                         microbatches: int = 0, seed: int = 0, use_graph: bool = True,
+                         verbose: bool = True) -> Optional[dict]:
+    cfg = get_preset(model)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if n_gpus != world:
+        raise ValueError(f"n_gpus={n_gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+    M = microbatches or world
+    plan = plan_stages(cfg, world, kv_tokens=max_seq * batch * M)
+    st = plan.stages[rank]
+    need = prompt_len + warmup + steps + 1
+    if need > max_seq:
+        raise ValueError(f"prompt+warmup+steps ({need}) exceeds max_seq {max_seq}")
+    if verbose and rank == 0:
+        print(f"[bench] {cfg.name} pp{world} plan: {plan.summary()}", flush=True)
+    t0 = time.perf_counter()
+    stage = PipelineStage(cfg, rank, world, st.start, st.end, dev, batch, M, max_seq,
+                          RandomSource(cfg, seed), use_graph=use_graph,
+                          max_prefill_rows=batch * prompt_len)
+    torch.cuda.synchronize()
+    load_s = time.perf_counter() - t0
+    if dist:
+        dist.barrier()
+
+    prompts = None
+    if stage.first:
+        g = torch.Generator().manual_seed(seed + 1)
+        prompts = torch.randint(3, cfg.vocab_size, (M, batch, prompt_len), generator=g, dtype=torch.int32)
+    torch.cuda.synchronize()
+    tp0 = time.perf_counter()
+    firsts = stage.prefill(prompts, prompt_len)
+    torch.cuda.synchronize()
+    ttft_ms = (time.perf_counter() - tp0) * 1e3 / M  # per micro-batch prefill through the pipeline
+    stage.build_graphs(firsts, history_len=warmup + steps)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+
+    for s in range(warmup):
+        stage.step(s)
+    stage.drain()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    events: list = []
+    t_start = time.perf_counter()
+    for s in range(steps):
+        stage.step(warmup + s, events if stage.last else None)
+    stage.drain()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+
+    # per-token latency of each sequence = time between its consecutive tokens (last stage)
+    tpot = []
+    if stage.last:
+        by_mb: dict = {}
+        for s, mb, ev in events:
+            by_mb.setdefault(mb, []).append(ev)
+        for evs in by_mb.values():
+            for a, b in zip(evs, evs[1:]):
+                tpot.append(a.elapsed_time(b))
+    stats = torch.tensor([elapsed, ttft_ms, _percentile(tpot, 0.5) if tpot else 0.0,
+                          _percentile(tpot, 0.9) if tpot else 0.0, load_s], dtype=torch.float64, device=dev)
+    if dist:
+        gathered = [torch.zeros_like(stats) for _ in range(world)]
+        dist.all_gather(gathered, stats)
+        allst = torch.stack(gathered).cpu()
+        elapsed = float(allst[:, 0].max())
+        ttft_ms = float(allst[0, 1])
+        p50, p90 = float(allst[world - 1, 2]), float(allst[world - 1, 3])
+        load_s = float(allst[:, 4].max())
+    else:
+        p50, p90 = float(stats[2]), float(stats[3])
+    tokens = steps * M * batch
+    res = {
+        "tok_s": tokens / elapsed,
+        "ms_per_step": elapsed * 1e3 / steps,
+        "p50_tpot_ms": p50,
+        "p90_tpot_ms": p90,
+        "ttft_ms": ttft_ms,
+        "global_batch": M * batch,
+        "microbatches": M,
+        "model_name": "Llama-2-7B" if model == "llama2-7b" else cfg.name,
+        "load_s": load_s,
+        "plan": plan.ranges(),
+    }
+    if stage.last and verbose:
+        hist = stage.graphs[0].history[:8, :4].cpu().tolist() if stage.graphs[0].history is not None else []
+        print(f"[bench] rank {rank} sample tokens (step x seq): {hist}", flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank != 0:
+        return None
+    if verbose:
+        print(f"[bench] load {load_s:.1f}s  ttft/mb {ttft_ms:.1f}ms  step {res['ms_per_step']:.3f}ms  "
+              f"p50 tpot {p50:.3f}ms  {res['tok_s']:.1f} tok/s", flush=True)
+    return res

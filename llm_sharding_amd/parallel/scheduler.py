@@ -1,0 +1,174 @@
+"""Master-side placement scheduler.
+
+The reference README describes a scheduling algorithm on the master node that calls
+``ConfigSender`` (``/root/reference/README.md:7-8``) but the repo ships none - placement is
+hand-written in ``send_config.py:5-44``. Its profiler produces the inputs such a scheduler
+needs: per-token compute capability ``c_k``, max layers per device, cold-start latency
+(``utils/node_profiler.py:46-62,368-476,1138-1172``).
+
+``plan_stages`` implements it: split the ``L`` decoder layers into contiguous ranges, one per
+device in chain order, minimising the bottleneck stage time
+
+    t(stage) = sum(layer_cost) * speed_factor(device) + extras (embedding / lm_head)
+
+subject to a per-device memory cap (weights + KV cache + workspace), by exact dynamic
+programming over (layer, stage). Default costs are the bytes streamed per decode token
+(batch-1 decode is HBM-bound on MI355X), which is what the profiler's ``c_k`` measures.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+from ..config import LlamaConfig
+
+
+@dataclass
+class DeviceSpec:
+    name: str = "mi355x"
+    mem_bytes: float = 288e9          # HBM3E per MI355X
+    reserve_bytes: float = 8e9        # runtime / workspace headroom
+    speed: float = 1.0                # relative time multiplier (profiled c_k ratio)
+    host: str = "127.0.0.1"
+    config_port: int = 40700
+    data_port: int = 40800
+
+
+@dataclass
+class StagePlan:
+    index: int
+    start: int
+    end: int
+    device: DeviceSpec
+    has_embed: bool
+    has_head: bool
+    est_time: float
+    weight_bytes: float
+    kv_bytes: float
+
+    @property
+    def n_layers(self) -> int:
+        return self.end - self.start
+
+
+@dataclass
+class Plan:
+    stages: List[StagePlan] = field(default_factory=list)
+
+    @property
+    def bottleneck(self) -> float:
+        return max(s.est_time for s in self.stages)
+
+    def ranges(self) -> list:
+        return [(s.start, s.end) for s in self.stages]
+
+    def summary(self) -> str:
+        return " | ".join(f"s{s.index}[{s.start},{s.end}){'E' if s.has_embed else ''}"
+                          f"{'H' if s.has_head else ''} {s.est_time:.3g}" for s in self.stages)
+
+
+def default_costs(cfg: LlamaConfig, elem_bytes: int = 2) -> tuple:
+    layer = [float(cfg.layer_bytes(elem_bytes))] * cfg.num_hidden_layers
+    head = float((cfg.vocab_size * cfg.hidden_size + cfg.hidden_size) * elem_bytes)
+    embed = float(cfg.hidden_size * elem_bytes)  # one row gathered per token
+    return layer, embed, head
+
+
+def plan_stages(cfg: LlamaConfig, devices: Sequence[DeviceSpec] | int, *,
+                layer_costs: Optional[Sequence[float]] = None, embed_cost: Optional[float] = None,
+                head_cost: Optional[float] = None, kv_tokens: int = 0, elem_bytes: int = 2,
+                min_layers: int = 1) -> Plan:
+    """Exact min-max contiguous partition. ``devices`` is a list (chain order) or a count."""
+    if isinstance(devices, int):
+        devices = [DeviceSpec() for _ in range(devices)]
+    n, L = len(devices), cfg.num_hidden_layers
+    if n < 1 or n * min_layers > L:
+        raise ValueError(f"cannot place {L} layers on {n} stages (min {min_layers} each)")
+    lc, ec, hc = default_costs(cfg, elem_bytes)
+    lc = list(layer_costs) if layer_costs is not None else lc
+    ec = ec if embed_cost is None else embed_cost
+    hc = hc if head_cost is None else head_cost
+    lbytes = float(cfg.layer_bytes(elem_bytes))
+    kv_per_layer = float(cfg.kv_bytes_per_token_per_layer(elem_bytes)) * kv_tokens
+    emb_bytes = float(cfg.vocab_size * cfg.hidden_size * elem_bytes)
+    head_bytes = emb_bytes if not cfg.tie_word_embeddings else 0.0
+
+    pre = [0.0]
+    for c in lc:
+        pre.append(pre[-1] + c)
+
+    def stage_cost(k: int, a: int, b: int) -> float:
+        t = pre[b] - pre[a]
+        if k == 0:
+            t += ec
+        if k == n - 1:
+            t += hc
+        return t * devices[k].speed
+
+    def stage_mem(k: int, a: int, b: int) -> float:
+        m = (b - a) * (lbytes + kv_per_layer)
+        if k == 0:
+            m += emb_bytes
+        if k == n - 1:
+            m += head_bytes + cfg.hidden_size * elem_bytes
+        return m
+
+    def fits(k: int, a: int, b: int) -> bool:
+        d = devices[k]
+        return stage_mem(k, a, b) <= d.mem_bytes - d.reserve_bytes
+
+    INF = float("inf")
+    # best[k][i] = min bottleneck placing layers [0, i) on stages 0..k-1 (stage k-1 ends at i)
+    best = [[INF] * (L + 1) for _ in range(n + 1)]
+    arg = [[-1] * (L + 1) for _ in range(n + 1)]
+    best[0][0] = 0.0
+    for k in range(1, n + 1):
+        for i in range(k * min_layers, L - (n - k) * min_layers + 1):
+            for j in range((k - 1) * min_layers, i - min_layers + 1):
+                if best[k - 1][j] == INF or not fits(k - 1, j, i):
+                    continue
+                v = max(best[k - 1][j], stage_cost(k - 1, j, i))
+                if v < best[k][i] - 1e-9:
+                    best[k][i], arg[k][i] = v, j
+    if best[n][L] == INF:
+        raise ValueError("model does not fit on the given devices")
+    cuts = [L]
+    i = L
+    for k in range(n, 0, -1):
+        i = arg[k][i]
+        cuts.append(i)
+    cuts = cuts[::-1]
+    plan = Plan()
+    for k in range(n):
+        a, b = cuts[k], cuts[k + 1]
+        plan.stages.append(StagePlan(k, a, b, devices[k], k == 0, k == n - 1, stage_cost(k, a, b),
+                                     stage_mem(k, a, b) - (b - a) * kv_per_layer, (b - a) * kv_per_layer))
+    return plan
+
+
+def even_split(n_layers: int, n_stages: int) -> list:
+    base, extra = divmod(n_layers, n_stages)
+    out, s = [], 0
+    for k in range(n_stages):
+        e = s + base + (1 if k < extra else 0)
+        out.append((s, e))
+        s = e
+    return out
+
+
+def build_chain_configs(plan: Plan, ingress_stage: int = 0) -> list:
+    """ConfigSender payloads (reference schema, config_sender.py:33-40) for a ring chain."""
+    n = len(plan.stages)
+    out = []
+    for k, st in enumerate(plan.stages):
+        nxt = plan.stages[(k + 1) % n]
+        first = plan.stages[0]
+        out.append({
+            "src_addr": f"tcp://*:{st.device.data_port}",
+            "dst_addr": f"tcp://{nxt.device.host}:{nxt.device.data_port}",
+            "can_receive_user_request": k == ingress_stage,
+            "first_node_addr": f"tcp://{first.device.host}:{first.device.data_port}" if k == ingress_stage else "",
+            "shards_start": st.start,
+            "shards_end": st.end,
+        })
+    return out

@@ -1,0 +1,490 @@
+"""StageEngine: one pipeline stage (layers ``[start, end)``) resident on one device.
+
+This is the MI355X-native replacement for the reference's per-stage forward
+(``NodeWorker.pass_through_shard`` -> ``LlamaShardPart.forward`` -> HF ``LlamaDecoderLayer``,
+``/root/reference/utils/node_worker.py:226-272``, ``utils/shard_loader.py:57-78``):
+
+* weights are loaded once (reference ``.pth`` shard files, or deterministic random init on
+  the device) and **pre-packed** into the MFMA fragment layout, with q/k/v and gate/up fused;
+* the KV cache is a **static** preallocated ``[slots, n_kv, max_seq, head_dim]`` tensor per
+  layer (no ``DynamicCache`` ``torch.cat`` growth), written in place by the QKV epilogue;
+* a row-batch of tokens (any mix of sequences: row r -> cache ``slot[r]`` at position
+  ``pos[r]``) runs through 5 fused HIP launches per layer for decode
+  (QKV+norm+RoPE+KV-append, split-KV attention(+combine), o-proj+residual,
+  gate/up+norm+SwiGLU, down+residual) or the MFMA GEMM path for prefill;
+* the last stage runs final-norm + lm_head + greedy argmax fused, on the device;
+* ``DecodeGraph`` captures a whole decode step into a hipGraph (device-side position
+  counters, so one capture serves every step).
+
+On a CPU device the same engine runs plain torch ops on unpacked weights (the
+"plumbing" configuration of BASELINE.json config 1); it is not used on the GPU.
+"""
+from __future__ import annotations
+
+import math
+import os
+from dataclasses import dataclass
+from typing import Callable, Optional
+
+import torch
+import torch.nn.functional as F
+
+from ..config import LlamaConfig, ceil_div
+from ..models import weights as W
+from ..models.rope import rope_table
+from ..ops import packing
+
+
+# ---------------------------------------------------------------------------- weight sources
+class WeightSource:
+    """Where a stage's weights come from."""
+
+    def layer(self, i: int, device, dtype) -> dict:
+        raise NotImplementedError
+
+    def embedding(self, device, dtype) -> torch.Tensor:
+        raise NotImplementedError
+
+    def final_norm(self, device, dtype) -> torch.Tensor:
+        raise NotImplementedError
+
+    def lm_head(self, device, dtype) -> torch.Tensor:
+        raise NotImplementedError
+
+
+class ShardFolderSource(WeightSource):
+    """Reference on-disk format (``block_{i}.pth`` ...), read with ``weights_only=True``."""
+
+    def __init__(self, shards_path: str, cfg: Optional[LlamaConfig] = None):
+        self.path = shards_path
+        self.cfg = cfg or LlamaConfig.from_pretrained(shards_path)
+
+    def layer(self, i, device, dtype):
+        return W.load_block(self.path, i, device, dtype)
+
+    def embedding(self, device, dtype):
+        return W.load_single(self.path, "embedding.pth", device, dtype)
+
+    def final_norm(self, device, dtype):
+        return W.load_single(self.path, "final_norm.pth", device, dtype)
+
+    def lm_head(self, device, dtype):
+        return W.load_lm_head(self.path, self.cfg, device, dtype)
+
+
+class RandomSource(WeightSource):
+    """Deterministic random init generated directly on the target device (no disk)."""
+
+    def __init__(self, cfg: LlamaConfig, seed: int = 0):
+        self.cfg, self.seed = cfg, seed
+
+    def layer(self, i, device, dtype):
+        return W.random_layer(self.cfg, i, dtype, device, self.seed)
+
+    def embedding(self, device, dtype):
+        return W.random_embedding(self.cfg, dtype, device, self.seed)
+
+    def final_norm(self, device, dtype):
+        return W.random_final_norm(self.cfg, dtype, device, self.seed)
+
+    def lm_head(self, device, dtype):
+        return W.random_lm_head(self.cfg, dtype, device, self.seed)
+
+
+@dataclass
+class LayerWeights:
+    qkv: torch.Tensor      # packed (GPU) or fused-unpacked (CPU) [qkv, H]
+    o: torch.Tensor
+    gate_up: torch.Tensor
+    down: torch.Tensor
+    ln_in: torch.Tensor
+    ln_post: torch.Tensor
+    raw: Optional[dict] = None  # CPU path keeps the reference state dict
+
+
+def _is_gpu(device: torch.device) -> bool:
+    return device.type == "cuda"
+
+
+class StageEngine:
+    DECODE_MAX_ROWS = 64  # rows handled by the weight-streaming GEMV path
+
+    def __init__(self, cfg: LlamaConfig, start: int, end: int, device="cpu",
+                 dtype=torch.bfloat16, *, has_embed: bool = False, has_head: bool = False,
+                 source: Optional[WeightSource] = None, max_slots: int = 1, max_seq: int = 2048,
+                 max_prefill_rows: int = 2048, causal: bool = True, load: bool = True,
+                 verbose: bool = False):
+        if not (0 <= start < end <= cfg.num_hidden_layers):
+            raise ValueError(f"[ERROR] invalid layer range [{start}, {end})")
+        self.cfg = cfg
+        self.start, self.end = start, end
+        self.n_layers = end - start
+        self.device = torch.device(device)
+        self.gpu = _is_gpu(self.device)
+        if self.gpu and dtype != torch.bfloat16:
+            raise ValueError("the HIP path computes in bfloat16 (pass dtype=torch.bfloat16)")
+        self.dtype = dtype
+        self.has_embed, self.has_head = has_embed, has_head
+        self.source = source
+        self.max_slots = int(max_slots)
+        self.max_seq = int(min(max_seq, cfg.max_position_embeddings))
+        self.max_prefill_rows = int(max_prefill_rows)
+        self.causal = causal
+        self.verbose = verbose
+        self.layers: list = []
+        self.embed_w = self.final_norm = self.lm_head = None
+        self.k_cache: list = []
+        self.v_cache: list = []
+        self.seq_len = [0] * self.max_slots  # host-side KV length per slot
+        self._graphs: dict = {}
+        if self.gpu:
+            from ..ops import hip as _hip  # noqa: F401  (fail loudly if the .so is missing)
+            _hip.lib()
+        if load:
+            self.load()
+
+    # ------------------------------------------------------------------------- loading
+    def _log(self, msg: str) -> None:
+        if self.verbose:
+            print(msg, flush=True)
+
+    def load(self) -> None:
+        cfg, dev, dt = self.cfg, self.device, self.dtype
+        src = self.source
+        if src is None:
+            raise ValueError("StageEngine needs a WeightSource")
+        self.layers = []
+        for i in range(self.start, self.end):
+            self._log(f"[INFO] loading hidden layer {i}")
+            lw = src.layer(i, dev, dt)
+            self.layers.append(self._prepare_layer(lw))
+            del lw
+        if self.has_embed:
+            self._log("[INFO] loading embedding layer...")
+            self.embed_w = src.embedding(dev, dt).contiguous()
+        if self.has_head:
+            self._log("[INFO] loading final norm / lm_head...")
+            self.final_norm = src.final_norm(dev, dt).contiguous()
+            lm = src.lm_head(dev, dt)
+            self.lm_head = packing.pack_b(lm) if self.gpu else lm.contiguous()
+            del lm
+        self._alloc_runtime()
+
+    def _prepare_layer(self, lw: dict) -> LayerWeights:
+        cfg = self.cfg
+        qkv = packing.fuse_qkv(lw["self_attn.q_proj.weight"], lw["self_attn.k_proj.weight"],
+                               lw["self_attn.v_proj.weight"], cfg.num_attention_heads,
+                               cfg.num_key_value_heads, cfg.head_dim)
+        gu = packing.fuse_gate_up(lw["mlp.gate_proj.weight"], lw["mlp.up_proj.weight"])
+        if self.gpu:
+            return LayerWeights(packing.pack_b(qkv), packing.pack_b(lw["self_attn.o_proj.weight"]),
+                                packing.pack_b(gu), packing.pack_b(lw["mlp.down_proj.weight"]),
+                                lw["input_layernorm.weight"].contiguous(),
+                                lw["post_attention_layernorm.weight"].contiguous())
+        return LayerWeights(None, None, None, None, lw["input_layernorm.weight"],
+                            lw["post_attention_layernorm.weight"], raw=lw)
+
+    def _alloc_runtime(self) -> None:
+        cfg, dev = self.cfg, self.device
+        nkv, hd = cfg.num_key_value_heads, cfg.head_dim
+        shape = (self.max_slots, nkv, self.max_seq, hd)
+        self.k_cache = [torch.zeros(shape, dtype=self.dtype, device=dev) for _ in range(self.n_layers)]
+        self.v_cache = [torch.zeros(shape, dtype=self.dtype, device=dev) for _ in range(self.n_layers)]
+        self.cos, self.sin = rope_table(cfg, self.max_seq, dev)
+        R = max(self.max_prefill_rows, self.DECODE_MAX_ROWS)
+        H, I = cfg.hidden_size, cfg.intermediate_size
+        if self.gpu:
+            bf = torch.bfloat16
+            self.buf_h = torch.zeros((R, H), dtype=bf, device=dev)
+            self.buf_xn = torch.zeros((R, H), dtype=bf, device=dev)
+            self.buf_q = torch.zeros((R, cfg.q_size), dtype=bf, device=dev)
+            self.buf_attn = torch.zeros((R, cfg.q_size), dtype=bf, device=dev)
+            self.buf_act = torch.zeros((R, I), dtype=bf, device=dev)
+            self.decode_nsplit = int(min(16, max(1, ceil_div(self.max_seq, 256))))
+            ws_rows = max(self.DECODE_MAX_ROWS * self.decode_nsplit, R * 4)
+            self.part_o = torch.zeros(ws_rows * cfg.num_attention_heads * hd, dtype=torch.float32, device=dev)
+            self.part_lse = torch.zeros(ws_rows * cfg.num_attention_heads, dtype=torch.float32, device=dev)
+            self.ws_rows = ws_rows
+            self.keys = torch.zeros(R, dtype=torch.int64, device=dev)
+            self.tokens = torch.zeros(R, dtype=torch.int32, device=dev)
+
+    def memory_bytes(self) -> int:
+        n = 0
+        for lw in self.layers:
+            for t in (lw.qkv, lw.o, lw.gate_up, lw.down, lw.ln_in, lw.ln_post):
+                if t is not None:
+                    n += t.numel() * t.element_size()
+            if lw.raw is not None:
+                n += sum(t.numel() * t.element_size() for t in lw.raw.values())
+        for t in (self.embed_w, self.final_norm, self.lm_head):
+            if t is not None:
+                n += t.numel() * t.element_size()
+        n += sum(t.numel() * t.element_size() for t in self.k_cache + self.v_cache)
+        return n
+
+    # ------------------------------------------------------------------------- state
+    def reset(self, slots=None) -> None:
+        """Forget the KV contents of ``slots`` (all by default). The static cache is not
+        zeroed: attention only ever reads positions < the row's length."""
+        for s in (range(self.max_slots) if slots is None else slots):
+            self.seq_len[s] = 0
+
+    # ------------------------------------------------------------------------- helpers
+    def _i32(self, x) -> torch.Tensor:
+        if isinstance(x, torch.Tensor):
+            return x.to(device=self.device, dtype=torch.int32).contiguous()
+        return torch.tensor(list(x), dtype=torch.int32, device=self.device)
+
+    # ------------------------------------------------------------------------- forward (eager)
+    def embed(self, ids: torch.Tensor) -> torch.Tensor:
+        """ids [rows] -> hidden [rows, H] (dtype)."""
+        if self.embed_w is None:
+            raise RuntimeError("[ERROR] this stage has no embedding layer")
+        ids = ids.reshape(-1)
+        if self.gpu:
+            from ..ops import hip
+            rows = ids.numel()
+            out = torch.empty((rows, self.cfg.hidden_size), dtype=torch.bfloat16, device=self.device)
+            hip.embed(self._i32(ids), self.embed_w, out)
+            return out
+        return F.embedding(ids.to(self.device, torch.long), self.embed_w)
+
+    def forward(self, h: torch.Tensor, slot, pos, kv_len=None) -> torch.Tensor:
+        """Run this stage's layers on ``h`` [rows, H]. Row r is a token of the sequence in
+        cache ``slot[r]`` at position ``pos[r]``. Returns the new hidden [rows, H]."""
+        rows = h.shape[0]
+        slot_t, pos_t = self._i32(slot), self._i32(pos)
+        kvl_t = None if kv_len is None else self._i32(kv_len)
+        if self.gpu:
+            return self._forward_hip(h, slot_t, pos_t, kvl_t, rows)
+        return self._forward_torch(h, slot_t.long(), pos_t.long(), None if kvl_t is None else kvl_t.long())
+
+    def head(self, h: torch.Tensor, rows_idx=None) -> torch.Tensor:
+        """final RMSNorm -> lm_head -> greedy argmax for the selected rows. Returns int64 [n]."""
+        if self.lm_head is None:
+            raise RuntimeError("[ERROR] this stage has no lm_head")
+        if rows_idx is None:
+            rows_idx = list(range(h.shape[0]))
+        if self.gpu:
+            from ..ops import hip
+            idx = self._i32(rows_idx)
+            n = idx.numel()
+            out = torch.empty(n, dtype=torch.int64, device=self.device)
+            for c0 in range(0, n, self.DECODE_MAX_ROWS):
+                c = min(self.DECODE_MAX_ROWS, n - c0)
+                keys = self.keys[:c]
+                keys.zero_()
+                ep = hip.make_epi(keys=keys)
+                hip.gemv(h, self.lm_head, c, self.cfg.vocab_size, self.cfg.hidden_size, hip.EPI_ARGMAX, ep,
+                         norm_w=self.final_norm, eps=self.cfg.rms_norm_eps, a_rows=idx[c0:c0 + c])
+                hip.argmax_finalize(keys, c, self.tokens)
+                out[c0:c0 + c] = self.tokens[:c].long()
+            return out
+        hs = h[torch.as_tensor(rows_idx, device=h.device, dtype=torch.long)]
+        lg = self.logits_torch(hs)
+        return torch.argmax(lg, dim=-1)
+
+    def logits_torch(self, hs: torch.Tensor) -> torch.Tensor:
+        from ..models.reference import rmsnorm
+        x = rmsnorm(hs, self.final_norm, self.cfg.rms_norm_eps)
+        return F.linear(x, self.lm_head.float())
+
+    # ------------------------------------------------------------------------- HIP path
+    def _attn_nsplit(self, rows: int, kv_max: int) -> int:
+        if rows <= self.DECODE_MAX_ROWS:
+            return self.decode_nsplit
+        want = max(1, min(8, ceil_div(kv_max, 512)))
+        return max(1, min(want, self.ws_rows // rows))
+
+    def _forward_hip(self, h, slot, pos, kv_len, rows, nsplit: Optional[int] = None) -> torch.Tensor:
+        from ..ops import hip
+        cfg = self.cfg
+        H, I, eps = cfg.hidden_size, cfg.intermediate_size, cfg.rms_norm_eps
+        nh, nkv, hd = cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim
+        if rows > self.max_prefill_rows and rows > self.DECODE_MAX_ROWS:
+            raise ValueError(f"{rows} rows exceed max_prefill_rows={self.max_prefill_rows}")
+        if h.dtype != torch.bfloat16 or not h.is_contiguous():
+            h = h.to(torch.bfloat16).contiguous()
+        hbuf = self.buf_h[:rows]
+        if h.data_ptr() != hbuf.data_ptr():
+            hbuf.copy_(h)
+        decode = rows <= self.DECODE_MAX_ROWS
+        if nsplit is None:
+            kv_max = self.max_seq if decode else (int(pos.max().item()) + 1 if kv_len is None else int(kv_len.max().item()))
+            nsplit = self._attn_nsplit(rows, kv_max)
+        q, attn_o, act, xn = self.buf_q[:rows], self.buf_attn[:rows], self.buf_act[:rows], self.buf_xn[:rows]
+        for li, lw in enumerate(self.layers):
+            kc, vc = self.k_cache[li], self.v_cache[li]
+            ep_qkv = hip.make_epi(out=q, k_cache=kc, v_cache=vc, slot=slot, pos=pos, cos=self.cos, sin=self.sin,
+                                  ldo=q.stride(0), n_heads=nh, n_kv=nkv, head_dim=hd, t_max=self.max_seq)
+            if decode:
+                hip.gemv(hbuf, lw.qkv, rows, cfg.qkv_size, H, hip.EPI_QKV, ep_qkv, norm_w=lw.ln_in, eps=eps)
+            else:
+                hip.rmsnorm(hbuf, lw.ln_in, xn, rows, eps)
+                hip.gemm(xn, lw.qkv, rows, cfg.qkv_size, H, hip.EPI_QKV, ep_qkv)
+            hip.attn(q, kc, vc, slot, pos, rows, nh, nkv, hd, nsplit, self.part_o, self.part_lse, attn_o,
+                     kv_len=kv_len)
+            ep_o = hip.make_epi(out=hbuf, resid=hbuf, ldo=hbuf.stride(0), ldr=hbuf.stride(0))
+            ep_gu = hip.make_epi(out=act, ldo=act.stride(0))
+            if decode:
+                hip.gemv(attn_o, lw.o, rows, H, cfg.q_size, hip.EPI_RESID, ep_o)
+                hip.gemv(hbuf, lw.gate_up, rows, 2 * I, H, hip.EPI_SWIGLU, ep_gu, norm_w=lw.ln_post, eps=eps)
+                hip.gemv(act, lw.down, rows, H, I, hip.EPI_RESID, ep_o)
+            else:
+                hip.gemm(attn_o, lw.o, rows, H, cfg.q_size, hip.EPI_RESID, ep_o)
+                hip.rmsnorm(hbuf, lw.ln_post, xn, rows, eps)
+                hip.gemm(xn, lw.gate_up, rows, 2 * I, H, hip.EPI_SWIGLU, ep_gu)
+                hip.gemm(act, lw.down, rows, H, I, hip.EPI_RESID, ep_o)
+        return hbuf
+
+    # ------------------------------------------------------------------------- torch path (CPU)
+    def _forward_torch(self, h, slot, pos, kv_len) -> torch.Tensor:
+        from ..models.reference import rmsnorm
+        cfg = self.cfg
+        nh, nkv, hd = cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim
+        g = nh // nkv
+        dt = self.dtype
+        rows = h.shape[0]
+        h = h.to(self.device, dt)
+        half = hd // 2
+        cos = self.cos[pos]  # [rows, half]
+        sin = self.sin[pos]
+        T = (pos + 1) if kv_len is None else kv_len
+        for li, lw in enumerate(self.layers):
+            w = lw.raw
+            x = rmsnorm(h, lw.ln_in, cfg.rms_norm_eps).to(dt)
+            q = F.linear(x.float(), w["self_attn.q_proj.weight"].float()).view(rows, nh, hd)
+            k = F.linear(x.float(), w["self_attn.k_proj.weight"].float()).view(rows, nkv, hd)
+            v = F.linear(x.float(), w["self_attn.v_proj.weight"].float()).view(rows, nkv, hd)
+
+            def rope(t):
+                t1, t2 = t[..., :half], t[..., half:]
+                c, s = cos[:, None, :], sin[:, None, :]
+                return torch.cat([t1 * c - t2 * s, t2 * c + t1 * s], dim=-1)
+
+            q, k = rope(q).to(dt), rope(k).to(dt)
+            kc, vc = self.k_cache[li], self.v_cache[li]
+            kc[slot, :, pos] = k
+            vc[slot, :, pos] = v.to(dt)
+            o = torch.empty((rows, nh, hd), dtype=torch.float32, device=self.device)
+            for s_ in torch.unique(slot).tolist():
+                sel = (slot == s_).nonzero().flatten()
+                tmax = int(T[sel].max())
+                K = kc[s_, :, :tmax].float().repeat_interleave(g, dim=0)  # [nh, t, hd]
+                V = vc[s_, :, :tmax].float().repeat_interleave(g, dim=0)
+                qs = q[sel].float().transpose(0, 1)  # [nh, n, hd]
+                sc = torch.matmul(qs, K.transpose(1, 2)) * (hd ** -0.5)  # [nh, n, t]
+                mask = torch.arange(tmax, device=self.device)[None, :] >= T[sel][:, None]
+                sc = sc.masked_fill(mask[None], float("-inf"))
+                p = torch.softmax(sc, dim=-1)
+                o[sel] = torch.matmul(p, V).transpose(0, 1)
+            o = o.reshape(rows, nh * hd).to(dt)
+            h = (h.float() + F.linear(o.float(), w["self_attn.o_proj.weight"].float())).to(dt)
+            x = rmsnorm(h, lw.ln_post, cfg.rms_norm_eps).to(dt).float()
+            a = (F.silu(F.linear(x, w["mlp.gate_proj.weight"].float())) *
+                 F.linear(x, w["mlp.up_proj.weight"].float())).to(dt)
+            h = (h.float() + F.linear(a.float(), w["mlp.down_proj.weight"].float())).to(dt)
+        return h
+
+    # ------------------------------------------------------------------------- sequence API
+    def prefill_rows(self, slot_ids: list, lengths: list) -> tuple:
+        """Build (slot, pos) row vectors for appending ``lengths[i]`` tokens to ``slot_ids[i]``."""
+        slot, pos = [], []
+        for s, n in zip(slot_ids, lengths):
+            p0 = self.seq_len[s]
+            if p0 + n > self.max_seq:
+                raise ValueError(f"[ERROR] sequence in slot {s} would exceed max_seq={self.max_seq}")
+            slot += [s] * n
+            pos += list(range(p0, p0 + n))
+        return slot, pos
+
+    def advance(self, slot_ids: list, lengths: list) -> None:
+        for s, n in zip(slot_ids, lengths):
+            self.seq_len[s] += n
+
+    def graph(self, key) -> Optional["DecodeGraph"]:
+        return self._graphs.get(key)
+
+
+class DecodeGraph:
+    """A hipGraph-captured decode step for a fixed set of ``rows`` (row r -> slot r).
+
+    ``mode``:
+      * ``"full"``  embed(tokens) -> layers -> head argmax -> tokens (single-stage loop)
+      * ``"first"`` embed(tokens) -> layers -> out hidden
+      * ``"mid"``   hidden in -> layers -> out hidden
+      * ``"last"``  hidden in -> layers -> head argmax -> tokens
+    Positions live on the device (``self.pos``) and are advanced inside the graph, so the
+    same graph is replayed every step. ``sync_pos()`` copies the host view after replays.
+    """
+
+    def __init__(self, eng: StageEngine, rows: int, mode: str, slots: Optional[list] = None,
+                 history_len: int = 0):
+        from ..ops import hip
+        if not eng.gpu:
+            raise RuntimeError("DecodeGraph needs a GPU stage")
+        if rows > eng.DECODE_MAX_ROWS:
+            raise ValueError(f"decode graph supports <= {eng.DECODE_MAX_ROWS} rows")
+        self.eng, self.rows, self.mode = eng, rows, mode
+        dev = eng.device
+        self.slots = list(range(rows)) if slots is None else list(slots)
+        self.slot = torch.tensor(self.slots, dtype=torch.int32, device=dev)
+        self.pos = torch.tensor([eng.seq_len[s] for s in self.slots], dtype=torch.int32, device=dev)
+        self.tokens = torch.zeros(rows, dtype=torch.int32, device=dev)
+        self.keys = torch.zeros(rows, dtype=torch.int64, device=dev)
+        self.h_in = torch.zeros((rows, eng.cfg.hidden_size), dtype=torch.bfloat16, device=dev)
+        self.history = torch.zeros((max(1, history_len), rows), dtype=torch.int32, device=dev) if history_len else None
+        self.step_ctr = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.graph = None
+        self._hip = hip
+
+    def _body(self) -> None:
+        hip, eng, rows = self._hip, self.eng, self.rows
+        h = eng.buf_h[:rows]
+        if self.mode in ("full", "first"):
+            hip.embed(self.tokens, eng.embed_w, h)
+        else:
+            h.copy_(self.h_in)
+        eng._forward_hip(h, self.slot, self.pos, None, rows, nsplit=eng.decode_nsplit)
+        if self.mode in ("full", "last"):
+            ep = hip.make_epi(keys=self.keys)
+            hip.gemv(h, eng.lm_head, rows, eng.cfg.vocab_size, eng.cfg.hidden_size, hip.EPI_ARGMAX, ep,
+                     norm_w=eng.final_norm, eps=eng.cfg.rms_norm_eps)
+            hip.argmax_finalize(self.keys, rows, self.tokens, self.pos, 1, self.history,
+                                self.step_ctr if self.history is not None else None)
+        else:
+            hip.pos_advance(self.pos, rows, 1)
+
+    @property
+    def out_hidden(self) -> torch.Tensor:
+        return self.eng.buf_h[:self.rows]
+
+    def capture(self, warmup: bool = True) -> "DecodeGraph":
+        """Capture the step. The warm-up replay (if any) is undone (positions restored)."""
+        pos0, tok0 = self.pos.clone(), self.tokens.clone()
+        s = torch.cuda.Stream(device=self.eng.device)
+        s.wait_stream(torch.cuda.current_stream(self.eng.device))
+        with torch.cuda.stream(s):
+            if warmup:
+                self._body()
+        torch.cuda.current_stream(self.eng.device).wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            self._body()
+        self.graph = g
+        self.pos.copy_(pos0)
+        self.tokens.copy_(tok0)
+        self.keys.zero_()
+        self.step_ctr.zero_()
+        return self
+
+    def replay(self) -> None:
+        self.graph.replay()
+
+    def set_positions(self) -> None:
+        self.pos.copy_(torch.tensor([self.eng.seq_len[s] for s in self.slots], dtype=torch.int32))
+
+    def sync_positions(self) -> None:
+        p = self.pos.tolist()
+        for s, v in zip(self.slots, p):
+            self.eng.seq_len[s] = int(v)

@@ -1,0 +1,115 @@
+"""GPU engine tests: the HIP stage forward vs the fp32 golden model, graph decode vs eager."""
+import pytest
+import torch
+
+from llm_sharding_amd.config import LlamaConfig, tiny
+from llm_sharding_amd.models import weights as W
+from llm_sharding_amd.models.reference import ReferenceLlama
+from llm_sharding_amd.runtime.engine import DecodeGraph, RandomSource, StageEngine
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def rel_err(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def _ref(cfg, seed, n_layers=None):
+    n = cfg.num_hidden_layers if n_layers is None else n_layers
+    layers = [W.random_layer(cfg, i, torch.bfloat16, seed=seed) for i in range(n)]
+    return ReferenceLlama(cfg, W.random_embedding(cfg, torch.bfloat16, seed=seed), layers,
+                          W.random_final_norm(cfg, torch.bfloat16, seed=seed),
+                          W.random_lm_head(cfg, torch.bfloat16, seed=seed), max_pos=256)
+
+
+def _mid_cfg():
+    # 7B-shaped layers (H=4096, 32 heads, I=11008) but 2 layers and a small vocab
+    return LlamaConfig(num_hidden_layers=2, vocab_size=4096, max_position_embeddings=1024, name="7b-2L")
+
+
+@pytest.mark.parametrize("cfg_fn,S", [(tiny, 7), (tiny, 90), (_mid_cfg, 5), (_mid_cfg, 130)])
+def test_engine_prefill_then_decode_vs_golden(cfg_fn, S):
+    cfg = cfg_fn()
+    seed = 11
+    # random weights are generated on CPU in both cases -> identical values
+    src = RandomSource(cfg, seed)
+
+    class CpuGen(RandomSource):
+        def layer(self, i, device, dtype):
+            return {k: v.to(device) for k, v in W.random_layer(cfg, i, dtype, "cpu", seed).items()}
+
+        def embedding(self, device, dtype):
+            return W.random_embedding(cfg, dtype, "cpu", seed).to(device)
+
+        def final_norm(self, device, dtype):
+            return W.random_final_norm(cfg, dtype, "cpu", seed).to(device)
+
+        def lm_head(self, device, dtype):
+            return W.random_lm_head(cfg, dtype, "cpu", seed).to(device)
+
+    eng = StageEngine(cfg, 0, cfg.num_hidden_layers, DEV, torch.bfloat16, has_embed=True, has_head=True,
+                      source=CpuGen(cfg, seed), max_seq=256, max_prefill_rows=256)
+    ref = _ref(cfg, seed)
+    g = torch.Generator().manual_seed(S)
+    ids = torch.randint(3, cfg.vocab_size, (S,), generator=g)
+    slot, pos = eng.prefill_rows([0], [S])
+    h = eng.forward(eng.embed(ids.to(DEV)), slot, pos)
+    eng.advance([0], [S])
+    href = ref.forward_hidden(ref.embed[ids][None])[0]
+    assert rel_err(h, href) < 3e-2
+    # decode 4 tokens feeding the golden model's own choices (no divergence compounding)
+    tok, lg = None, ref.logits(href[-1:])
+    for _ in range(4):
+        tok = int(lg.argmax(-1)[0])
+        slot, pos = eng.prefill_rows([0], [1])
+        h = eng.forward(eng.embed(torch.tensor([tok], device=DEV)), slot, pos)
+        eng.advance([0], [1])
+        href = ref.forward_hidden(ref.embed[torch.tensor([[tok]])])[0]
+        assert rel_err(h, href) < 3e-2
+        lg = ref.logits(href)
+        got = int(eng.head(h, [0])[0])
+        top2 = lg[0].topk(2).values
+        if (top2[0] - top2[1]).item() > 0.05 * lg.abs().max().item():
+            assert got == int(lg.argmax(-1)[0])
+
+
+def test_decode_graph_matches_eager():
+    cfg = tiny()
+    src = RandomSource(cfg, seed=4)
+    rows = 3
+    kw = dict(has_embed=True, has_head=True, source=src, max_slots=rows, max_seq=128)
+    e1 = StageEngine(cfg, 0, cfg.num_hidden_layers, DEV, torch.bfloat16, **kw)
+    e2 = StageEngine(cfg, 0, cfg.num_hidden_layers, DEV, torch.bfloat16, **kw)
+    prompts = [torch.tensor([1, 9, 8, 7]), torch.tensor([1, 100]), torch.tensor([1, 55, 44, 33, 22, 11])]
+    firsts = []
+    for e in (e1, e2):
+        f = []
+        for s, p in enumerate(prompts):
+            sl, po = e.prefill_rows([s], [p.numel()])
+            hh = e.forward(e.embed(p.to(DEV)), sl, po)
+            e.advance([s], [p.numel()])
+            f.append(int(e.head(hh, [p.numel() - 1])[0]))
+        firsts.append(f)
+    assert firsts[0] == firsts[1]
+    # eager decode on e1
+    toks = torch.tensor(firsts[0])
+    eager = []
+    for _ in range(8):
+        sl, po = e1.prefill_rows(list(range(rows)), [1] * rows)
+        hh = e1.forward(e1.embed(toks.to(DEV)), sl, po)
+        e1.advance(list(range(rows)), [1] * rows)
+        toks = e1.head(hh).cpu()
+        eager.append(toks.tolist())
+    # graph decode on e2
+    dg = DecodeGraph(e2, rows, "full", history_len=8)
+    dg.tokens.copy_(torch.tensor(firsts[1], dtype=torch.int32))
+    dg.capture()
+    for _ in range(8):
+        dg.replay()
+    torch.cuda.synchronize()
+    graph = dg.history.cpu().tolist()
+    assert graph == eager
+    dg.sync_positions()
+    assert e2.seq_len == e1.seq_len

@@ -1,0 +1,268 @@
+"""GPU numerics tests: every HIP kernel vs a plain PyTorch fp32 reference of the same op."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from llm_sharding_amd.ops import packing
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def hip():
+    from llm_sharding_amd.ops import hip as h
+    h.lib()
+    return h
+
+
+def rel_err(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def _rnd(*shape, scale=1.0, gen=None):
+    return (torch.randn(*shape, generator=gen, device=DEV) * scale).to(torch.bfloat16)
+
+
+def _rmsnorm(x, w, eps):
+    xf = x.float()
+    return xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * w.float()
+
+
+def test_native_library_loaded_in_process():
+    h = hip()
+    assert h.lib().lsa_version() == 1
+    maps = open("/proc/self/maps").read()
+    assert "liblsa_kernels.so" in maps
+    # exactly one HIP runtime in the process (ours resolved to torch's by soname)
+    runtimes = {l.split()[-1] for l in maps.splitlines() if "libamdhip64" in l}
+    assert len(runtimes) == 1, runtimes
+
+
+@pytest.mark.parametrize("M", [1, 3, 16, 17, 40, 64])
+@pytest.mark.parametrize("N,K", [(4096, 4096), (256, 11008), (512, 256)])
+def test_gemv_store(M, N, K):
+    h = hip()
+    g = torch.Generator(device=DEV).manual_seed(M * 7 + N)
+    x = _rnd(M, K, gen=g)
+    w = _rnd(N, K, scale=0.02, gen=g)
+    out = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
+    ep = h.make_epi(out=out, ldo=N)
+    h.gemv(x, packing.pack_b(w), M, N, K, h.EPI_STORE, ep)
+    ref = x.float() @ w.float().T
+    assert rel_err(out, ref) < 8e-3
+
+
+@pytest.mark.parametrize("M", [1, 7, 33])
+def test_gemv_norm_resid_tn(M):
+    h = hip()
+    N, K = 1024, 4096
+    x = _rnd(M, K)
+    nw = (1 + 0.1 * torch.randn(K, device=DEV)).to(torch.bfloat16)
+    w = _rnd(N, K, scale=0.02)
+    resid = _rnd(M, N)
+    out = resid.clone()
+    ref = resid.float() + _rmsnorm(x, nw, 1e-5) @ w.float().T
+    for tn in (1, 2, 4):
+        if M > 32 and tn > 2:
+            continue
+        out.copy_(resid)
+        ep = h.make_epi(out=out, resid=out, ldo=N, ldr=N)
+        h.gemv(x, packing.pack_b(w), M, N, K, h.EPI_RESID, ep, norm_w=nw, eps=1e-5, tn=tn)
+        assert rel_err(out, ref) < 8e-3, tn
+
+
+@pytest.mark.parametrize("M", [1, 12, 64])
+def test_gemv_swiglu(M):
+    h = hip()
+    I, H = 1024, 512
+    x = _rnd(M, H)
+    wg, wu = _rnd(I, H, scale=0.05), _rnd(I, H, scale=0.05)
+    out = torch.zeros(M, I, dtype=torch.bfloat16, device=DEV)
+    ep = h.make_epi(out=out, ldo=I)
+    h.gemv(x, packing.pack_b(packing.fuse_gate_up(wg, wu)), M, 2 * I, H, h.EPI_SWIGLU, ep)
+    ref = F.silu(x.float() @ wg.float().T) * (x.float() @ wu.float().T)
+    assert rel_err(out, ref) < 1e-2
+
+
+def _rope_ref(t, pos, cos, sin):
+    half = t.shape[-1] // 2
+    c, s = cos[pos][:, None, :], sin[pos][:, None, :]
+    t1, t2 = t[..., :half], t[..., half:]
+    return torch.cat([t1 * c - t2 * s, t2 * c + t1 * s], dim=-1)
+
+
+@pytest.mark.parametrize("path", ["gemv", "gemm"])
+@pytest.mark.parametrize("nh,nkv,hd", [(32, 32, 128), (8, 2, 64), (24, 8, 128)])
+def test_qkv_rope_kv_append(path, nh, nkv, hd):
+    from llm_sharding_amd.config import tiny
+    from llm_sharding_amd.models.rope import rope_table
+    h = hip()
+    H = 512
+    M = 5 if path == "gemv" else 150
+    slots, T = 3, 256
+    wq, wk, wv = _rnd(nh * hd, H, scale=0.05), _rnd(nkv * hd, H, scale=0.05), _rnd(nkv * hd, H, scale=0.05)
+    x = _rnd(M, H)
+    cfg = tiny(head_dim=hd)
+    cos, sin = rope_table(cfg, T, DEV)
+    slot = torch.randint(0, slots, (M,), device=DEV, dtype=torch.int32)
+    pos = torch.randperm(T, device=DEV)[:M].to(torch.int32)  # distinct -> no write collisions
+    q = torch.zeros(M, nh * hd, dtype=torch.bfloat16, device=DEV)
+    kc = torch.zeros(slots, nkv, T, hd, dtype=torch.bfloat16, device=DEV)
+    vc = torch.zeros_like(kc)
+    wp = packing.pack_b(packing.fuse_qkv(wq, wk, wv, nh, nkv, hd))
+    N = (nh + 2 * nkv) * hd
+    ep = h.make_epi(out=q, k_cache=kc, v_cache=vc, slot=slot, pos=pos, cos=cos, sin=sin, ldo=nh * hd,
+                    n_heads=nh, n_kv=nkv, head_dim=hd, t_max=T)
+    if path == "gemv":
+        h.gemv(x, wp, M, N, H, h.EPI_QKV, ep)
+    else:
+        h.gemm(x, wp, M, N, H, h.EPI_QKV, ep)
+    xf = x.float()
+    pl = pos.long()
+    qr = _rope_ref((xf @ wq.float().T).view(M, nh, hd), pl, cos, sin).reshape(M, -1)
+    kr = _rope_ref((xf @ wk.float().T).view(M, nkv, hd), pl, cos, sin)
+    vr = (xf @ wv.float().T).view(M, nkv, hd)
+    assert rel_err(q, qr) < 1e-2
+    sl = slot.long()
+    assert rel_err(kc[sl, :, pl], kr) < 1e-2
+    assert rel_err(vc[sl, :, pl], vr) < 1e-2
+
+
+@pytest.mark.parametrize("M", [1, 4, 64])
+def test_gemv_argmax_with_rows(M):
+    h = hip()
+    V, H = 32000, 4096
+    hid = _rnd(100, H)
+    fn = (1 + 0.1 * torch.randn(H, device=DEV)).to(torch.bfloat16)
+    lm = _rnd(V, H, scale=0.02)
+    rows = torch.randint(0, 100, (M,), device=DEV, dtype=torch.int32)
+    keys = torch.zeros(M, dtype=torch.int64, device=DEV)
+    ep = h.make_epi(keys=keys)
+    h.gemv(hid, packing.pack_b(lm), M, V, H, h.EPI_ARGMAX, ep, norm_w=fn, eps=1e-5, a_rows=rows)
+    tok = torch.zeros(M, dtype=torch.int32, device=DEV)
+    h.argmax_finalize(keys, M, tok)
+    logits = _rmsnorm(hid[rows.long()], fn, 1e-5) @ lm.float().T
+    want = logits.argmax(-1)
+    # bf16 rounding of the normalized activation can flip near-ties: require the chosen
+    # logit to be within tolerance of the max and most picks to be exact.
+    chosen = logits.gather(1, tok.long()[:, None])[:, 0]
+    assert torch.all(logits.max(-1).values - chosen < 2e-2 * logits.abs().max())
+    assert (tok.long() == want).float().mean() >= 0.9
+    assert torch.all(keys == 0)  # finalize resets the keys
+
+
+@pytest.mark.parametrize("M", [17, 128, 333])
+@pytest.mark.parametrize("N,K", [(4096, 4096), (512, 11008), (192, 256)])
+def test_gemm_store_resid(M, N, K):
+    h = hip()
+    a = _rnd(M, K)
+    w = _rnd(N, K, scale=0.02)
+    out = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
+    h.gemm(a, packing.pack_b(w), M, N, K, h.EPI_STORE, h.make_epi(out=out, ldo=N))
+    ref = a.float() @ w.float().T
+    assert rel_err(out, ref) < 8e-3
+    r = _rnd(M, N)
+    o2 = r.clone()
+    h.gemm(a, packing.pack_b(w), M, N, K, h.EPI_RESID, h.make_epi(out=o2, resid=o2, ldo=N, ldr=N))
+    assert rel_err(o2, r.float() + ref) < 8e-3
+
+
+def test_gemm_swiglu():
+    h = hip()
+    M, I, H = 200, 1024, 512
+    x = _rnd(M, H)
+    wg, wu = _rnd(I, H, scale=0.05), _rnd(I, H, scale=0.05)
+    out = torch.zeros(M, I, dtype=torch.bfloat16, device=DEV)
+    h.gemm(x, packing.pack_b(packing.fuse_gate_up(wg, wu)), M, 2 * I, H, h.EPI_SWIGLU, h.make_epi(out=out, ldo=I))
+    ref = F.silu(x.float() @ wg.float().T) * (x.float() @ wu.float().T)
+    assert rel_err(out, ref) < 1e-2
+
+
+def _attn_ref(q, kc, vc, slot, kvlen, nh, nkv, hd):
+    rows = q.shape[0]
+    g = nh // nkv
+    out = torch.zeros(rows, nh * hd, device=DEV)
+    for r in range(rows):
+        T = int(kvlen[r])
+        K = kc[int(slot[r]), :, :T].float().repeat_interleave(g, 0)
+        V = vc[int(slot[r]), :, :T].float().repeat_interleave(g, 0)
+        qq = q[r].float().view(nh, 1, hd)
+        p = torch.softmax(qq @ K.transpose(1, 2) / math.sqrt(hd), -1)
+        out[r] = (p @ V).reshape(-1)
+    return out
+
+
+@pytest.mark.parametrize("nh,nkv,hd", [(32, 32, 128), (64, 8, 128), (24, 8, 128), (8, 2, 64)])
+@pytest.mark.parametrize("nsplit", [1, 4, 16])
+def test_attention_split(nh, nkv, hd, nsplit):
+    h = hip()
+    slots, T = 3, 1100
+    rows = 6
+    q = _rnd(rows, nh * hd)
+    kc, vc = _rnd(slots, nkv, T, hd), _rnd(slots, nkv, T, hd)
+    slot = torch.tensor([0, 1, 2, 0, 1, 2], dtype=torch.int32, device=DEV)
+    pos = torch.tensor([0, 1, 37, 255, 511, 1099], dtype=torch.int32, device=DEV)
+    po = torch.zeros(rows * nh * nsplit * hd, device=DEV)
+    pl = torch.zeros(rows * nh * nsplit, device=DEV)
+    out = torch.zeros(rows, nh * hd, dtype=torch.bfloat16, device=DEV)
+    h.attn(q, kc, vc, slot, pos, rows, nh, nkv, hd, nsplit, po, pl, out)
+    ref = _attn_ref(q, kc, vc, slot, pos + 1, nh, nkv, hd)
+    assert rel_err(out, ref) < 1e-2
+
+
+def test_attention_kvlen_override():
+    h = hip()
+    nh, nkv, hd, rows, T = 8, 8, 128, 4, 64
+    q = _rnd(rows, nh * hd)
+    kc, vc = _rnd(1, nkv, T, hd), _rnd(1, nkv, T, hd)
+    slot = torch.zeros(rows, dtype=torch.int32, device=DEV)
+    pos = torch.arange(rows, dtype=torch.int32, device=DEV)
+    kvl = torch.full((rows,), 50, dtype=torch.int32, device=DEV)
+    po = torch.zeros(rows * nh * 2 * hd, device=DEV)
+    pl = torch.zeros(rows * nh * 2, device=DEV)
+    out = torch.zeros(rows, nh * hd, dtype=torch.bfloat16, device=DEV)
+    h.attn(q, kc, vc, slot, pos, rows, nh, nkv, hd, 2, po, pl, out, kv_len=kvl)
+    assert rel_err(out, _attn_ref(q, kc, vc, slot, kvl, nh, nkv, hd)) < 1e-2
+
+
+def test_embed_and_rmsnorm():
+    h = hip()
+    V, H = 1000, 4096
+    table = _rnd(V, H)
+    ids = torch.randint(0, V, (37,), device=DEV, dtype=torch.int32)
+    out = torch.zeros(37, H, dtype=torch.bfloat16, device=DEV)
+    h.embed(ids, table, out)
+    assert torch.equal(out, table[ids.long()])
+    w = (1 + 0.1 * torch.randn(H, device=DEV)).to(torch.bfloat16)
+    o2 = torch.zeros_like(out)
+    h.rmsnorm(out, w, o2, 37, 1e-5)
+    assert rel_err(o2, _rmsnorm(out, w, 1e-5)) < 5e-3
+
+
+def test_argmax_finalize_history_and_pos():
+    h = hip()
+    rows = 5
+    keys = torch.zeros(rows, dtype=torch.int64, device=DEV)
+    # build keys via the real kernel path: a gemv argmax on an identity-like problem
+    H, V = 64, 256
+    hid = torch.zeros(rows, H, dtype=torch.bfloat16, device=DEV)
+    want = torch.tensor([3, 100, 7, 255, 0])
+    lm = torch.zeros(V, H, dtype=torch.bfloat16, device=DEV)
+    for r, t in enumerate(want.tolist()):
+        hid[r, r] = 1.0
+        lm[t, r] = 1.0
+    h.gemv(hid, packing.pack_b(lm), rows, V, H, h.EPI_ARGMAX, h.make_epi(keys=keys))
+    tokens = torch.zeros(rows, dtype=torch.int32, device=DEV)
+    pos = torch.zeros(rows, dtype=torch.int32, device=DEV)
+    hist = torch.zeros(4, rows, dtype=torch.int32, device=DEV)
+    step = torch.zeros(1, dtype=torch.int32, device=DEV)
+    h.argmax_finalize(keys, rows, tokens, pos, 1, hist, step)
+    assert tokens.cpu().tolist() == want.tolist()
+    assert pos.cpu().tolist() == [1] * rows and int(step) == 1
+    assert hist[0].cpu().tolist() == want.tolist()
+    h.pos_advance(pos, rows, 2)
+    assert pos.cpu().tolist() == [3] * rows
