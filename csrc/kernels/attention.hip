@@ -27,7 +27,8 @@ __global__ __launch_bounds__(ATT_THR) void attn_split_kernel(
     const bf16_raw* __restrict__ q, int ldq, const bf16_raw* __restrict__ kc,
     const bf16_raw* __restrict__ vc, const int* __restrict__ slot, const int* __restrict__ pos,
     const int* __restrict__ kv_len, int n_heads, int n_kv, int t_max, float scale_log2,
-    int nsplit, int min_chunk, float* __restrict__ part_o, float* __restrict__ part_lse) {
+    int nsplit, int min_chunk, float* __restrict__ part_o, float* __restrict__ part_lse,
+    bf16_raw* __restrict__ out, int ldo) {
   constexpr int LPK = HD / 8;          // lanes per key row (8 bf16 = 16 B per lane)
   constexpr int KPW = LSA_WAVE / LPK;  // keys per wave-instruction
   constexpr int KPI = KPW * ATT_WAVES; // keys per workgroup iteration
@@ -164,9 +165,13 @@ __global__ __launch_bounds__(ATT_THR) void attn_split_kernel(
       ls += s_l[i][r] * a;
       os += s_o[i][r][d] * a;
     }
-    const size_t pi = pbase + (size_t)r * nsplit;
-    part_o[pi * HD + d] = os / ls;
-    if (d == 0) part_lse[pi] = mm + log2f(ls);
+    if (nsplit == 1) {  // single split: final output directly, no combine launch
+      out[(size_t)row * ldo + (size_t)(kvh * G + r) * HD + d] = f2bf(os / ls);
+    } else {
+      const size_t pi = pbase + (size_t)r * nsplit;
+      part_o[pi * HD + d] = os / ls;
+      if (d == 0) part_lse[pi] = mm + log2f(ls);
+    }
   }
 }
 
@@ -193,10 +198,11 @@ __global__ __launch_bounds__(HD) void attn_combine_kernel(const float* __restric
 template <int HD, int G>
 int launch_split(const bf16_raw* q, int ldq, const bf16_raw* kc, const bf16_raw* vc, const int* slot,
                  const int* pos, const int* kv_len, int rows, int n_heads, int n_kv, int t_max,
-                 float scale_log2, int nsplit, int min_chunk, float* po, float* pl, hipStream_t s) {
+                 float scale_log2, int nsplit, int min_chunk, float* po, float* pl, bf16_raw* out,
+                 int ldo, hipStream_t s) {
   dim3 grid(nsplit, n_kv, rows);
   attn_split_kernel<HD, G><<<grid, ATT_THR, 0, s>>>(q, ldq, kc, vc, slot, pos, kv_len, n_heads, n_kv,
-                                                     t_max, scale_log2, nsplit, min_chunk, po, pl);
+                                                     t_max, scale_log2, nsplit, min_chunk, po, pl, out, ldo);
   LSA_CHECK_LAUNCH();
   return LSA_OK;
 }
@@ -204,9 +210,10 @@ int launch_split(const bf16_raw* q, int ldq, const bf16_raw* kc, const bf16_raw*
 template <int HD>
 int dispatch_g(int g, const bf16_raw* q, int ldq, const bf16_raw* kc, const bf16_raw* vc,
                const int* slot, const int* pos, const int* kv_len, int rows, int n_heads, int n_kv,
-               int t_max, float sl2, int nsplit, int min_chunk, float* po, float* pl, hipStream_t s) {
+               int t_max, float sl2, int nsplit, int min_chunk, float* po, float* pl, bf16_raw* out,
+               int ldo, hipStream_t s) {
 #define LSA_G(GG) \
-  case GG: return launch_split<HD, GG>(q, ldq, kc, vc, slot, pos, kv_len, rows, n_heads, n_kv, t_max, sl2, nsplit, min_chunk, po, pl, s);
+  case GG: return launch_split<HD, GG>(q, ldq, kc, vc, slot, pos, kv_len, rows, n_heads, n_kv, t_max, sl2, nsplit, min_chunk, po, pl, out, ldo, s);
   switch (g) {
     LSA_G(1) LSA_G(2) LSA_G(3) LSA_G(4) LSA_G(6) LSA_G(8)
     default: return LSA_UNSUPPORTED;
@@ -227,14 +234,15 @@ extern "C" int lsa_attn_decode(const void* q, int ldq, const void* k_cache, cons
   const bf16_raw* qq = static_cast<const bf16_raw*>(q);
   const bf16_raw* kc = static_cast<const bf16_raw*>(k_cache);
   const bf16_raw* vc = static_cast<const bf16_raw*>(v_cache);
+  bf16_raw* o = static_cast<bf16_raw*>(out);
   int rc;
   if (head_dim == 128)
-    rc = dispatch_g<128>(g, qq, ldq, kc, vc, slot, pos, kv_len, rows, n_heads, n_kv, t_max, sl2, nsplit, min_chunk, part_o, part_lse, stream);
+    rc = dispatch_g<128>(g, qq, ldq, kc, vc, slot, pos, kv_len, rows, n_heads, n_kv, t_max, sl2, nsplit, min_chunk, part_o, part_lse, o, ldo, stream);
   else if (head_dim == 64)
-    rc = dispatch_g<64>(g, qq, ldq, kc, vc, slot, pos, kv_len, rows, n_heads, n_kv, t_max, sl2, nsplit, min_chunk, part_o, part_lse, stream);
+    rc = dispatch_g<64>(g, qq, ldq, kc, vc, slot, pos, kv_len, rows, n_heads, n_kv, t_max, sl2, nsplit, min_chunk, part_o, part_lse, o, ldo, stream);
   else
     return LSA_UNSUPPORTED;
-  if (rc != LSA_OK) return rc;
+  if (rc != LSA_OK || nsplit == 1) return rc;
   dim3 grid(n_heads, rows);
   if (head_dim == 128)
     attn_combine_kernel<128><<<grid, 128, 0, stream>>>(part_o, part_lse, n_heads, nsplit, static_cast<bf16_raw*>(out), ldo);

@@ -40,9 +40,9 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const bf16_raw* __restrict
   const float rs = rsqrtf((s_part[0] + s_part[1] + s_part[2] + s_part[3]) / (float)H + eps);
   bf16_raw* orow = out + (size_t)row * ldo;
   for (int c = tid; c < (H >> 3); c += 256) {
-    float f[8], g[8];
+    float f[8], g[8] = {1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
     unpack8(ld16(xr + c * 8), f);
-    unpack8(ld16(w + c * 8), g);
+    if (w) unpack8(ld16(w + c * 8), g);  // w == nullptr: weight folded into the next GEMM
 #pragma unroll
     for (int j = 0; j < 8; ++j) f[j] = f[j] * rs * g[j];
     st16(orow + c * 8, pack8(f));

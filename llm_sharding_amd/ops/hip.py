@@ -52,7 +52,7 @@ def lib() -> ctypes.CDLL:
             "(or __graft_entry__.build()).")
     L = ctypes.CDLL(KERNELS_SO, mode=ctypes.RTLD_GLOBAL)
     vp, i, f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
-    L.lsa_gemv.argtypes = [vp, i, vp, vp, i, i, i, vp, f, i, ctypes.POINTER(EpiArgs), i, vp]
+    L.lsa_gemv.argtypes = [vp, i, vp, vp, i, i, i, i, f, i, ctypes.POINTER(EpiArgs), i, i, i, vp]
     L.lsa_gemm.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(EpiArgs), i, vp]
     L.lsa_attn_decode.argtypes = [vp, i, vp, vp, vp, vp, vp, i, i, i, i, i, f, i, i, vp, vp, vp, i, vp]
     L.lsa_embed.argtypes = [vp, i, vp, i, vp, i, vp]
@@ -97,24 +97,26 @@ def make_epi(out=None, resid=None, k_cache=None, v_cache=None, slot=None, pos=No
 
 # ------------------------------------------------------------------------------ projections
 def gemv(x: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep: EpiArgs,
-         norm_w: Optional[torch.Tensor] = None, eps: float = 1e-5,
-         a_rows: Optional[torch.Tensor] = None, tn: int = 0) -> None:
-    """Decode projection, M <= 16 rows. ``wp`` is ``pack_b(W)``, W: [N, K]."""
-    from .packing import pick_tn
-    _req(1 <= M <= 16, f"gemv supports 1..16 rows, got {M}")
-    _req(_is_bf16_cuda(x, wp, norm_w), "gemv: bf16 cuda tensors required")
+         norm: bool = False, eps: float = 1e-5, a_rows: Optional[torch.Tensor] = None,
+         tn: int = 0, nw: int = 0, u: int = 0) -> None:
+    """Decode projection, M <= 64 rows. ``wp`` is ``pack_b(W)`` (``pack_b(fold_norm(W, g))``
+    when ``norm``: RMSNorm of the A rows is then applied in-kernel), W: [N, K]."""
+    from .packing import GEMV_CONFIGS, gemv_config, row_blocks
+    _req(1 <= M <= 64, f"gemv supports 1..64 rows, got {M}")
+    _req(_is_bf16_cuda(x, wp), "gemv: bf16 cuda tensors required")
     _req(wp.numel() == N * K and N % 16 == 0 and K % 32 == 0, "gemv: packed weight shape")
     _req(x.dim() == 2 and x.shape[1] >= K and x.stride(1) == 1, "gemv: x must be [rows, >=K] row-major")
     if a_rows is None:
         _req(x.shape[0] >= M, "gemv: x has fewer rows than M")
     else:
         _req(a_rows.dtype == torch.int32 and a_rows.is_cuda and a_rows.numel() >= M, "gemv: a_rows")
-    if norm_w is not None:
-        _req(norm_w.numel() == K, "gemv: norm weight size")
     if tn == 0:
-        tn = pick_tn(N // 16, need_even=(epi == EPI_SWIGLU))
-    rc = lib().lsa_gemv(_p(x), x.stride(0), _p(a_rows), _p(wp), M, N, K, _p(norm_w), float(eps), epi,
-                        ctypes.byref(ep), tn, _stream())
+        tn, nw, u = gemv_config(N // 16, M, need_even=(epi == EPI_SWIGLU), k=K)
+    mb = row_blocks(M)
+    _req((tn, mb, nw, u) in GEMV_CONFIGS, f"gemv: config tn={tn} nw={nw} u={u} not built for {M} rows")
+    _req((K // 32) % u == 0, f"gemv: K={K} must be a multiple of {32 * u}")
+    rc = lib().lsa_gemv(_p(x), x.stride(0), _p(a_rows), _p(wp), M, N, K, int(norm), float(eps), epi,
+                        ctypes.byref(ep), tn, nw, u, _stream())
     _check(rc, "lsa_gemv")
 
 
@@ -164,8 +166,10 @@ def embed(ids: torch.Tensor, table: torch.Tensor, out: torch.Tensor, rows: Optio
     _check(rc, "lsa_embed")
 
 
-def rmsnorm(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, rows: int, eps: float) -> None:
-    H = w.numel()
+def rmsnorm(x: torch.Tensor, w: Optional[torch.Tensor], out: torch.Tensor, rows: int, eps: float,
+            H: Optional[int] = None) -> None:
+    """out = x * rsqrt(mean(x^2)+eps) [* w]. ``w=None``: weight folded into the next GEMM."""
+    H = w.numel() if w is not None else (H or x.shape[1])
     _req(_is_bf16_cuda(x, w, out), "rmsnorm: bf16 cuda tensors")
     rc = lib().lsa_rmsnorm(_p(x), x.stride(0), _p(w), rows, H, float(eps), _p(out), out.stride(0), _stream())
     _check(rc, "lsa_rmsnorm")

@@ -16,6 +16,9 @@ q/k/v and gate/up ``nn.Linear`` modules inside HF ``LlamaDecoderLayer``):
 """
 from __future__ import annotations
 
+import json
+import os
+
 import torch
 
 
@@ -59,8 +62,71 @@ def fuse_gate_up(wg: torch.Tensor, wu: torch.Tensor) -> torch.Tensor:
     return torch.stack([wg.view(I // 16, 16, H), wu.view(I // 16, 16, H)], dim=1).reshape(2 * I, H)
 
 
-def pick_tn(n_tiles: int, need_even: bool = False, prefer: tuple = (4, 2, 1)) -> int:
-    for tn in prefer:
-        if n_tiles % tn == 0 and (not need_even or tn % 2 == 0):
-            return tn
-    raise ValueError(f"no tile factor for {n_tiles} tiles")
+def fold_norm(w: torch.Tensor, g: torch.Tensor) -> torch.Tensor:
+    """``W' = W * diag(g)`` (fp32 product, rounded once): RMSNorm's weight folded into the
+    following projection, so the decode GEMV applies only ``rsqrt(mean(x^2)+eps)`` per row."""
+    return (w.float() * g.float()[None, :]).to(w.dtype)
+
+
+N_CU = 256  # MI355X compute units
+
+
+# (tn, mb, nw, u) instantiated in csrc/kernels/gemv.hip (LSA_GEMV_CONFIGS) - keep in sync.
+GEMV_CONFIGS = [
+    (1, 1, 4, 4), (1, 1, 8, 4), (1, 1, 16, 4), (1, 1, 4, 8), (1, 1, 8, 8),
+    (1, 2, 4, 4), (1, 2, 8, 4), (1, 2, 16, 2), (1, 4, 4, 2), (1, 4, 8, 2),
+    (2, 1, 4, 4), (2, 1, 8, 4), (2, 1, 16, 2), (2, 1, 8, 2), (2, 2, 4, 2),
+    (2, 2, 8, 2), (2, 4, 4, 2), (2, 4, 8, 2), (4, 1, 4, 2), (4, 1, 8, 2),
+    (4, 2, 4, 2), (4, 2, 8, 2), (4, 4, 4, 2),
+]
+
+_TUNED = None
+TUNING_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemv_tuning.json")
+
+
+def row_blocks(rows: int) -> int:
+    return 1 if rows <= 16 else (2 if rows <= 32 else 4)
+
+
+def gemv_candidates(n_tiles: int, k: int, rows: int, need_even: bool = False) -> list:
+    mb = row_blocks(rows)
+    return [(tn, nw, u) for (tn, b, nw, u) in GEMV_CONFIGS
+            if b == mb and n_tiles % tn == 0 and (not need_even or tn % 2 == 0) and (k // 32) % u == 0]
+
+
+def _tuned() -> dict:
+    global _TUNED
+    if _TUNED is None:
+        _TUNED = {}
+        if os.path.exists(TUNING_FILE):
+            with open(TUNING_FILE) as f:
+                for e in json.load(f).get("entries", []):
+                    _TUNED[(e["N"], e["K"], e["mb"], bool(e["even"]))] = tuple(e["cfg"])
+    return _TUNED
+
+
+def gemv_config(n_tiles: int, rows: int, need_even: bool = False, k: int = 4096) -> tuple:
+    """(tn, nw, u) for the decode GEMV. Uses the on-device tuning table measured on MI355X
+    (scripts/bench_kernels.py --tune) when the shape is in it, else a cost model:
+    time ~ (weight bytes + A re-reads / 5) / grid efficiency, where each workgroup re-reads
+    the whole A (rows x K) from L2 (~5x the HBM rate) and grid efficiency =
+    workgroups / (256 CUs x rounds)."""
+    mb = row_blocks(rows)
+    t = _tuned().get((n_tiles * 16, k, mb, bool(need_even)))
+    cands = gemv_candidates(n_tiles, k, rows, need_even)
+    if t is not None and t in cands:
+        return t
+    best, best_cost = None, float("inf")
+    for tn, nw, u in cands:
+        g = n_tiles // tn
+        eff = g / (N_CU * -(-g // N_CU))
+        cost = (1.0 + 0.2 * rows / (16.0 * tn)) / eff - 0.01 * (nw * u / 32.0)
+        if cost < best_cost - 1e-9:
+            best, best_cost = (tn, nw, u), cost
+    if best is None:
+        raise ValueError(f"no GEMV config for {n_tiles} tiles, K={k}, rows={rows}")
+    return best
+
+
+def pick_tn(n_tiles: int, need_even: bool = False, rows: int = 1, k: int = 4096) -> int:
+    return gemv_config(n_tiles, rows, need_even, k)[0]

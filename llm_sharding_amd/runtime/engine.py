@@ -166,7 +166,8 @@ class StageEngine:
             self._log("[INFO] loading final norm / lm_head...")
             self.final_norm = src.final_norm(dev, dt).contiguous()
             lm = src.lm_head(dev, dt)
-            self.lm_head = packing.pack_b(lm) if self.gpu else lm.contiguous()
+            # GPU: final RMSNorm weight folded into the packed lm_head (fused norm+GEMV+argmax)
+            self.lm_head = packing.pack_b(packing.fold_norm(lm, self.final_norm)) if self.gpu else lm.contiguous()
             del lm
         self._alloc_runtime()
 
@@ -177,10 +178,13 @@ class StageEngine:
                                cfg.num_key_value_heads, cfg.head_dim)
         gu = packing.fuse_gate_up(lw["mlp.gate_proj.weight"], lw["mlp.up_proj.weight"])
         if self.gpu:
-            return LayerWeights(packing.pack_b(qkv), packing.pack_b(lw["self_attn.o_proj.weight"]),
-                                packing.pack_b(gu), packing.pack_b(lw["mlp.down_proj.weight"]),
-                                lw["input_layernorm.weight"].contiguous(),
-                                lw["post_attention_layernorm.weight"].contiguous())
+            # RMSNorm weights are folded into the projections that consume the normed input
+            ln_in, ln_post = lw["input_layernorm.weight"], lw["post_attention_layernorm.weight"]
+            return LayerWeights(packing.pack_b(packing.fold_norm(qkv, ln_in)),
+                                packing.pack_b(lw["self_attn.o_proj.weight"]),
+                                packing.pack_b(packing.fold_norm(gu, ln_post)),
+                                packing.pack_b(lw["mlp.down_proj.weight"]),
+                                ln_in.contiguous(), ln_post.contiguous())
         return LayerWeights(None, None, None, None, lw["input_layernorm.weight"],
                             lw["post_attention_layernorm.weight"], raw=lw)
 
@@ -200,8 +204,8 @@ class StageEngine:
             self.buf_q = torch.zeros((R, cfg.q_size), dtype=bf, device=dev)
             self.buf_attn = torch.zeros((R, cfg.q_size), dtype=bf, device=dev)
             self.buf_act = torch.zeros((R, I), dtype=bf, device=dev)
-            self.decode_nsplit = int(min(16, max(1, ceil_div(self.max_seq, 256))))
-            ws_rows = max(self.DECODE_MAX_ROWS * self.decode_nsplit, R * 4)
+            self.max_decode_nsplit = int(min(16, max(1, ceil_div(self.max_seq, 256))))
+            ws_rows = max(self.DECODE_MAX_ROWS * self.max_decode_nsplit, R * 4)
             self.part_o = torch.zeros(ws_rows * cfg.num_attention_heads * hd, dtype=torch.float32, device=dev)
             self.part_lse = torch.zeros(ws_rows * cfg.num_attention_heads, dtype=torch.float32, device=dev)
             self.ws_rows = ws_rows
@@ -276,7 +280,7 @@ class StageEngine:
                 keys.zero_()
                 ep = hip.make_epi(keys=keys)
                 hip.gemv(h, self.lm_head, c, self.cfg.vocab_size, self.cfg.hidden_size, hip.EPI_ARGMAX, ep,
-                         norm_w=self.final_norm, eps=self.cfg.rms_norm_eps, a_rows=idx[c0:c0 + c])
+                         norm=True, eps=self.cfg.rms_norm_eps, a_rows=idx[c0:c0 + c])
                 hip.argmax_finalize(keys, c, self.tokens)
                 out[c0:c0 + c] = self.tokens[:c].long()
             return out
@@ -290,10 +294,17 @@ class StageEngine:
         return F.linear(x, self.lm_head.float())
 
     # ------------------------------------------------------------------------- HIP path
+    def decode_nsplit(self, rows: int) -> int:
+        """Split-KV factor for a decode batch, fixed at graph capture: no split once the batch
+        alone gives >= 512 attention workgroups (measured: splitting then only adds the combine
+        launch), else aim for ~512 workgroups, chunks of >= 256 keys at max_seq."""
+        wgs = rows * self.cfg.num_key_value_heads
+        return int(max(1, min(self.max_decode_nsplit, ceil_div(512, wgs))))
+
     def _attn_nsplit(self, rows: int, kv_max: int) -> int:
         if rows <= self.DECODE_MAX_ROWS:
-            return self.decode_nsplit
-        want = max(1, min(8, ceil_div(kv_max, 512)))
+            return self.decode_nsplit(rows)
+        want = max(1, min(8, ceil_div(kv_max, 512), ceil_div(1024, rows * self.cfg.num_key_value_heads)))
         return max(1, min(want, self.ws_rows // rows))
 
     def _forward_hip(self, h, slot, pos, kv_len, rows, nsplit: Optional[int] = None) -> torch.Tensor:
@@ -318,9 +329,9 @@ class StageEngine:
             ep_qkv = hip.make_epi(out=q, k_cache=kc, v_cache=vc, slot=slot, pos=pos, cos=self.cos, sin=self.sin,
                                   ldo=q.stride(0), n_heads=nh, n_kv=nkv, head_dim=hd, t_max=self.max_seq)
             if decode:
-                hip.gemv(hbuf, lw.qkv, rows, cfg.qkv_size, H, hip.EPI_QKV, ep_qkv, norm_w=lw.ln_in, eps=eps)
+                hip.gemv(hbuf, lw.qkv, rows, cfg.qkv_size, H, hip.EPI_QKV, ep_qkv, norm=True, eps=eps)
             else:
-                hip.rmsnorm(hbuf, lw.ln_in, xn, rows, eps)
+                hip.rmsnorm(hbuf, None, xn, rows, eps, H)
                 hip.gemm(xn, lw.qkv, rows, cfg.qkv_size, H, hip.EPI_QKV, ep_qkv)
             hip.attn(q, kc, vc, slot, pos, rows, nh, nkv, hd, nsplit, self.part_o, self.part_lse, attn_o,
                      kv_len=kv_len)
@@ -328,11 +339,11 @@ class StageEngine:
             ep_gu = hip.make_epi(out=act, ldo=act.stride(0))
             if decode:
                 hip.gemv(attn_o, lw.o, rows, H, cfg.q_size, hip.EPI_RESID, ep_o)
-                hip.gemv(hbuf, lw.gate_up, rows, 2 * I, H, hip.EPI_SWIGLU, ep_gu, norm_w=lw.ln_post, eps=eps)
+                hip.gemv(hbuf, lw.gate_up, rows, 2 * I, H, hip.EPI_SWIGLU, ep_gu, norm=True, eps=eps)
                 hip.gemv(act, lw.down, rows, H, I, hip.EPI_RESID, ep_o)
             else:
                 hip.gemm(attn_o, lw.o, rows, H, cfg.q_size, hip.EPI_RESID, ep_o)
-                hip.rmsnorm(hbuf, lw.ln_post, xn, rows, eps)
+                hip.rmsnorm(hbuf, None, xn, rows, eps, H)
                 hip.gemm(xn, lw.gate_up, rows, 2 * I, H, hip.EPI_SWIGLU, ep_gu)
                 hip.gemm(act, lw.down, rows, H, I, hip.EPI_RESID, ep_o)
         return hbuf
@@ -445,11 +456,11 @@ class DecodeGraph:
             hip.embed(self.tokens, eng.embed_w, h)
         else:
             h.copy_(self.h_in)
-        eng._forward_hip(h, self.slot, self.pos, None, rows, nsplit=eng.decode_nsplit)
+        eng._forward_hip(h, self.slot, self.pos, None, rows, nsplit=eng.decode_nsplit(rows))
         if self.mode in ("full", "last"):
             ep = hip.make_epi(keys=self.keys)
             hip.gemv(h, eng.lm_head, rows, eng.cfg.vocab_size, eng.cfg.hidden_size, hip.EPI_ARGMAX, ep,
-                     norm_w=eng.final_norm, eps=eng.cfg.rms_norm_eps)
+                     norm=True, eps=eng.cfg.rms_norm_eps)
             hip.argmax_finalize(self.keys, rows, self.tokens, self.pos, 1, self.history,
                                 self.step_ctr if self.history is not None else None)
         else:

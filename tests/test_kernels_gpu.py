@@ -66,13 +66,29 @@ def test_gemv_norm_resid_tn(M):
     resid = _rnd(M, N)
     out = resid.clone()
     ref = resid.float() + _rmsnorm(x, nw, 1e-5) @ w.float().T
-    for tn in (1, 2, 4):
-        if M > 32 and tn > 2:
-            continue
+    for (tn, nwv, u) in packing.gemv_candidates(N // 16, K, M):
         out.copy_(resid)
         ep = h.make_epi(out=out, resid=out, ldo=N, ldr=N)
-        h.gemv(x, packing.pack_b(w), M, N, K, h.EPI_RESID, ep, norm_w=nw, eps=1e-5, tn=tn)
-        assert rel_err(out, ref) < 8e-3, tn
+        h.gemv(x, packing.pack_b(packing.fold_norm(w, nw)), M, N, K, h.EPI_RESID, ep, norm=True, eps=1e-5,
+               tn=tn, nw=nwv, u=u)
+        assert rel_err(out, ref) < 8e-3, (tn, nwv, u)
+
+
+@pytest.mark.parametrize("cfg", packing.GEMV_CONFIGS)
+def test_gemv_every_config(cfg):
+    """Every instantiated (tn, mb, nw, u) on shapes with uneven per-wave K splits."""
+    h = hip()
+    tn, mb, nw, u = cfg
+    N = 256
+    M = {1: 7, 2: 29, 4: 50}[mb]
+    for K in (11008, 256, 768):
+        if (K // 32) % u:
+            continue
+        x = _rnd(M, K)
+        w = _rnd(N, K, scale=0.02)
+        out = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
+        h.gemv(x, packing.pack_b(w), M, N, K, h.EPI_STORE, h.make_epi(out=out, ldo=N), tn=tn, nw=nw, u=u)
+        assert rel_err(out, x.float() @ w.float().T) < 8e-3, (cfg, K)
 
 
 @pytest.mark.parametrize("M", [1, 12, 64])
@@ -142,7 +158,7 @@ def test_gemv_argmax_with_rows(M):
     rows = torch.randint(0, 100, (M,), device=DEV, dtype=torch.int32)
     keys = torch.zeros(M, dtype=torch.int64, device=DEV)
     ep = h.make_epi(keys=keys)
-    h.gemv(hid, packing.pack_b(lm), M, V, H, h.EPI_ARGMAX, ep, norm_w=fn, eps=1e-5, a_rows=rows)
+    h.gemv(hid, packing.pack_b(packing.fold_norm(lm, fn)), M, V, H, h.EPI_ARGMAX, ep, norm=True, eps=1e-5, a_rows=rows)
     tok = torch.zeros(M, dtype=torch.int32, device=DEV)
     h.argmax_finalize(keys, M, tok)
     logits = _rmsnorm(hid[rows.long()], fn, 1e-5) @ lm.float().T
@@ -241,6 +257,8 @@ def test_embed_and_rmsnorm():
     o2 = torch.zeros_like(out)
     h.rmsnorm(out, w, o2, 37, 1e-5)
     assert rel_err(o2, _rmsnorm(out, w, 1e-5)) < 5e-3
+    h.rmsnorm(out, None, o2, 37, 1e-5, H)  # unit weight (folded into the next GEMM)
+    assert rel_err(o2, _rmsnorm(out, torch.ones_like(w), 1e-5)) < 5e-3
 
 
 def test_argmax_finalize_history_and_pos():
@@ -248,7 +266,7 @@ def test_argmax_finalize_history_and_pos():
     rows = 5
     keys = torch.zeros(rows, dtype=torch.int64, device=DEV)
     # build keys via the real kernel path: a gemv argmax on an identity-like problem
-    H, V = 64, 256
+    H, V = 128, 256
     hid = torch.zeros(rows, H, dtype=torch.bfloat16, device=DEV)
     want = torch.tensor([3, 100, 7, 255, 0])
     lm = torch.zeros(V, H, dtype=torch.bfloat16, device=DEV)
