@@ -29,7 +29,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-BASELINE_TOK_S = None  # BASELINE.json "published" is empty: no reference number to divide by
+BASELINE_TOK_S = 4.3  # only reference figure (~4.3 tok/s, start_node.py:20 comment; different HW/model)
 
 
 def parse():

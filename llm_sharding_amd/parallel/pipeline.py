@@ -25,8 +25,50 @@ from typing import Optional
 import torch
 
 from ..config import get_preset
-from ..runtime.engine import DecodeGraph, RandomSource, StageEngine
+from ..runtime.engine import DecodeGraph, EagerDecode, RandomSource, StageEngine
 from .scheduler import plan_stages
+
+
+class DistP2P:
+    """Point-to-point over torch.distributed (RCCL on GPUs, gloo on CPU)."""
+
+    def isend(self, t: torch.Tensor, dst: int):
+        import torch.distributed as dist
+        return dist.isend(t, dst)
+
+    def recv(self, t: torch.Tensor, src: int) -> None:
+        import torch.distributed as dist
+        dist.irecv(t, src).wait()
+
+
+class LocalP2P:
+    """In-process device-copy transport: several stages in ONE process (e.g. N stages on one
+    GPU, SURVEY.md §4 'local device-copy backend'). Messages are snapshot copies queued per
+    (src, dst); stages must be driven in pipeline order (see :func:`drive_local_pipeline`)."""
+
+    class _Done:
+        def wait(self):
+            return None
+
+    def __init__(self):
+        self.boxes: dict = {}
+
+    def bind(self, rank: int) -> "LocalP2P._Endpoint":
+        return LocalP2P._Endpoint(self, rank)
+
+    class _Endpoint:
+        def __init__(self, hub, rank):
+            self.hub, self.rank = hub, rank
+
+        def isend(self, t, dst):
+            self.hub.boxes.setdefault((self.rank, dst), []).append(t.clone())
+            return LocalP2P._Done()
+
+        def recv(self, t, src):
+            box = self.hub.boxes.get((src, self.rank))
+            if not box:
+                raise RuntimeError(f"local p2p: no message from stage {src} to {self.rank} (drive order?)")
+            t.copy_(box.pop(0))
 
 
 def _percentile(xs, q):
@@ -43,17 +85,20 @@ class PipelineStage:
 
     def __init__(self, cfg, rank: int, world: int, start: int, end: int, device, batch: int,
                  microbatches: int, max_seq: int, source, use_graph: bool = True,
-                 max_prefill_rows: int = 2048):
+                 max_prefill_rows: int = 2048, dtype=torch.bfloat16, p2p=None):
         self.cfg, self.rank, self.world = cfg, rank, world
+        self.p2p = p2p if p2p is not None else DistP2P()
         self.first, self.last = rank == 0, rank == world - 1
         self.B, self.M = batch, microbatches
         self.device = torch.device(device)
-        self.use_graph = use_graph
-        self.eng = StageEngine(cfg, start, end, device, torch.bfloat16, has_embed=self.first,
+        self.gpu = self.device.type == "cuda"
+        self.use_graph = use_graph and self.gpu
+        self.dtype = torch.bfloat16 if self.gpu else dtype
+        self.eng = StageEngine(cfg, start, end, device, self.dtype, has_embed=self.first,
                                has_head=self.last, source=source, max_slots=batch * microbatches,
                                max_seq=max_seq, max_prefill_rows=max(max_prefill_rows, batch))
         H = cfg.hidden_size
-        self.h_out = [torch.zeros((batch, H), dtype=torch.bfloat16, device=self.device) for _ in range(microbatches)]
+        self.h_out = [torch.zeros((batch, H), dtype=self.dtype, device=self.device) for _ in range(microbatches)]
         self.tok_out = [torch.zeros(batch, dtype=torch.int32, device=self.device) for _ in range(microbatches)]
         self.graphs: list = []
         self.send_works: dict = {}
@@ -61,19 +106,15 @@ class PipelineStage:
 
     # ---------------------------------------------------------------- p2p helpers
     def _send(self, t: torch.Tensor, dst: int, key):
-        import torch.distributed as dist
-        w = dist.isend(t, dst)
-        self.send_works[key] = w
+        self.send_works[key] = self.p2p.isend(t, dst)
 
     def _wait_send(self, key):
         w = self.send_works.pop(key, None)
         if w is not None:
             w.wait()
 
-    @staticmethod
-    def _recv(t: torch.Tensor, src: int):
-        import torch.distributed as dist
-        dist.irecv(t, src).wait()
+    def _recv(self, t: torch.Tensor, src: int):
+        self.p2p.recv(t, src)
 
     # ---------------------------------------------------------------- prefill
     def slots(self, mb: int) -> list:
@@ -82,34 +123,43 @@ class PipelineStage:
     def prefill(self, prompts: Optional[torch.Tensor], prompt_len: int) -> Optional[list]:
         """Prefill every micro-batch through the pipeline. ``prompts``: [M, B, P] int (rank 0).
         Returns (on rank 0) the first generated token per micro-batch ([B] int32 tensors)."""
-        eng, B, P, H = self.eng, self.B, prompt_len, self.cfg.hidden_size
         firsts = []
         for mb in range(self.M):
-            sl = self.slots(mb)
-            slot, pos = eng.prefill_rows(sl, [P] * B)
-            if self.first:
-                h = eng.embed(prompts[mb].reshape(-1).to(self.device))
-            else:
-                h = torch.empty((B * P, H), dtype=torch.bfloat16, device=self.device)
-                self._recv(h, self.rank - 1)
-            h = eng.forward(h, slot, pos)
-            eng.advance(sl, [P] * B)
-            if self.last:
-                tok = eng.head(h, [i * P + P - 1 for i in range(B)]).to(torch.int32)
-                if self.world > 1:
-                    self._send(tok, 0, ("pf", mb))
-                    self._wait_send(("pf", mb))
-                else:
-                    firsts.append(tok)
-            else:
-                hs = h.clone()
-                self._send(hs, self.rank + 1, ("pf", mb))
-                self._wait_send(("pf", mb))
-            if self.first and self.world > 1:
-                tok = torch.empty(B, dtype=torch.int32, device=self.device)
-                self._recv(tok, self.world - 1)
+            tok = self.prefill_mb(mb, prompts, prompt_len, recv_token=True)
+            if tok is not None:
                 firsts.append(tok)
         return firsts if self.first else None
+
+    def prefill_mb(self, mb: int, prompts, prompt_len: int, recv_token: bool = True):
+        """Prefill one micro-batch on this stage. Returns the first generated ids on the stage
+        that ends up holding them (rank 0 after the back-edge, or a single-stage pipeline)."""
+        eng, B, P, H = self.eng, self.B, prompt_len, self.cfg.hidden_size
+        sl = self.slots(mb)
+        slot, pos = eng.prefill_rows(sl, [P] * B)
+        if self.first:
+            h = eng.embed(prompts[mb].reshape(-1).to(self.device))
+        else:
+            h = torch.empty((B * P, H), dtype=self.dtype, device=self.device)
+            self._recv(h, self.rank - 1)
+        h = eng.forward(h, slot, pos)
+        eng.advance(sl, [P] * B)
+        if self.last:
+            tok = eng.head(h, [i * P + P - 1 for i in range(B)]).to(torch.int32)
+            if self.world == 1:
+                return tok
+            self._send(tok, 0, ("pf", mb))
+            self._wait_send(("pf", mb))
+        else:
+            self._send(h.clone(), self.rank + 1, ("pf", mb))
+            self._wait_send(("pf", mb))
+        if self.first and recv_token:
+            return self.recv_first_token()
+        return None
+
+    def recv_first_token(self) -> torch.Tensor:
+        tok = torch.zeros(self.B, dtype=torch.int32, device=self.device)
+        self._recv(tok, self.world - 1)
+        return tok
 
     # ---------------------------------------------------------------- decode
     def build_graphs(self, first_tokens: Optional[list], history_len: int) -> None:
@@ -117,8 +167,8 @@ class PipelineStage:
         self.mode = mode
         self.graphs = []
         for mb in range(self.M):
-            g = DecodeGraph(self.eng, self.B, mode, slots=self.slots(mb),
-                            history_len=history_len if self.last else 0)
+            cls = DecodeGraph if self.gpu else EagerDecode
+            g = cls(self.eng, self.B, mode, slots=self.slots(mb), history_len=history_len if self.last else 0)
             if first_tokens is not None and mode in ("full", "first"):
                 g.tokens.copy_(first_tokens[mb])
             if self.use_graph:
@@ -133,30 +183,34 @@ class PipelineStage:
 
     def step(self, s: int, events: Optional[list] = None) -> None:
         """One decode step for every micro-batch (the host never blocks on the GPU here)."""
-        for mb, g in enumerate(self.graphs):
-            if self.world > 1:
-                if self.first:
-                    if not self.tokens_ready[mb]:
-                        self._recv(g.tokens, self.world - 1)
-                    self.tokens_ready[mb] = False
-                else:
-                    self._recv(g.h_in, self.rank - 1)
-            self._run_mb(g)
-            if events is not None:
-                ev = torch.cuda.Event(enable_timing=True)
-                ev.record()
-                events.append((s, mb, ev))
-            if self.world > 1:
-                if self.last:
-                    # the next replay rewrites g.tokens: send from a private copy, reused only
-                    # after the previous send of this micro-batch completed
-                    self._wait_send(("tok", mb))
-                    self.tok_out[mb].copy_(g.tokens)
-                    self._send(self.tok_out[mb], 0, ("tok", mb))
-                else:
-                    self._wait_send(("h", mb))
-                    self.h_out[mb].copy_(g.out_hidden)
-                    self._send(self.h_out[mb], self.rank + 1, ("h", mb))
+        for mb in range(self.M):
+            self.step_mb(s, mb, events)
+
+    def step_mb(self, s: int, mb: int, events: Optional[list] = None) -> None:
+        g = self.graphs[mb]
+        if self.world > 1:
+            if self.first:
+                if not self.tokens_ready[mb]:
+                    self._recv(g.tokens, self.world - 1)
+                self.tokens_ready[mb] = False
+            else:
+                self._recv(g.h_in, self.rank - 1)
+        self._run_mb(g)
+        if events is not None and self.gpu:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            events.append((s, mb, ev))
+        if self.world > 1:
+            if self.last:
+                # the next replay rewrites g.tokens: send from a private copy, reused only
+                # after the previous send of this micro-batch completed
+                self._wait_send(("tok", mb))
+                self.tok_out[mb].copy_(g.tokens)
+                self._send(self.tok_out[mb], 0, ("tok", mb))
+            else:
+                self._wait_send(("h", mb))
+                self.h_out[mb].copy_(g.out_hidden.reshape(self.h_out[mb].shape))
+                self._send(self.h_out[mb], self.rank + 1, ("h", mb))
 
     def drain(self):
         """End of a phase: stage 0 collects the token ids the last stage produced in the final
@@ -168,6 +222,78 @@ class PipelineStage:
                     self.tokens_ready[mb] = True
         for k in list(self.send_works):
             self._wait_send(k)
+
+
+def run_pipeline_generate(cfg, source, prompts: Optional[torch.Tensor], n_new: int, rank: int, world: int,
+                          device="cpu", batch: int = 1, microbatches: int = 1, max_seq: int = 256,
+                          plan=None, dtype=torch.float32) -> Optional[torch.Tensor]:
+    """Greedy generation through the micro-batched pipeline (torch.distributed already
+    initialised; gloo on CPU or nccl/RCCL on GPUs). ``prompts`` [M, B, P] on rank 0.
+    Returns [n_new, M, B] generated ids on rank 0 (gathered from the last stage)."""
+    import torch.distributed as dist
+    plan = plan or plan_stages(cfg, world)
+    st = plan.stages[rank]
+    P = int(prompts.shape[-1]) if prompts is not None else 0
+    if world > 1:
+        pl = torch.tensor([P], dtype=torch.int64)
+        dist.broadcast(pl, 0)
+        P = int(pl[0])
+    stage = PipelineStage(cfg, rank, world, st.start, st.end, device, batch, microbatches, max_seq, source,
+                          use_graph=True, max_prefill_rows=batch * P, dtype=dtype)
+    firsts = stage.prefill(prompts, P)
+    stage.build_graphs(firsts, history_len=n_new - 1)
+    for s in range(n_new - 1):
+        stage.step(s)
+    stage.drain()
+    if stage.gpu:
+        torch.cuda.synchronize()
+    out = None
+    if stage.last:
+        hist = torch.stack([g.history for g in stage.graphs], dim=1).cpu()  # [n_new-1, M, B]
+        out = hist
+    if world > 1:
+        if stage.last:
+            dist.send(out.contiguous(), 0) if rank != 0 else None
+        if rank == 0 and not stage.last:
+            out = torch.zeros((n_new - 1, microbatches, batch), dtype=torch.int32)
+            dist.recv(out, world - 1)
+    if rank == 0:
+        first = torch.stack([f.cpu() for f in firsts], dim=0)[None]  # [1, M, B]
+        return torch.cat([first, out], dim=0)
+    return None
+
+
+def drive_local_pipeline(cfg, source, prompts: torch.Tensor, n_new: int, n_stages: int, device,
+                         batch: int = 1, microbatches: int = 1, max_seq: int = 256, plan=None,
+                         dtype=torch.bfloat16, use_graph: bool = True) -> torch.Tensor:
+    """All stages of a pipeline in ONE process (one device), connected by :class:`LocalP2P`
+    and driven in pipeline order. Same PipelineStage code as the multi-process RCCL path."""
+    if n_stages < 2:
+        raise ValueError("drive_local_pipeline needs >= 2 stages (use run_pipeline_generate for 1)")
+    plan = plan or plan_stages(cfg, n_stages)
+    hub = LocalP2P()
+    P = int(prompts.shape[-1])
+    stages = [PipelineStage(cfg, r, n_stages, st.start, st.end, device, batch, microbatches, max_seq, source,
+                            use_graph=use_graph, max_prefill_rows=batch * P, dtype=dtype, p2p=hub.bind(r))
+              for r, st in enumerate(plan.stages)]
+    firsts = []
+    for mb in range(microbatches):
+        for st in stages:
+            st.prefill_mb(mb, prompts if st.first else None, P, recv_token=False)
+        firsts.append(stages[0].recv_first_token())
+    for st in stages:
+        st.build_graphs(firsts if st.first else None, history_len=n_new - 1)
+    for s in range(n_new - 1):
+        for mb in range(microbatches):
+            for st in stages:
+                st.step_mb(s, mb)
+    for st in stages:
+        st.drain()
+    if stages[0].gpu:
+        torch.cuda.synchronize()
+    hist = torch.stack([g.history for g in stages[-1].graphs], dim=1).cpu()
+    first = torch.stack([f.cpu() for f in firsts], dim=0)[None]
+    return torch.cat([first, hist], dim=0)
 
 
 def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int = 64, warmup: int = 8,

@@ -499,3 +499,43 @@ class DecodeGraph:
         p = self.pos.tolist()
         for s, v in zip(self.slots, p):
             self.eng.seq_len[s] = int(v)
+
+
+class EagerDecode:
+    """Same interface as :class:`DecodeGraph` for devices without graphs (the CPU torch path
+    used by the multi-process gloo tests): one decode step per ``_body()`` call."""
+
+    def __init__(self, eng: StageEngine, rows: int, mode: str, slots: Optional[list] = None,
+                 history_len: int = 0):
+        self.eng, self.rows, self.mode = eng, rows, mode
+        self.slots = list(range(rows)) if slots is None else list(slots)
+        self.tokens = torch.zeros(rows, dtype=torch.int32)
+        self.h_in = torch.zeros((rows, eng.cfg.hidden_size), dtype=eng.dtype)
+        self.history = torch.zeros((history_len, rows), dtype=torch.int32) if history_len else None
+        self.step = 0
+        self._out = None
+
+    def _body(self) -> None:
+        eng = self.eng
+        h = eng.embed(self.tokens) if self.mode in ("full", "first") else self.h_in
+        slot, pos = eng.prefill_rows(self.slots, [1] * self.rows)
+        h = eng.forward(h, slot, pos)
+        eng.advance(self.slots, [1] * self.rows)
+        if self.mode in ("full", "last"):
+            self.tokens.copy_(eng.head(h).to(torch.int32))
+            if self.history is not None and self.step < self.history.shape[0]:
+                self.history[self.step] = self.tokens
+            self.step += 1
+        self._out = h
+
+    replay = _body
+
+    def capture(self, warmup: bool = True) -> "EagerDecode":
+        return self
+
+    @property
+    def out_hidden(self) -> torch.Tensor:
+        return self._out
+
+    def sync_positions(self) -> None:
+        pass

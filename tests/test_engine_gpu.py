@@ -113,3 +113,18 @@ def test_decode_graph_matches_eager():
     assert graph == eager
     dg.sync_positions()
     assert e2.seq_len == e1.seq_len
+
+
+@pytest.mark.parametrize("n_stages", [2, 4])
+def test_multistage_on_one_gpu_graphs(n_stages):
+    """The pipelined micro-batch decode (hipGraph per stage/micro-batch, local device-copy
+    hand-off) generates exactly what the single-stage graph loop generates."""
+    from llm_sharding_amd.parallel.pipeline import drive_local_pipeline, run_pipeline_generate
+    cfg = tiny(layers=8)
+    src = RandomSource(cfg, seed=21)
+    g = torch.Generator().manual_seed(5)
+    prompts = torch.randint(3, cfg.vocab_size, (3, 4, 9), generator=g)
+    single = run_pipeline_generate(cfg, src, prompts, 10, 0, 1, device=DEV, batch=4, microbatches=3, max_seq=64,
+                                   dtype=torch.bfloat16)
+    multi = drive_local_pipeline(cfg, src, prompts, 10, n_stages, DEV, batch=4, microbatches=3, max_seq=64)
+    assert multi.tolist() == single.tolist()
