@@ -1,0 +1,482 @@
+"""Reference-compatible pipeline-stage runtime and node control plane.
+
+API parity with ``/root/reference/utils/node_worker.py``:
+
+* :class:`Communicator` (re-exported, C1 ``:13-67``) - native TCP PUSH/PULL, in-memory framing.
+* :class:`NodeWorker` (C2 ``:70-382``) - ``load_shards``, ``receive_user_request``,
+  ``pass_through_shard``, ``receive_next_token``, ``clear_KV_cache``, the clear-KV ring command
+  builders/predicates and the ``CLEAR_KV_CACHE_*`` constants, with the same message dicts
+  (``input_token_info``, ``next_state_info``, next-token Tensor).
+* :class:`NodeController` (C3 ``:385-559``) - config receive on ``tcp://*:<listen_port>``, the
+  worker event loop with the reference's dispatch rules, hot re-configuration, request
+  forwarding to the chain head.
+
+MI355X-native underneath: the stage forward is a :class:`StageEngine` (fused HIP kernels,
+packed weights, static KV cache, fused final-norm/lm_head/argmax) instead of HF modules and a
+``DynamicCache``. Reference quirks fixed on purpose: causal prefill by
+default (Q1, ``noncausal_prefill=True`` restores the unmasked reference behaviour); batch > 1
+(Q2: next tokens embed to ``[B, 1, H]``); lm_head only on the last position (Q3); EOS by id as
+well as by string (Q4); no disk staging (Q5); blocking receive with timeout instead of a busy
+poll (Q6); a real request ingress (Q7: ``{"command": "user_request", ...}`` on the config port,
+or :meth:`NodeController.receive_request`); no AttributeError when a non-ingress node keeps
+its role (Q8); sockets closed on a role change (Q9).
+
+On ROCm devices the engine computes in bfloat16: ``dtype=torch.float16`` is accepted (the
+reference default) and mapped to bfloat16 with a notice.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+from typing import Optional
+
+import torch
+
+from ..config import LlamaConfig
+from ..models.rope import full_cos_sin
+from ..models.tokenizer import load_tokenizer
+from ..parallel import protocol
+from ..parallel.communicator import Again, Communicator
+from ..parallel.transport import PullSocket, PushSocket, parse_addr
+from ..runtime.engine import ShardFolderSource, StageEngine, WeightSource
+from .forwarding_utils import build_position_ids
+
+
+def _log(msg: str) -> None:
+    print(msg, flush=True)
+
+
+class _EngineKV:
+    """``past_key_value`` view of the worker's static cache (``get_seq_length``)."""
+
+    def __init__(self, worker: "NodeWorker"):
+        self.w = worker
+
+    def get_seq_length(self, layer_idx: int = 0) -> int:
+        return 0 if self.w.engine is None else int(self.w.engine.seq_len[0])
+
+
+class NodeWorker:
+    CLEAR_KV_CACHE_COMMAND = "clear_KV_cache"
+    CLEAR_KV_CACHE_ORIGIN_KEY = "origin_node"
+
+    def __init__(self, src_addr: str, dst_addr: str, can_receive_user_request: bool, shards_path: str,
+                 device="cpu", dtype=torch.float16, backend: str = "tcp", max_batch: int = 8,
+                 max_seq: int = 4096, noncausal_prefill: bool = False,
+                 source: Optional[WeightSource] = None, verbose: bool = True):
+        self.communicator = Communicator(src_addr=src_addr, dst_addr=dst_addr, backend=backend)
+        self.can_receive_user_request = can_receive_user_request
+        self.shards_path = shards_path
+        self.device = torch.device(device)
+        if self.device.type == "cuda" and dtype != torch.bfloat16:
+            if verbose:
+                _log(f"[INFO] {dtype} requested on {self.device}: the MI355X kernels compute in torch.bfloat16")
+            dtype = torch.bfloat16
+        self.dtype = dtype
+        self.config = LlamaConfig.from_pretrained(shards_path)
+        self.layer_num = self.config.num_hidden_layers
+        self.max_batch, self.max_seq = max_batch, max_seq
+        self.noncausal_prefill = noncausal_prefill
+        self.source = source or ShardFolderSource(shards_path, self.config)
+        self.verbose = verbose
+
+        self.tokenizer = None
+        self.embed_tokens = None   # embedding table [V, H] (ingress / head stage)
+        self.engine: Optional[StageEngine] = None
+        self.rope = None           # (cos, sin) tables [max_pos, Hd/2] (every stage)
+        self.shard = None          # alias of the engine (reference attribute name)
+        self.lm_head = None
+        self.past_key_value = None
+        self.start = 0
+        self.end = 0
+        self.batch_size = 0
+        if can_receive_user_request:
+            self.generated_ids: list = []
+            self._load_embedding()
+            self.input_token_length = None
+
+    # ------------------------------------------------------------------ loading
+    def _load_embedding(self) -> None:
+        if self.verbose:
+            _log("[INFO] loading tokenizer...")
+        self.tokenizer = load_tokenizer(self.shards_path)
+        if self.verbose:
+            _log("[INFO] loading embedding layer...")
+        self.embed_tokens = self.source.embedding(self.device, self.dtype).contiguous()
+        if self.verbose:
+            _log("[INFO] embedding layer loaded.")
+
+    def load_shards(self, start: int, end: int) -> None:
+        if start < 0 or start >= end or end > self.layer_num:
+            raise ValueError("[ERROR] start or end is invalid")
+        self.start, self.end = start, end
+        self.engine = self.shard = self.lm_head = None
+        if self.device.type == "cuda":
+            torch.cuda.empty_cache()
+        if self.verbose:
+            _log(f"[INFO] loading hidden layer {start}~{end}(end excluded)...")
+        self.engine = StageEngine(self.config, start, end, self.device, self.dtype,
+                                  has_embed=False, has_head=(end == self.layer_num), source=self.source,
+                                  max_slots=self.max_batch, max_seq=self.max_seq,
+                                  causal=not self.noncausal_prefill)
+        self.shard = self.engine
+        self.rope = (self.engine.cos, self.engine.sin)
+        self.lm_head = self.engine.lm_head
+        self.past_key_value = _EngineKV(self)
+        if self.verbose:
+            _log(f"[INFO] hidden layer {start}~{end}(end excluded) loaded.")
+
+    # ------------------------------------------------------------------ helpers
+    def _embed(self, ids: torch.Tensor) -> torch.Tensor:
+        ids = ids.to(self.device)
+        if self.device.type == "cuda":
+            from ..ops import hip
+            flat = ids.reshape(-1).to(torch.int32)
+            out = torch.empty((flat.numel(), self.config.hidden_size), dtype=torch.bfloat16, device=self.device)
+            hip.embed(flat, self.embed_tokens, out)
+            return out.reshape(*ids.shape, -1)
+        return torch.nn.functional.embedding(ids.long(), self.embed_tokens)
+
+    # ------------------------------------------------------------------ ingress
+    @torch.inference_mode()
+    def receive_user_request(self, request: str = "Write a poem about the blue sky.",
+                             input_ids: Optional[torch.Tensor] = None) -> dict:
+        if not self.can_receive_user_request:
+            raise RuntimeError("[ERROR] this node does not have embedding layer while receiving user request.")
+        if input_ids is None:
+            if self.verbose:
+                _log("[INFO] input: " + request)
+            input_ids = self.tokenizer(request, return_tensors="pt")["input_ids"]
+        else:
+            if input_ids.ndim != 2:
+                raise ValueError("[ERROR] input_ids must be a 2D tensor with shape [batch_size, seq_len].")
+            if self.verbose:
+                _log("[INFO] input: inputted from direct token ids.")
+        input_ids = input_ids.to(dtype=torch.long)
+        self.input_token_length = int(input_ids.shape[1])
+        if self.verbose:
+            _log("[INFO] input token number: " + str(self.input_token_length))
+        self.generated_ids = [input_ids.cpu()]
+        hidden_states = self._embed(input_ids)
+        B, S = int(input_ids.shape[0]), int(input_ids.shape[1])
+        self.batch_size = B
+        return {"hidden_states": hidden_states, "batch_size": B, "seq_len": S}
+
+    # ------------------------------------------------------------------ stage forward
+    @torch.inference_mode()
+    def pass_through_shard(self, state_info: dict):
+        if self.engine is None:
+            raise RuntimeError("[ERROR] no shard loaded")
+        if self.is_input_token_info(state_info):
+            if self.start != 0:
+                raise RuntimeError("[ERROR] after embedding layer, the states should first passing hidden layer 0!")
+            self.batch_size = int(state_info["batch_size"])
+        elif self.is_next_state_info(state_info):
+            pass  # positions come from this stage's own KV length (same values as shipped cos/sin)
+        else:
+            attrs = [a for a in dir(state_info) if not a.startswith("__")]
+            raise RuntimeError(f"[ERROR] Received unknown state_info type: {type(state_info)}; "
+                               f"Attributes: {attrs if attrs else 'No attributes found'}")
+        hs = state_info["hidden_states"]
+        B, S, H = hs.shape
+        if B > self.max_batch:
+            raise ValueError(f"[ERROR] batch {B} exceeds max_batch={self.max_batch}")
+        eng = self.engine
+        past = eng.seq_len[0]
+        slots = list(range(B))
+        slot, pos = eng.prefill_rows(slots, [S] * B)
+        kv_len = [past + S] * (B * S) if (self.noncausal_prefill and S > 1) else None
+        h = eng.forward(hs.reshape(B * S, H).to(self.device, eng.dtype), slot, pos, kv_len=kv_len)
+        eng.advance(slots, [S] * B)
+        if self.end == self.layer_num:
+            return eng.head(h, [b * S + S - 1 for b in range(B)]).to("cpu", torch.long)
+        position_ids = torch.arange(past, past + S, dtype=torch.long)[None].expand(B, S)
+        cos, sin = full_cos_sin(eng.cos.cpu(), eng.sin.cpu(), position_ids, dtype=eng.dtype)
+        return {"hidden_states": h.reshape(B, S, H).clone(), "cos": cos, "sin": sin}
+
+    # ------------------------------------------------------------------ autoregression
+    @torch.inference_mode()
+    def receive_next_token(self, next_token_id: torch.Tensor, max_new_tokens: int = 1024) -> tuple:
+        if not self.can_receive_user_request:
+            raise RuntimeError('[ERROR] this node does not store the "generated token id" list, but received a next_token_id.')
+        next_token_id = next_token_id.reshape(-1).to("cpu", torch.long)
+        self.generated_ids.append(next_token_id.unsqueeze(-1))
+        tid = int(next_token_id[0])
+        next_token = self.tokenizer.decode(tid)
+        if self.verbose:
+            print(repr(next_token), end=" ", flush=True)
+        eos_ids = set(self.config.eos_ids)
+        if getattr(self.tokenizer, "eos_token_id", None) is not None:
+            eos_ids.add(int(self.tokenizer.eos_token_id))
+        reached_eos = next_token == getattr(self.tokenizer, "eos_token", None) or bool(
+            all(int(t) in eos_ids for t in next_token_id))
+        reached_max = len(self.generated_ids) > max_new_tokens
+        if reached_eos or reached_max:
+            if self.verbose:
+                print()
+                final_ids = torch.cat(self.generated_ids, dim=-1)
+                _log("output: " + self.tokenizer.decode(final_ids[0]))
+                _log("\n[INFO] output token number: " + str(len(self.generated_ids) - 1))
+            return True, None
+        hidden_states = self._embed(next_token_id.unsqueeze(-1))  # [B, 1, H]
+        return False, {"hidden_states": hidden_states, "batch_size": self.batch_size, "seq_len": 1}
+
+    def output_ids(self) -> torch.Tensor:
+        return torch.cat(self.generated_ids, dim=-1)
+
+    # ------------------------------------------------------------------ protocol predicates
+    @staticmethod
+    def is_input_token_info(data) -> bool:
+        return isinstance(data, dict) and "batch_size" in data and "seq_len" in data
+
+    @staticmethod
+    def is_next_state_info(data) -> bool:
+        return isinstance(data, dict) and "cos" in data and "sin" in data
+
+    def clear_KV_cache(self) -> None:
+        """Reset the per-request state; weights stay resident (reference ``:319-355``)."""
+        if self.engine is not None:
+            self.engine.reset()
+        self.batch_size = 0
+        if self.can_receive_user_request:
+            self.generated_ids = []
+            self.input_token_length = None
+        if self.verbose:
+            _log("\n[INFO] KV cache and all states caused by prev user are cleared.")
+
+    def _get_clear_KV_cache_origin(self) -> dict:
+        return {"src_addr": self.communicator.src_addr, "dst_addr": self.communicator.dst_addr,
+                "shards_start": self.start, "shards_end": self.end}
+
+    def build_clear_KV_cache_command(self) -> dict:
+        return {"command": self.CLEAR_KV_CACHE_COMMAND,
+                self.CLEAR_KV_CACHE_ORIGIN_KEY: self._get_clear_KV_cache_origin()}
+
+    @classmethod
+    def is_clear_KV_cache_command(cls, data) -> bool:
+        return isinstance(data, dict) and data.get("command") == cls.CLEAR_KV_CACHE_COMMAND
+
+    def is_clear_KV_cache_command_origin(self, data) -> bool:
+        return (self.is_clear_KV_cache_command(data)
+                and data.get(self.CLEAR_KV_CACHE_ORIGIN_KEY) == self._get_clear_KV_cache_origin())
+
+    def close(self) -> None:
+        self.communicator.close()
+
+
+CONFIG_KEYS = ("src_addr", "dst_addr", "can_receive_user_request", "first_node_addr", "shards_start", "shards_end")
+
+
+class NodeController:
+    """Node-side control plane (reference C3). Config JSON arrives on ``tcp://*:listen_port``."""
+
+    def __init__(self, shards_path: str, device, dtype=torch.float16, listen_port: int = 40700,
+                 backend: str = "tcp", wait_config: bool = True, config: Optional[dict] = None,
+                 worker_kwargs: Optional[dict] = None, poll_ms: int = 20, verbose: bool = True):
+        self.shards_path = shards_path
+        self.device = device
+        self.dtype = dtype
+        self.backend = backend
+        self.poll_ms = poll_ms
+        self.verbose = verbose
+        self.worker_kwargs = dict(worker_kwargs or {})
+        self.listen_addr = "tcp://*:" + str(listen_port)
+        self.recv_config_socket = PullSocket(self.listen_addr)
+        self.listen_port = self.recv_config_socket.port
+        self.send_request_socket = None
+        self.first_node_addr = ""
+        self.pending_requests: list = []
+        self.running = False
+        self.finished_outputs: list = []
+        self.node_worker: Optional[NodeWorker] = None
+        self.received_config = config if config is not None else (self._receive_config() if wait_config else None)
+        if self.received_config is not None:
+            self._apply_new_role(self.received_config)
+            if self.verbose:
+                _log("[INFO] Node is ready.")
+
+    # ------------------------------------------------------------------ config
+    def _receive_config(self, no_block: bool = False) -> Optional[dict]:
+        while True:
+            if no_block:
+                try:
+                    raw = self.recv_config_socket.recv_bytes(0)
+                except Again:
+                    return None
+            else:
+                if self.verbose:
+                    _log("[CONFIG] Waiting for configuration file from master node...")
+                raw = self.recv_config_socket.recv_bytes(-1)
+            msg = json.loads(raw.decode())
+            if isinstance(msg, dict) and msg.get("command") in ("user_request", "shutdown"):
+                self._handle_command(msg)
+                if no_block:
+                    continue
+                continue
+            if self.verbose:
+                _log("[CONFIG] Received configuration file from master node:")
+                for k, v in msg.items():
+                    _log(f"  - {k}: {v}")
+            return msg
+
+    def _handle_command(self, msg: dict) -> None:
+        if msg["command"] == "shutdown":
+            self.running = False
+        elif msg["command"] == "user_request":
+            self.pending_requests.append(msg)
+
+    def _apply_new_role(self, cfg: dict) -> None:
+        for k in CONFIG_KEYS:
+            if k not in cfg:
+                raise KeyError(f"[ERROR] configuration misses {k!r}")
+        if self.node_worker is not None:
+            self.node_worker.close()  # Q9: release the old sockets before rebinding
+            self.node_worker = None
+        self._set_first_node_addr(cfg)
+        self.node_worker = NodeWorker(cfg["src_addr"], cfg["dst_addr"], cfg["can_receive_user_request"],
+                                      self.shards_path, device=self.device, dtype=self.dtype, backend=self.backend,
+                                      verbose=self.verbose, **self.worker_kwargs)
+        self.node_worker.load_shards(cfg["shards_start"], cfg["shards_end"])
+
+    def _set_first_node_addr(self, cfg: dict) -> None:
+        new = cfg.get("first_node_addr", "") if cfg.get("can_receive_user_request") else ""
+        if new != self.first_node_addr:
+            if self.send_request_socket is not None:
+                self.send_request_socket.close()
+                self.send_request_socket = None
+            if new:
+                self.send_request_socket = PushSocket(new)
+            self.first_node_addr = new
+
+    def _change_first_node_addr(self, new_first_node_addr: str) -> str:
+        self._set_first_node_addr({"can_receive_user_request": True, "first_node_addr": new_first_node_addr})
+        return self.first_node_addr
+
+    def check_new_config(self) -> None:
+        new = self._receive_config(no_block=True)
+        if not new:
+            return
+        old = self.received_config or {}
+        w = self.node_worker
+        if w is None or new["can_receive_user_request"] != old.get("can_receive_user_request"):
+            self._apply_new_role(new)
+        else:
+            w.communicator.change_src_addr(new["src_addr"])
+            w.communicator.change_dst_addr(new["dst_addr"])
+            self._set_first_node_addr(new)  # Q8: no-op for non-ingress nodes
+            if (new["shards_start"], new["shards_end"]) != (w.start, w.end):
+                w.load_shards(new["shards_start"], new["shards_end"])
+            else:
+                w.clear_KV_cache()
+        self.received_config = new
+        if self.verbose:
+            _log("[INFO] The new configuration node is ready.")
+
+    # ------------------------------------------------------------------ requests
+    def _forward_request(self, data: dict, data_path: str = "results/send_request.pt", keep_data: bool = False):
+        payload = protocol.encode(data)
+        self.send_request_socket.send_bytes(payload)
+        if keep_data:
+            os.makedirs(os.path.dirname(data_path) or ".", exist_ok=True)
+            with open(data_path, "wb") as f:
+                f.write(payload)
+            return data_path
+        return None
+
+    def receive_request(self, request: str = "Write a poem about the blue sky.",
+                        input_ids: Optional[torch.Tensor] = None) -> None:
+        if not self.node_worker.can_receive_user_request:
+            raise RuntimeError("[ERROR] this node cannot receive user request.")
+        token_info = self.node_worker.receive_user_request(request, input_ids=input_ids)
+        if self.send_request_socket is None:
+            raise RuntimeError("[ERROR] no first_node_addr configured for request forwarding")
+        self._forward_request(token_info)
+
+    # ------------------------------------------------------------------ loop
+    def process_one(self, received_data, max_new_tokens: int = 1024) -> bool:
+        """Dispatch one data-plane message (reference ``run_worker_loop`` body). Returns True
+        if something was forwarded down the chain."""
+        w = self.node_worker
+        if w.is_clear_KV_cache_command(received_data):
+            if not w.is_clear_KV_cache_command_origin(received_data):
+                w.communicator.transfer_data(received_data)
+                w.clear_KV_cache()
+            return False
+        if isinstance(received_data, torch.Tensor):
+            if w.start != 0:
+                raise RuntimeError('[ERROR] I\'m not the first node in the model chain, but received "next_token_id".')
+            reached_end, received_data = w.receive_next_token(received_data, max_new_tokens)
+            if reached_end:
+                self.finished_outputs.append(w.output_ids())
+                w.communicator.transfer_data(w.build_clear_KV_cache_command())
+                w.clear_KV_cache()
+                return False
+        elif w.is_input_token_info(received_data):
+            if w.start != 0:
+                raise RuntimeError('[ERROR] I\'m not the first node in the model chain, but received "input_token_info".')
+        elif w.is_next_state_info(received_data):
+            if w.start == 0:
+                raise RuntimeError('[ERROR] I\'m the first node in the model chain, but received "next_state_info".')
+        else:
+            attrs = [a for a in dir(received_data) if not a.startswith("__")]
+            raise RuntimeError(f"[ERROR] Received unknown data type: {type(received_data)}; "
+                               f"Attributes: {attrs if attrs else 'No attributes found'}")
+        processed = w.pass_through_shard(received_data)
+        w.communicator.transfer_data(processed)
+        if w.start != 0 and self.verbose:
+            print("*", end=" ", flush=True)
+        return True
+
+    def run_worker_loop(self, max_new_tokens: int = 1024, max_idle_s: Optional[float] = None) -> None:
+        """Serve until a ``shutdown`` command arrives (or ``max_idle_s`` without traffic)."""
+        self.running = True
+        idle_since = time.monotonic()
+        while self.running:
+            try:
+                data = self.node_worker.communicator.receive_data(timeout_ms=self.poll_ms)
+                idle_since = time.monotonic()
+                self.process_one(data, max_new_tokens)
+            except Again:
+                pass
+            while self.pending_requests and self.node_worker.can_receive_user_request:
+                req = self.pending_requests.pop(0)
+                ids = torch.tensor(req["input_ids"]) if req.get("input_ids") is not None else None
+                self.receive_request(req.get("text", ""), input_ids=ids)
+                idle_since = time.monotonic()
+            self.check_new_config()
+            if max_idle_s is not None and time.monotonic() - idle_since > max_idle_s:
+                break
+        self.running = False
+
+    def close(self) -> None:
+        if self.node_worker is not None:
+            self.node_worker.close()
+        if self.send_request_socket is not None:
+            self.send_request_socket.close()
+        self.recv_config_socket.close()
+
+
+def send_user_request(node_ip: str, port: int, text: str = "", input_ids=None, max_new_tokens: int = None) -> None:
+    """Client helper: submit a request to an ingress NodeController's config port (fixes Q7)."""
+    msg = {"command": "user_request", "text": text}
+    if input_ids is not None:
+        msg["input_ids"] = [list(map(int, r)) for r in (input_ids.tolist() if hasattr(input_ids, "tolist") else input_ids)]
+    s = PushSocket(f"tcp://{node_ip}:{port}")
+    s.send_bytes(json.dumps(msg).encode())
+    s.close(linger_ms=5000)
+
+
+def send_shutdown(node_ip: str, port: int) -> None:
+    s = PushSocket(f"tcp://{node_ip}:{port}")
+    s.send_bytes(json.dumps({"command": "shutdown"}).encode())
+    s.close(linger_ms=5000)
+
+
+__all__ = ["Communicator", "NodeWorker", "NodeController", "send_user_request", "send_shutdown", "Again"]
+
+
+if __name__ == "__main__":
+    shards = sys.argv[1] if len(sys.argv) > 1 else "shards/Llama-2-7b-chat-hf_float16"
+    NodeController(shards, device="cuda:0" if torch.cuda.is_available() else "cpu", dtype=torch.bfloat16).run_worker_loop()
