@@ -111,12 +111,25 @@ def save_tensor_dict(d: dict, path: str) -> None:
     torch.save({k: v.contiguous() for k, v in d.items()}, path)
 
 
+def dequantize(d: dict) -> dict:
+    """FP8 shards (ModelSharder dtype=float8_e4m3fn): ``w * w_scale[:, None]`` -> bf16."""
+    out = {}
+    for k, v in d.items():
+        if k.endswith("_scale"):
+            continue
+        s = d.get(k + "_scale")
+        if s is not None:
+            v = (v.float() * s.float()[:, None].to(v.device)).to(torch.bfloat16)
+        out[k] = v
+    return out
+
+
 def load_tensor_dict(path: str, device="cpu") -> dict:
     st = os.path.splitext(path)[0] + ".safetensors"
     if os.path.exists(st):
         from safetensors.torch import load_file
-        return load_file(st, device=str(device))
-    return torch.load(path, map_location=device, weights_only=True)
+        return dequantize(load_file(st, device=str(device)))
+    return dequantize(torch.load(path, map_location=device, weights_only=True))
 
 
 def load_block(shards_path: str, i: int, device="cpu", dtype=None) -> dict:

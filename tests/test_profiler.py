@@ -1,0 +1,109 @@
+"""NodeProfiler on CPU with a tiny model: sweeps, fits, similarity, assisted two-device mode
+(two threads over loopback TCP), cold start, max-layer probe, golden ring runs."""
+import os
+import socket
+import threading
+
+import pytest
+import torch
+
+from llm_sharding_amd.models import weights as W
+from llm_sharding_amd.models.reference import ReferenceLlama
+from llm_sharding_amd.utils.node_profiler import NodeProfiler
+
+
+def free_ports(n):
+    socks = [socket.socket() for _ in range(n)]
+    for s in socks:
+        s.bind(("127.0.0.1", 0))
+    ps = [s.getsockname()[1] for s in socks]
+    for s in socks:
+        s.close()
+    return ps
+
+
+class QuickProfiler(NodeProfiler):
+    PROFILE_INTERVAL_SLEEP_TIME = 0
+    PROFILE_REPEAT_NUM = 2
+    PROFILE_PREFILL_INPUT_TOKEN_LENGTHS = [8, 16, 32, 64]
+    PROFILE_DECODE_OUTPUT_TOKEN_LENGTHS = [4, 8, 16]
+
+
+def test_fit_models_exact(tmp_path):
+    p = QuickProfiler.__new__(QuickProfiler)
+    p.plot_dir, p.verbose = str(tmp_path), False
+    S = [8, 16, 32, 64, 128]
+    T = [0.5 * s * s + 2 * s + 3 for s in S]
+    r = p._fit_latency_models(S, T, S, T, "x", "y", "t", "fit.png")
+    assert torch.allclose(r["quadratic_coefficients"], torch.tensor([0.5, 2.0, 3.0], dtype=torch.float64), atol=1e-6)
+    assert abs(r["quadratic_r_squared"] - 1.0) < 1e-9 and os.path.exists(r["plot"])
+    with pytest.raises(ValueError):
+        p._fit_latency_models([1, 2], [1, 2], [1], [1], "x", "y", "t", "f.png")
+
+
+def test_profile_compute_capability_full(tiny_shards, tmp_path):
+    p = QuickProfiler(tiny_shards, dtype=torch.float32, plot_dir=str(tmp_path), verbose=False)
+    r = p.profile_compute_capability(max_layer_num=-1)
+    assert len(r["prefill_latencies"]) == 4 and r["prefill_c_k"] > 0
+    assert "decode_c_k" in r and r["similarity"]["slope_ratio"] > 0
+    assert os.path.exists(os.path.join(str(tmp_path), "profile_prefill_compute_capability.png"))
+
+
+def test_assisted_profile_two_devices(tiny_shards, tmp_path):
+    a, b = free_ports(2)
+    target = QuickProfiler(tiny_shards, dtype=torch.float32, plot_dir=str(tmp_path), verbose=False)
+    assistor = QuickProfiler(tiny_shards, dtype=torch.float32, plot_dir=str(tmp_path), verbose=False)
+    res = {}
+    t = threading.Thread(target=lambda: res.update(target.profile_compute_capability(
+        max_layer_num=3, assisted=True, src_addr=f"tcp://*:{a}", dst_addr=f"tcp://127.0.0.1:{b}")))
+    t.start()
+    assistor.assist_profile_compute_capability(target_max_layer_num=3, src_addr=f"tcp://*:{b}",
+                                               dst_addr=f"tcp://127.0.0.1:{a}")
+    t.join(timeout=120)
+    assert res["loaded_layer_num"] == 2 and len(res["prefill_latencies"]) == 4
+    assert len(res["decode_cumulative_latencies"]) >= 3
+
+
+def test_cold_start_and_max_layers(tiny_shards):
+    p = QuickProfiler(tiny_shards, dtype=torch.float32, verbose=False)
+    assert p.profile_max_layer_num() == p.layer_num
+    per_layer = W.layer_shapes(p.config)
+    lim = 2.5 * sum(torch.Size(s).numel() for s in per_layer.values()) * 4 + p.config.vocab_size * 256 * 4
+    assert p.profile_max_layer_num(memory_limit_bytes=lim) < p.layer_num
+    r = p.profile_cold_start_latency(max_layer_num=-1)
+    assert r["layers"] == p.layer_num and r["cold_start_s"] > 0
+    with pytest.raises(ValueError):
+        p._resolve_assisted_target_loaded_layer_num(-1)
+
+
+def test_golden_runs_agree(tiny_shards):
+    p = QuickProfiler(tiny_shards, dtype=torch.float32, verbose=False)
+    ids = torch.tensor([[1, 60, 61, 62]])
+    solo = p.go_through_every_shards_only_by_profiler(out_token_num=6, input_ids=ids)
+    cfg, emb, layers, fn, lm = W.load_full_model(tiny_shards)
+    want = ReferenceLlama(cfg, emb, layers, fn, lm).generate(ids, 6)[0].tolist()
+    assert solo[4:] == want
+
+
+def test_go_through_every_shards_ring(tiny_shards):
+    p = QuickProfiler(tiny_shards, dtype=torch.float32, verbose=False)
+    ids = torch.tensor([[1, 60, 61, 62]])
+    ports = free_ports(4)
+    base = min(ports)
+    # find 4 consecutive free ports
+    for cand in range(base, base + 200, 7):
+        try:
+            ss = [socket.socket() for _ in range(4)]
+            for i, s in enumerate(ss):
+                s.bind(("127.0.0.1", cand + i))
+            for s in ss:
+                s.close()
+            base = cand
+            break
+        except OSError:
+            for s in ss:
+                s.close()
+    out = p.go_through_every_shards(out_token_num=6, base_port=base, input_ids=ids)
+    cfg, emb, layers, fn, lm = W.load_full_model(tiny_shards)
+    want = ReferenceLlama(cfg, emb, layers, fn, lm).generate(ids, 6)[0].tolist()
+    assert out[4:] == want
