@@ -1,0 +1,74 @@
+"""Master node: profile-driven placement + deployment of a NodeController chain.
+
+The reference README (``/root/reference/README.md:7-8``) describes a scheduling algorithm on
+the master that calls ``ConfigSender``; the repository only ships a hand-written placement
+(``send_config.py:5-44``). ``MasterNode`` closes that gap:
+
+1. devices (host, config/data ports, HBM capacity, relative speed) are described by
+   :class:`DeviceSpec` - speed factors can be taken from ``NodeProfiler`` results
+   (per-token compute capability ``c_k``, :meth:`MasterNode.speed_from_profiles`);
+2. :func:`plan_stages` picks contiguous layer ranges minimising the bottleneck stage under
+   the memory caps (exact DP);
+3. :meth:`deploy` sends the reference 6-key configs (ring chain, ingress = stage 0) through
+   ``ConfigSender``; :meth:`submit` / :meth:`shutdown` drive the deployed chain.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence
+
+from ..config import LlamaConfig
+from ..parallel.scheduler import DeviceSpec, Plan, build_chain_configs, plan_stages
+from .config_sender import ConfigSender
+from .node_worker import send_shutdown, send_user_request
+
+
+class MasterNode:
+    def __init__(self, cfg: LlamaConfig, devices: Sequence[DeviceSpec], kv_tokens: int = 4096):
+        self.cfg = cfg
+        self.devices = list(devices)
+        self.kv_tokens = kv_tokens
+        self.plan: Optional[Plan] = None
+        self.senders: List[ConfigSender] = []
+
+    @classmethod
+    def from_shards(cls, shards_path: str, devices: Sequence[DeviceSpec], kv_tokens: int = 4096) -> "MasterNode":
+        return cls(LlamaConfig.from_pretrained(shards_path), devices, kv_tokens)
+
+    @staticmethod
+    def speed_from_profiles(profiles: Sequence[dict]) -> list:
+        """Relative time multipliers from NodeProfiler results (decode c_k if present, else
+        prefill c_k); the fastest device gets 1.0."""
+        ck = [p.get("decode_c_k", p.get("prefill_c_k")) for p in profiles]
+        base = min(ck)
+        return [c / base for c in ck]
+
+    def make_plan(self) -> Plan:
+        self.plan = plan_stages(self.cfg, self.devices, kv_tokens=self.kv_tokens)
+        return self.plan
+
+    def configs(self) -> list:
+        if self.plan is None:
+            self.make_plan()
+        return build_chain_configs(self.plan)
+
+    def deploy(self, timeout_ms: int = 10000) -> list:
+        cfgs = self.configs()
+        self.senders = []
+        for st, c in zip(self.plan.stages, cfgs):
+            s = ConfigSender(node_port=st.device.config_port)
+            s.build_config(c["shards_start"], c["shards_end"], c["can_receive_user_request"], c["src_addr"],
+                           c["dst_addr"], first_node_addr=c["first_node_addr"])
+            if not s.send_config(st.device.host, timeout_ms):
+                raise TimeoutError(f"config not delivered to {st.device.host}:{st.device.config_port}")
+            self.senders.append(s)
+        return cfgs
+
+    def submit(self, text: str = "", input_ids=None) -> None:
+        ing = self.plan.stages[0].device
+        send_user_request(ing.host, ing.config_port, text=text, input_ids=input_ids)
+
+    def shutdown(self) -> None:
+        for st in self.plan.stages:
+            send_shutdown(st.device.host, st.device.config_port)
+        for s in self.senders:
+            s.close()

@@ -128,3 +128,59 @@ def test_multistage_on_one_gpu_graphs(n_stages):
                                    dtype=torch.bfloat16)
     multi = drive_local_pipeline(cfg, src, prompts, 10, n_stages, DEV, batch=4, microbatches=3, max_seq=64)
     assert multi.tolist() == single.tolist()
+
+
+def test_node_worker_chain_on_gpu(tiny_shards_bf16):
+    """Reference-API NodeWorkers on the GPU (tcp hand-off on loopback) == single-stage engine."""
+    import socket
+    from llm_sharding_amd.utils.node_worker import NodeWorker
+    socks = [socket.socket() for _ in range(2)]
+    for s in socks:
+        s.bind(("127.0.0.1", 0))
+    ports = [s.getsockname()[1] for s in socks]
+    for s in socks:
+        s.close()
+    a = NodeWorker(f"tcp://*:{ports[0]}", f"tcp://127.0.0.1:{ports[1]}", True, tiny_shards_bf16, device=DEV,
+                   dtype=torch.float16, verbose=False)
+    b = NodeWorker(f"tcp://*:{ports[1]}", f"tcp://127.0.0.1:{ports[0]}", False, tiny_shards_bf16, device=DEV,
+                   dtype=torch.float16, verbose=False)
+    a.load_shards(0, 2)
+    b.load_shards(2, 4)
+    prompt = torch.tensor([[1, 33, 44, 55, 66, 77]])
+    d = a.receive_user_request(input_ids=prompt)
+    for _ in range(6):
+        a.communicator.transfer_data(a.pass_through_shard(d))
+        x = b.communicator.receive_data(timeout_ms=10000)
+        b.communicator.transfer_data(b.pass_through_shard(x))
+        tok = a.communicator.receive_data(timeout_ms=10000)
+        end, d = a.receive_next_token(tok, max_new_tokens=6)
+        if end:
+            break
+    got = a.output_ids()[0, 6:].tolist()
+    from llm_sharding_amd.runtime.engine import ShardFolderSource
+    cfg = a.config
+    eng = StageEngine(cfg, 0, 4, DEV, torch.bfloat16, has_embed=True, has_head=True,
+                      source=ShardFolderSource(tiny_shards_bf16), max_seq=64)
+    ids, want = prompt[0], []
+    for _ in range(len(got)):
+        sl, po = eng.prefill_rows([0], [ids.numel()])
+        h = eng.forward(eng.embed(ids.to(DEV)), sl, po)
+        eng.advance([0], [ids.numel()])
+        ids = eng.head(h, [ids.numel() - 1]).cpu()
+        want.append(int(ids[0]))
+    assert got == want
+    a.close()
+    b.close()
+
+
+def test_profiler_on_gpu(tiny_shards_bf16, tmp_path):
+    from llm_sharding_amd.utils.node_profiler import NodeProfiler
+
+    class Q(NodeProfiler):
+        PROFILE_INTERVAL_SLEEP_TIME = 0
+        PROFILE_REPEAT_NUM = 2
+        PROFILE_DECODE_OUTPUT_TOKEN_LENGTHS = [8, 16, 32]
+
+    r = Q(tiny_shards_bf16, device=DEV, dtype=torch.bfloat16, plot_dir=str(tmp_path), verbose=False
+          ).profile_compute_capability(max_layer_num=-1)
+    assert r["prefill_c_k"] > 0 and len(r["decode_cumulative_latencies"]) >= 3
