@@ -184,3 +184,48 @@ def test_profiler_on_gpu(tiny_shards_bf16, tmp_path):
     r = Q(tiny_shards_bf16, device=DEV, dtype=torch.bfloat16, plot_dir=str(tmp_path), verbose=False
           ).profile_compute_capability(max_layer_num=-1)
     assert r["prefill_c_k"] > 0 and len(r["decode_cumulative_latencies"]) >= 3
+
+
+@pytest.mark.parametrize("preset", ["llama2-70b", "llama3.2-3b"])
+def test_other_families_two_layers_vs_golden(preset):
+    """Llama-2-70B (GQA 8:1, H=8192) and Llama-3.2-3B (GQA 3:1, llama3 RoPE scaling, tied
+    embeddings, 128K vocab) layer shapes through the HIP path, 2 layers, vs the fp32 golden."""
+    from llm_sharding_amd.config import get_preset
+    cfg = get_preset(preset)
+    cfg.num_hidden_layers = 2
+    if preset == "llama2-70b":
+        cfg.vocab_size = 4096  # keep the fp32 golden lm_head small; the GEMV path is shape-generic
+    cfg.max_position_embeddings = 512
+    seed = 3
+
+    class CpuGen(RandomSource):
+        def layer(self, i, device, dtype):
+            return {k: v.to(device) for k, v in W.random_layer(cfg, i, dtype, "cpu", seed).items()}
+
+        def embedding(self, device, dtype):
+            return W.random_embedding(cfg, dtype, "cpu", seed).to(device)
+
+        def final_norm(self, device, dtype):
+            return W.random_final_norm(cfg, dtype, "cpu", seed).to(device)
+
+        def lm_head(self, device, dtype):
+            return W.random_lm_head(cfg, dtype, "cpu", seed).to(device)
+
+    eng = StageEngine(cfg, 0, 2, DEV, torch.bfloat16, has_embed=True, has_head=True, source=CpuGen(cfg, seed),
+                      max_seq=256, max_prefill_rows=128)
+    ref = _ref(cfg, seed)
+    ids = torch.randint(3, cfg.vocab_size, (80,), generator=torch.Generator().manual_seed(1))
+    sl, po = eng.prefill_rows([0], [80])  # > 64 rows: MFMA GEMM prefill path
+    h = eng.forward(eng.embed(ids.to(DEV)), sl, po)
+    eng.advance([0], [80])
+    href = ref.forward_hidden(ref.embed[ids][None])[0]
+    assert rel_err(h, href) < 3e-2
+    for t in (5, 17):
+        sl, po = eng.prefill_rows([0], [1])
+        h = eng.forward(eng.embed(torch.tensor([t], device=DEV)), sl, po)
+        eng.advance([0], [1])
+        href = ref.forward_hidden(ref.embed[torch.tensor([[t]])])[0]
+        assert rel_err(h, href) < 3e-2
+    lg = ref.logits(href)
+    got = int(eng.head(h, [0])[0])
+    assert lg[0, got] >= lg[0].max() - 0.05 * lg.abs().max()
