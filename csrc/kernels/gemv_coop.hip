@@ -1,0 +1,345 @@
+// Cooperative split-K decode projection for 17..64 rows: y[M, N] = A[M, K] @ W^T.
+//
+// Why (profiles/r1_gemv_o_proj_pmc.txt): in gemv.hip every workgroup re-reads all of A from
+// L2 (waves split K inside the workgroup, so A is never shared); at M >= 32 the L1->L2 request
+// count grows ~5x over M = 1 at equal HBM bytes and issue stalls dominate. Here
+//  * the NW waves of a workgroup own NW*TNW different 16-column tiles and SHARE each A chunk
+//    (M rows x 64 k) staged once through LDS (XOR-swizzled 16-B chunks, double-buffered,
+//    register-prefetched one chunk ahead, one barrier per chunk);
+//  * every wave streams only its own packed weight fragments (buffer loads, nt), prefetched
+//    one chunk ahead in registers;
+//  * K is split over SK workgroups; each writes fp32 partial tiles (+ partial sum(x^2) for the
+//    fused RMSNorm) to a slab with write-through (sc1) stores, and the last-arriving workgroup
+//    of a column group (arrival counter, sc1 loads: the sc1 form of cdna_hip_programming.md
+//    §5 'In-launch split-K reduction' / §6 Guideline 16) sums the SK slabs in a fixed order
+//    (deterministic) and runs the fused epilogue. The arrival counter
+//    is reset by the last arriver, so the kernel is replay-safe inside hipGraphs.
+#include "epilogue.h"
+
+namespace {
+
+template <int KC>
+LSA_DEVICE int a_off(int row, int c16) { return row * (KC * 2) + ((c16 ^ (row & 7)) << 4); }
+
+template <int MB, int TNW, int NW, int KF, int EPI, bool NORM>
+__global__ __launch_bounds__(NW * 64) void gemv_coop_kernel(
+    const bf16_raw* __restrict__ x, int ldx, const int* __restrict__ a_rows, const bf16_raw* __restrict__ wp,
+    int M, int N, int K, int SK, float eps, EpiArgs ep, float* __restrict__ slab, unsigned* __restrict__ counters) {
+  constexpr int NTHR = NW * 64;
+  constexpr int KC = 32 * KF;                   // k per chunk (KF MFMA k-fragments)
+  constexpr int C16 = KC / 8;                   // 16-B pieces per A row
+  constexpr int MR = 16 * MB;
+  constexpr int TG = NW * TNW;                  // 16-col tiles per workgroup
+  constexpr int ABUF = MR * KC * 2;             // bytes per A buffer
+  constexpr int RED = TG * MR * 16 * 4;         // fp32 reduction tile
+  constexpr int SMEM = (2 * ABUF > RED ? 2 * ABUF : RED);
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
+  __shared__ float s_ss[MR];
+  __shared__ int s_last;
+  __shared__ unsigned long long s_key[MR];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int KT = K >> 5;
+  const int G = N / 16 / TG;                    // column groups
+  const int g = blockIdx.x % G, s = blockIdx.x / G;
+  const int nt0 = g * TG + w * TNW;             // this wave's first tile
+  const int nch_all = KT / KF;                  // KC-k chunks; split s owns [c_lo, c_hi)
+  const int c_lo = s * nch_all / SK, c_hi = (s + 1) * nch_all / SK;
+  const int kt0 = c_lo * KF, nchunk = c_hi - c_lo;
+
+  // ---- A staging: thread -> (row + i*RSTEP, 16-B chunk) fixed for all chunks
+  constexpr int LPT = MR * C16 / NTHR;         // A loads per thread per chunk (exact: no
+  static_assert(LPT * NTHR == MR * C16, "A tile must split evenly");  // guarded loads/stores)
+  constexpr int RSTEP = NTHR / C16;
+  const int arow = tid / C16, ac16 = tid % C16;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, 0x7fffffff, 0x00020000);
+  int a_voff[LPT];
+  bool a_valid[LPT];
+#pragma unroll
+  for (int i = 0; i < LPT; ++i) {
+    const int r = arow + i * RSTEP;
+    a_valid[i] = r < M;
+    a_voff[i] = ((a_valid[i] ? (a_rows ? a_rows[r] : r) : 0) * ldx + ac16 * 8) * 2;
+  }
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)wp, (short)0, 0x7fffffff, 0x00020000);
+  const int lane16 = lane * 16;
+  const u32x4_t zero = {0u, 0u, 0u, 0u};
+  float ss[LPT];
+#pragma unroll
+  for (int i = 0; i < LPT; ++i) ss[i] = 0.f;
+
+  struct AV { u32x4_t v[LPT]; };
+  auto load_a = [&](int c) -> AV {
+    AV a;
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      a.v[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, a_voff[i], (kt0 * 32 + c * KC) * 2, 0);
+    }
+    return a;
+  };
+  auto store_a = [&](int buf, const AV& a_in, float count) {  // count: 0 for clamped duplicates
+    AV a;  // rows >= M were loaded from row 0 (valid memory): zero them here, after the MFMAs
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) a.v[i] = a_valid[i] ? a_in.v[i] : zero;
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      if (NORM) {
+        float f[8];
+        unpack8(a.v[i], f);
+        float t = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) t += f[j] * f[j];
+        ss[i] += count * t;
+      }
+      *reinterpret_cast<u32x4_t*>(smem + buf * ABUF + a_off<KC>(arow + i * RSTEP, ac16)) = a.v[i];
+    }
+  };
+  auto load_b = [&](int c, u32x4_t (&b)[KF][TNW]) {
+#pragma unroll
+    for (int kf = 0; kf < KF; ++kf)
+#pragma unroll
+      for (int t = 0; t < TNW; ++t)
+        b[kf][t] = __builtin_amdgcn_raw_buffer_load_b128(
+            wr, lane16, (((nt0 + t) * KT + kt0 + c * KF + kf) * 512) * 2, 2);
+  };
+
+  f32x4_t acc[MB][TNW];
+#pragma unroll
+  for (int rb = 0; rb < MB; ++rb)
+#pragma unroll
+    for (int t = 0; t < TNW; ++t) acc[rb][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int buf, u32x4_t (&b)[KF][TNW]) {
+    const unsigned char* base = smem + buf * ABUF;
+#pragma unroll
+    for (int kf = 0; kf < KF; ++kf)
+#pragma unroll
+      for (int rb = 0; rb < MB; ++rb) {
+        const int row = rb * 16 + (lane & 15);
+        const u32x4_t a = *reinterpret_cast<const u32x4_t*>(base + a_off<KC>(row, kf * 4 + (lane >> 4)));
+#pragma unroll
+        for (int t = 0; t < TNW; ++t) acc[rb][t] = mfma16(a, b[kf][t], acc[rb][t]);
+      }
+  };
+
+  {
+    // Prefetch distance 2 chunks for both operands through 3-deep register rings: B (HBM
+    // weights) is consumed straight from registers, A (L2-resident activations) is written
+    // to one of 2 LDS buffers one chunk before use. vmcnt is in-order, so A(c+1) must be
+    // issued before B(c+1) - otherwise waiting for A would drain the B prefetch too. Loads
+    // are unconditional (tail chunk indices clamped, duplicates hit L2) so every s_waitcnt
+    // is a static count, never vmcnt(0).
+    u32x4_t bX[KF][TNW], bY[KF][TNW], bZ[KF][TNW];
+    AV aX, aY, aZ;
+    const int last = nchunk - 1;
+    auto clampc = [&](int c) { return c < last ? c : last; };
+    aX = load_a(0);
+    load_b(0, bX);
+    aY = load_a(clampc(1));
+    load_b(clampc(1), bY);
+    store_a(0, aX, 1.f);
+    __syncthreads();
+    // step c: prefetch chunk c+2 into (a2, b2), compute chunk c from (LDS c&1, bc), then
+    // publish A(c+1) from a1 into LDS.
+    auto step = [&](int c, u32x4_t (&bc)[KF][TNW], u32x4_t (&b2)[KF][TNW], AV& a1, AV& a2) {
+      a2 = load_a(clampc(c + 2));
+      load_b(clampc(c + 2), b2);
+      __builtin_amdgcn_sched_barrier(0);  // keep the prefetches ahead of this chunk's MFMAs
+      compute(c & 1, bc);
+      __builtin_amdgcn_sched_barrier(0);
+      store_a((c + 1) & 1, a1, c < last ? 1.f : 0.f);
+      __syncthreads();
+    };
+    for (int c = 0;;) {
+      step(c, bX, bZ, aY, aZ);
+      if (++c > last) break;
+      step(c, bY, bX, aZ, aX);
+      if (++c > last) break;
+      step(c, bZ, bY, aX, aY);
+      if (++c > last) break;
+    }
+  }
+
+  // row sum(x^2) of this split: the C16 threads of a row are consecutive lanes
+  if (NORM) {
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+#pragma unroll
+      for (int o = 1; o < C16; o <<= 1) ss[i] += __shfl_xor(ss[i], o, 64);
+    }
+  }
+  __syncthreads();  // all waves done with the A buffers: smem becomes the reduction tile
+  float* red = reinterpret_cast<float*>(smem);  // [TG][MR][16]
+  if (SK == 1) {
+#pragma unroll
+    for (int rb = 0; rb < MB; ++rb)
+#pragma unroll
+      for (int t = 0; t < TNW; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          red[((w * TNW + t) * MR + rb * 16 + (lane >> 4) * 4 + r) * 16 + (lane & 15)] = acc[rb][t][r];
+    if (NORM && ac16 == 0) {
+#pragma unroll
+      for (int i = 0; i < LPT; ++i) s_ss[arow + i * RSTEP] = ss[i];
+    }
+  } else {
+    // Split-K hand-off (cdna_hip_programming.md §5 'In-launch split-K reduction', sc1 form):
+    // every partial is stored write-through (sc1, 16-B stores), every storing wave drains its
+    // stores, the workgroup barriers, one lane takes a relaxed agent-scope ticket; the
+    // workgroup that draws SK-1 reads all slabs with sc1 loads. No L2 writeback (release) or
+    // invalidate (acquire) is needed in this form.
+    // Slab layout, fragment-native so each lane stores its 4 accumulators as one 16-B word:
+    //   [SK][N/16 tiles][MB][64 lanes][4]  fp32, then [SK][G][MR] partial sum(x^2).
+    const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc((void*)slab, (short)0, 0x7fffffff, 0x00020000);
+    const int split_stride = (N / 16) * MR * 16;  // floats
+#pragma unroll
+    for (int rb = 0; rb < MB; ++rb)
+#pragma unroll
+      for (int t = 0; t < TNW; ++t)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, acc[rb][t]), sr,
+                                               ((((nt0 + t) * MB + rb) * 64 + lane) * 4) * 4, s * split_stride * 4,
+                                               16 /* sc1 */);
+    const int ss_base = SK * split_stride;  // floats
+    if (NORM && ac16 == 0) {
+#pragma unroll
+      for (int i = 0; i < LPT; ++i)
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ss[i]), sr, ((s * G + g) * MR + arow + i * RSTEP) * 4,
+                                              ss_base * 4, 16);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      const unsigned old = __hip_atomic_fetch_add(&counters[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = old == (unsigned)(SK - 1);
+    }
+    __syncthreads();
+    if (!s_last) return;
+    // Last arriver: sum the SK slabs in fixed split order (deterministic). The group's region
+    // is one contiguous run of TG*MB*256 floats per split; every thread keeps E4 16-B loads x
+    // 4 splits in flight per round trip (cross-XCD reads: batching them keeps this short).
+    constexpr int E4 = TG * MB * 64 / NTHR;
+    static_assert(E4 * NTHR == TG * MB * 64, "combine tiling");
+    const int gbase = g * TG * MB * 256;  // floats
+    f32x4_t sum[E4];
+#pragma unroll
+    for (int j = 0; j < E4; ++j) sum[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int q0 = 0; q0 < SK; q0 += 4) {
+      f32x4_t v[4][E4];
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const int q = q0 + qq < SK ? q0 + qq : 0;
+#pragma unroll
+        for (int j = 0; j < E4; ++j)
+          v[qq][j] = __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(
+                                                     sr, (gbase + (j * NTHR + tid) * 4) * 4, q * split_stride * 4, 16));
+      }
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq)
+        if (q0 + qq < SK)
+#pragma unroll
+          for (int j = 0; j < E4; ++j) sum[j] += v[qq][j];
+    }
+#pragma unroll
+    for (int j = 0; j < E4; ++j) {
+      const int u = j * NTHR + tid;
+      const int tl = u / (MB * 64), rb = (u >> 6) % MB, ln = u & 63;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[(tl * MR + rb * 16 + (ln >> 4) * 4 + r) * 16 + (ln & 15)] = sum[j][r];
+    }
+    if (NORM && tid < MR) {
+      float t2 = 0.f;
+      for (int q = 0; q < SK; ++q)
+        t2 += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(sr, ((q * G + g) * MR + tid) * 4, ss_base * 4, 16));
+      s_ss[tid] = t2;
+    }
+    if (tid == 0) __hip_atomic_store(&counters[g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (EPI == EPI_ARGMAX && tid < MR) s_key[tid] = 0ull;
+  __syncthreads();
+
+  auto rstd = [&](int mm) -> float { return NORM ? rsqrtf(s_ss[mm] / (float)K + eps) : 1.f; };
+  const int ntg0 = g * TG;
+  if (EPI == EPI_SWIGLU) {
+    for (int e = tid; e < (TG / 2) * MR * 16; e += NTHR) {
+      const int tp = e / (MR * 16), mm = (e >> 4) % MR, n = e & 15;
+      if (mm >= M) continue;
+      const float r = rstd(mm);
+      const float gg = red[((2 * tp) * MR + mm) * 16 + n] * r, uu = red[((2 * tp + 1) * MR + mm) * 16 + n] * r;
+      ep.out[(size_t)mm * ep.ldo + (ntg0 / 2 + tp) * 16 + n] = f2bf(silu(gg) * uu);
+    }
+  } else {
+    for (int e = tid; e < TG * MR * 16; e += NTHR) {
+      const int t = e / (MR * 16), mm = (e >> 4) % MR, n = e & 15;
+      if (mm >= M) continue;
+      const float r = rstd(mm);
+      const float v = red[(t * MR + mm) * 16 + n] * r;
+      const int col = (ntg0 + t) * 16 + n;
+      if (EPI == EPI_STORE) {
+        ep.out[(size_t)mm * ep.ldo + col] = f2bf(v);
+      } else if (EPI == EPI_RESID) {
+        ep.out[(size_t)mm * ep.ldo + col] = f2bf(bf2f(ep.resid[(size_t)mm * ep.ldr + col]) + v);
+      } else if (EPI == EPI_QKV) {
+        epi_qkv_store(ep, mm, col, v, red[(t * MR + mm) * 16 + (n ^ 8)] * r);
+      } else if (EPI == EPI_ARGMAX) {
+        atomicMax(&s_key[mm], argmax_key(v, (unsigned)(col + ep.col_offset)));
+      }
+    }
+    if (EPI == EPI_ARGMAX) {
+      __syncthreads();
+      if (tid < M) atomicMax(&ep.keys[tid], s_key[tid]);
+    }
+  }
+}
+
+template <int MB, int TNW, int NW, int KF, int EPI>
+int launch(bool norm, const bf16_raw* x, int ldx, const int* a_rows, const bf16_raw* wp, int M, int N, int K, int SK, float eps,
+           const EpiArgs& ep, float* slab, unsigned* cnt, hipStream_t s) {
+  const int G = N / 16 / (NW * TNW);
+  dim3 grid(G * SK), block(NW * 64);
+  if (norm)
+    gemv_coop_kernel<MB, TNW, NW, KF, EPI, true><<<grid, block, 0, s>>>(x, ldx, a_rows, wp, M, N, K, SK, eps, ep, slab, cnt);
+  else
+    gemv_coop_kernel<MB, TNW, NW, KF, EPI, false><<<grid, block, 0, s>>>(x, ldx, a_rows, wp, M, N, K, SK, eps, ep, slab, cnt);
+  LSA_CHECK_LAUNCH();
+  return LSA_OK;
+}
+
+#define LSA_COOP_CONFIGS(X) \
+  X(2, 1, 8, 8) X(4, 1, 8, 8) X(2, 1, 8, 4) X(4, 1, 8, 4) X(2, 2, 8, 4) X(4, 2, 8, 4) X(2, 2, 4, 4) X(4, 2, 4, 4)
+
+template <int EPI>
+int dispatch(int mb, int tnw, int nw, int kf, bool norm, const bf16_raw* x, int ldx, const int* a_rows, const bf16_raw* wp, int M, int N,
+             int K, int SK, float eps, const EpiArgs& ep, float* slab, unsigned* cnt, hipStream_t s) {
+#define LSA_C(B, T, W, F) \
+  if (mb == B && tnw == T && nw == W && kf == F) return launch<B, T, W, F, EPI>(norm, x, ldx, a_rows, wp, M, N, K, SK, eps, ep, slab, cnt, s);
+  LSA_COOP_CONFIGS(LSA_C)
+#undef LSA_C
+  return LSA_UNSUPPORTED;
+}
+
+}  // namespace
+
+// K is split into 32*kf-k chunks, spread over the SK splits as evenly as possible.
+// Workspace: slab >= SK*N*16*MB*4 + SK*(N/16/(nw*tnw))*16*MB*4 bytes (only when SK > 1);
+// counters: N/16/(nw*tnw) zero-initialised uint32 (reset by the kernel itself).
+extern "C" int lsa_gemv_coop(const void* x, int ldx, const int* a_rows, const void* wp, int M, int N, int K, int norm, float eps,
+                             int epi, const EpiArgs* ep, int tnw, int nw, int kf, int sk, float* slab, unsigned* counters,
+                             hipStream_t stream) {
+  if (M < 1 || M > 64 || kf < 1 || K % (32 * kf) || ldx < K || sk < 1) return LSA_BAD_SHAPE;
+  const int mb = M <= 32 ? 2 : 4;
+  const int tg = nw * tnw;
+  if (N % (16 * tg) || sk > K / (32 * kf)) return LSA_BAD_SHAPE;
+  if (sk > 1 && (!slab || !counters)) return LSA_BAD_SHAPE;
+  const bf16_raw* xx = static_cast<const bf16_raw*>(x);
+  const bf16_raw* w = static_cast<const bf16_raw*>(wp);
+  const bool n = norm != 0;
+  switch (epi) {
+    case EPI_STORE: return dispatch<EPI_STORE>(mb, tnw, nw, kf, n, xx, ldx, a_rows, w, M, N, K, sk, eps, *ep, slab, counters, stream);
+    case EPI_RESID: return dispatch<EPI_RESID>(mb, tnw, nw, kf, n, xx, ldx, a_rows, w, M, N, K, sk, eps, *ep, slab, counters, stream);
+    case EPI_SWIGLU: return dispatch<EPI_SWIGLU>(mb, tnw, nw, kf, n, xx, ldx, a_rows, w, M, N, K, sk, eps, *ep, slab, counters, stream);
+    case EPI_QKV: return dispatch<EPI_QKV>(mb, tnw, nw, kf, n, xx, ldx, a_rows, w, M, N, K, sk, eps, *ep, slab, counters, stream);
+    case EPI_ARGMAX: return dispatch<EPI_ARGMAX>(mb, tnw, nw, kf, n, xx, ldx, a_rows, w, M, N, K, sk, eps, *ep, slab, counters, stream);
+    default: return LSA_UNSUPPORTED;
+  }
+}

@@ -53,13 +53,14 @@ def lib() -> ctypes.CDLL:
     L = ctypes.CDLL(KERNELS_SO, mode=ctypes.RTLD_GLOBAL)
     vp, i, f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
     L.lsa_gemv.argtypes = [vp, i, vp, vp, i, i, i, i, f, i, ctypes.POINTER(EpiArgs), i, i, i, vp]
+    L.lsa_gemv_coop.argtypes = [vp, i, vp, vp, i, i, i, i, f, i, ctypes.POINTER(EpiArgs), i, i, i, i, vp, vp, vp]
     L.lsa_gemm.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(EpiArgs), i, vp]
     L.lsa_attn_decode.argtypes = [vp, i, vp, vp, vp, vp, vp, i, i, i, i, i, f, i, i, vp, vp, vp, i, vp]
     L.lsa_embed.argtypes = [vp, i, vp, i, vp, i, vp]
     L.lsa_rmsnorm.argtypes = [vp, i, vp, i, i, f, vp, i, vp]
     L.lsa_argmax_finalize.argtypes = [vp, i, vp, vp, i, vp, i, i, vp, vp]
     L.lsa_pos_advance.argtypes = [vp, i, i, vp]
-    for name in ("lsa_gemv", "lsa_gemm", "lsa_attn_decode", "lsa_embed", "lsa_rmsnorm",
+    for name in ("lsa_gemv", "lsa_gemv_coop", "lsa_gemm", "lsa_attn_decode", "lsa_embed", "lsa_rmsnorm",
                  "lsa_argmax_finalize", "lsa_pos_advance", "lsa_version"):
         getattr(L, name).restype = ctypes.c_int
     _lib = L
@@ -96,12 +97,41 @@ def make_epi(out=None, resid=None, k_cache=None, v_cache=None, slot=None, pos=No
 
 
 # ------------------------------------------------------------------------------ projections
+class CoopWorkspace:
+    """Split-K partial slabs + per-column-group arrival counters for ``lsa_gemv_coop``.
+
+    Launches on one stream may share a workspace (they are stream-ordered and the last
+    arriving workgroup resets its counter before the kernel ends). The counters are zeroed
+    once here; the slab needs no initialisation."""
+
+    def __init__(self, device, slab_floats: int = 1 << 22, groups: int = 1 << 14):
+        self.slab = torch.empty(max(slab_floats, 1), dtype=torch.float32, device=device)
+        self.counters = torch.zeros(groups, dtype=torch.int32, device=device)
+
+
+_WS = {}
+
+
+def default_workspace(device=None) -> CoopWorkspace:
+    """Process-wide workspace per (device, stream), grown on demand (outside graph capture)."""
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    key = (dev.index, torch.cuda.current_stream(dev).cuda_stream)
+    if key not in _WS:
+        _WS[key] = CoopWorkspace(dev, slab_floats=1 << 24)
+    return _WS[key]
+
+
 def gemv(x: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep: EpiArgs,
          norm: bool = False, eps: float = 1e-5, a_rows: Optional[torch.Tensor] = None,
-         tn: int = 0, nw: int = 0, u: int = 0) -> None:
+         tn: int = 0, nw: int = 0, u: int = 0, coop: Optional[tuple] = None,
+         ws: Optional[CoopWorkspace] = None) -> None:
     """Decode projection, M <= 64 rows. ``wp`` is ``pack_b(W)`` (``pack_b(fold_norm(W, g))``
-    when ``norm``: RMSNorm of the A rows is then applied in-kernel), W: [N, K]."""
-    from .packing import GEMV_CONFIGS, gemv_config, row_blocks
+    when ``norm``: RMSNorm of the A rows is then applied in-kernel), W: [N, K].
+
+    Kernel choice: explicit ``tn/nw/u`` -> streaming GEMV (gemv.hip); explicit
+    ``coop=(tnw, nw, kf, sk)`` -> cooperative split-K (gemv_coop.hip); neither -> the tuned
+    choice of :func:`packing.proj_config`."""
+    from .packing import GEMV_CONFIGS, coop_candidates, coop_slab_floats, proj_config, row_blocks
     _req(1 <= M <= 64, f"gemv supports 1..64 rows, got {M}")
     _req(_is_bf16_cuda(x, wp), "gemv: bf16 cuda tensors required")
     _req(wp.numel() == N * K and N % 16 == 0 and K % 32 == 0, "gemv: packed weight shape")
@@ -110,8 +140,25 @@ def gemv(x: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep
         _req(x.shape[0] >= M, "gemv: x has fewer rows than M")
     else:
         _req(a_rows.dtype == torch.int32 and a_rows.is_cuda and a_rows.numel() >= M, "gemv: a_rows")
-    if tn == 0:
-        tn, nw, u = gemv_config(N // 16, M, need_even=(epi == EPI_SWIGLU), k=K)
+    if tn == 0 and coop is None:
+        algo, cfg = proj_config(N // 16, M, need_even=(epi == EPI_SWIGLU), k=K)
+        if algo == "coop":
+            coop = cfg
+        else:
+            tn, nw, u = cfg
+    if coop is not None:
+        coop = tuple(coop)
+        tnw, cnw, kf, sk = coop
+        _req(coop in coop_candidates(N // 16, K, M), f"gemv: coop config {coop} invalid for N={N} K={K} M={M}")
+        if ws is None:
+            ws = default_workspace(x.device)
+        need = coop_slab_floats(N, M, tnw, cnw, kf, sk)
+        _req(ws.slab.numel() >= need, f"gemv: coop workspace too small ({ws.slab.numel()} < {need} floats)")
+        _req(ws.counters.numel() >= N // 16 // (tnw * cnw), "gemv: coop workspace counters too small")
+        rc = lib().lsa_gemv_coop(_p(x), x.stride(0), _p(a_rows), _p(wp), M, N, K, int(norm), float(eps), epi,
+                                 ctypes.byref(ep), tnw, cnw, kf, sk, _p(ws.slab), _p(ws.counters), _stream())
+        _check(rc, "lsa_gemv_coop")
+        return
     mb = row_blocks(M)
     _req((tn, mb, nw, u) in GEMV_CONFIGS, f"gemv: config tn={tn} nw={nw} u={u} not built for {M} rows")
     _req((K // 32) % u == 0, f"gemv: K={K} must be a multiple of {32 * u}")

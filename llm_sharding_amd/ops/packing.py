@@ -94,6 +94,36 @@ def gemv_candidates(n_tiles: int, k: int, rows: int, need_even: bool = False) ->
             if b == mb and n_tiles % tn == 0 and (not need_even or tn % 2 == 0) and (k // 32) % u == 0]
 
 
+# (mb, tnw, nw, kf) instantiated in csrc/kernels/gemv_coop.hip (LSA_COOP_CONFIGS) - keep in sync.
+COOP_CONFIGS = [(2, 1, 8, 8), (4, 1, 8, 8), (2, 1, 8, 4), (4, 1, 8, 4), (2, 2, 8, 4), (4, 2, 8, 4),
+                (2, 2, 4, 4), (4, 2, 4, 4)]
+COOP_SPLITS = (1, 2, 4, 8, 16)
+
+
+def coop_candidates(n_tiles: int, k: int, rows: int) -> list:
+    """(tnw, nw, kf, sk) for the cooperative split-K GEMV (rows 17..64): every split keeps at
+    least two K chunks of 32*kf so the register prefetch overlaps."""
+    if rows <= 16:
+        return []
+    mb = row_blocks(rows)
+    out = []
+    for (b, tnw, nw, kf) in COOP_CONFIGS:
+        if b != mb or n_tiles % (tnw * nw) or k % (32 * kf):
+            continue
+        for sk in COOP_SPLITS:
+            if k // (32 * kf) >= 2 * sk and (n_tiles // (tnw * nw)) * sk <= 4 * N_CU:
+                out.append((tnw, nw, kf, sk))
+    return out
+
+
+def coop_slab_floats(n: int, rows: int, tnw: int, nw: int, kf: int, sk: int) -> int:
+    """fp32 workspace a coop launch needs (0 when sk == 1)."""
+    if sk == 1:
+        return 0
+    mr = 16 * row_blocks(rows)
+    return sk * n * mr + sk * (n // 16 // (tnw * nw)) * mr
+
+
 def _tuned() -> dict:
     global _TUNED
     if _TUNED is None:
@@ -101,8 +131,29 @@ def _tuned() -> dict:
         if os.path.exists(TUNING_FILE):
             with open(TUNING_FILE) as f:
                 for e in json.load(f).get("entries", []):
-                    _TUNED[(e["N"], e["K"], e["mb"], bool(e["even"]))] = tuple(e["cfg"])
+                    _TUNED[(e["N"], e["K"], e["mb"], bool(e["even"]))] = (e.get("algo", "gemv"), tuple(e["cfg"]))
     return _TUNED
+
+
+def proj_config(n_tiles: int, rows: int, need_even: bool = False, k: int = 4096) -> tuple:
+    """("gemv", (tn, nw, u)) or ("coop", (tnw, nw, kf, sk)) for a decode projection of ``rows``
+    rows. The tuning table (measured on MI355X) wins; otherwise rows <= 16 use the
+    weight-streaming GEMV and larger row counts the cooperative split-K kernel with the
+    smallest split that fills the 256 CUs."""
+    t = _tuned().get((n_tiles * 16, k, row_blocks(rows), bool(need_even)))
+    if t is not None:
+        algo, cfg = t
+        if (algo == "coop" and cfg in coop_candidates(n_tiles, k, rows)) or \
+           (algo == "gemv" and cfg in gemv_candidates(n_tiles, k, rows, need_even)):
+            return t
+    if rows > 16:
+        cands = [c for c in coop_candidates(n_tiles, k, rows) if c[:3] == (1, 8, 8)]
+        for c in cands:
+            if (n_tiles // 8) * c[3] >= N_CU:
+                return ("coop", c)
+        if cands:
+            return ("coop", cands[-1])
+    return ("gemv", gemv_config(n_tiles, rows, need_even, k))
 
 
 def gemv_config(n_tiles: int, rows: int, need_even: bool = False, k: int = 4096) -> tuple:
@@ -111,11 +162,10 @@ def gemv_config(n_tiles: int, rows: int, need_even: bool = False, k: int = 4096)
     time ~ (weight bytes + A re-reads / 5) / grid efficiency, where each workgroup re-reads
     the whole A (rows x K) from L2 (~5x the HBM rate) and grid efficiency =
     workgroups / (256 CUs x rounds)."""
-    mb = row_blocks(rows)
-    t = _tuned().get((n_tiles * 16, k, mb, bool(need_even)))
+    t = _tuned().get((n_tiles * 16, k, row_blocks(rows), bool(need_even)))
     cands = gemv_candidates(n_tiles, k, rows, need_even)
-    if t is not None and t in cands:
-        return t
+    if t is not None and t[0] == "gemv" and t[1] in cands:
+        return t[1]
     best, best_cost = None, float("inf")
     for tn, nw, u in cands:
         g = n_tiles // tn

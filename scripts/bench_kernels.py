@@ -58,6 +58,7 @@ def gemv_sweep(out_rows, models, rows_list, tune_entries):
     from llm_sharding_amd.models.rope import rope_table
     from llm_sharding_amd.config import llama2_7b
     cos, sin = rope_table(llama2_7b(), 1024, DEV)
+    cws = hip.CoopWorkspace(DEV, slab_floats=1 << 25)
     for model in models:
         for name, (N, K) in MODEL_SHAPES[model].items():
             epi = EPIS[name]
@@ -84,15 +85,19 @@ def gemv_sweep(out_rows, models, rows_list, tune_entries):
                 res = []
                 for tn, nw, u in packing.gemv_candidates(N // 16, K, M, even):
                     us = timeit(lambda i: hip.gemv(x, ws[i % nbuf], M, N, K, epi, ep, norm=norm, tn=tn, nw=nw, u=u))
-                    res.append((us, tn, nw, u, N * K * 2 / us / 1e6))
-                res.sort()
+                    res.append((us, "gemv", (tn, nw, u), N * K * 2 / us / 1e6))
+                for cfg in packing.coop_candidates(N // 16, K, M):
+                    us = timeit(lambda i: hip.gemv(x, ws[i % nbuf], M, N, K, epi, ep, norm=norm, coop=cfg, ws=cws))
+                    res.append((us, "coop", cfg, N * K * 2 / us / 1e6))
+                res.sort(key=lambda r: r[0])
                 best = res[0]
                 line = {"kernel": "gemv", "model": model, "shape": name, "N": N, "K": K, "M": M,
-                        "best_us": round(best[0], 2), "best_cfg": list(best[1:4]), "best_TBps": round(best[4], 2),
-                        "all": [(round(r[0], 2),) + tuple(r[1:4]) for r in res]}
+                        "best_us": round(best[0], 2), "best_algo": best[1], "best_cfg": list(best[2]),
+                        "best_TBps": round(best[3], 2),
+                        "all": [(round(r[0], 2), r[1]) + tuple(r[2]) for r in res]}
                 print(json.dumps(line), flush=True)
                 out_rows.append(line)
-                tune_entries[(N, K, packing.row_blocks(M), even)] = list(best[1:4])
+                tune_entries[(N, K, packing.row_blocks(M), even)] = (best[1], list(best[2]))
             del ws
             torch.cuda.empty_cache()
 
@@ -127,7 +132,7 @@ def gemm_sweep(out_rows):
             a = torch.randn(M, K, device=DEV).to(torch.bfloat16)
             out = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
             ep = hip.make_epi(out=out, ldo=N)
-            us = timeit(lambda i: hip.gemm(a, w, M, N, K, hip.EPI_STORE, ep), reps=10, warm=2)
+            us = timeit(lambda i: hip.gemm(a, w, M, N, K, hip.EPI_STORE, ep), reps=10)
             line = {"kernel": "gemm", "N": N, "K": K, "M": M, "us": round(us, 1),
                     "TFLOPs": round(2 * M * N * K / us / 1e6, 1)}
             print(json.dumps(line), flush=True)
@@ -151,9 +156,10 @@ def main():
             old = {}
             if os.path.exists(packing.TUNING_FILE):
                 for e in json.load(open(packing.TUNING_FILE)).get("entries", []):
-                    old[(e["N"], e["K"], e["mb"], bool(e["even"]))] = e["cfg"]
+                    old[(e["N"], e["K"], e["mb"], bool(e["even"]))] = (e.get("algo", "gemv"), e["cfg"])
             old.update(tune)
-            ents = [{"N": k[0], "K": k[1], "mb": k[2], "even": k[3], "cfg": v} for k, v in sorted(old.items())]
+            ents = [{"N": k[0], "K": k[1], "mb": k[2], "even": k[3], "algo": v[0], "cfg": v[1]}
+                    for k, v in sorted(old.items())]
             with open(packing.TUNING_FILE, "w") as f:
                 json.dump({"device": torch.cuda.get_device_name(), "entries": ents}, f, indent=1)
             print(f"wrote {len(ents)} tuning entries to {packing.TUNING_FILE}")

@@ -91,6 +91,69 @@ def test_gemv_every_config(cfg):
         assert rel_err(out, x.float() @ w.float().T) < 8e-3, (cfg, K)
 
 
+@pytest.mark.parametrize("cfg", packing.COOP_CONFIGS)
+def test_gemv_coop_every_config(cfg):
+    """Cooperative split-K GEMV: every instantiated (mb, tnw, nw) x every legal split, with
+    the fused RMSNorm + residual epilogue (partial sum(x^2) combined across splits) and
+    uneven chunk splits (K = 11008 -> 43 or 86 chunks)."""
+    h = hip()
+    mb, tnw, nw, kf = cfg
+    M = {2: 29, 4: 50}[mb]
+    N = 16 * tnw * nw * 3
+    for K in (11008, 512):
+        x = _rnd(M, K)
+        g = (1 + 0.1 * torch.randn(K, device=DEV)).to(torch.bfloat16)
+        w = _rnd(N, K, scale=0.02)
+        wp = packing.pack_b(packing.fold_norm(w, g))
+        resid = _rnd(M, N)
+        ref = resid.float() + _rmsnorm(x, g, 1e-5) @ w.float().T
+        for c in packing.coop_candidates(N // 16, K, M):
+            if c[:3] != (tnw, nw, kf):
+                continue
+            out = resid.clone()
+            h.gemv(x, wp, M, N, K, h.EPI_RESID, h.make_epi(out=out, resid=out, ldo=N, ldr=N), norm=True,
+                   coop=c)
+            assert rel_err(out, ref) < 8e-3, (cfg, K, c)
+
+
+@pytest.mark.parametrize("M", [20, 64])
+def test_gemv_coop_swiglu_argmax_graph(M):
+    """SwiGLU and argmax epilogues through the coop kernel, replayed in a hipGraph (the
+    arrival counters must reset themselves between replays)."""
+    h = hip()
+    I, H, V = 1024, 4096, 4096
+    x = _rnd(M, H)
+    wg, wu = _rnd(I, H, scale=0.05), _rnd(I, H, scale=0.05)
+    lm = _rnd(V, H, scale=0.02)
+    out = torch.zeros(M, I, dtype=torch.bfloat16, device=DEV)
+    keys = torch.zeros(M, dtype=torch.int64, device=DEV)
+    tok = torch.zeros(M, dtype=torch.int32, device=DEV)
+    wgu, wlm = packing.pack_b(packing.fuse_gate_up(wg, wu)), packing.pack_b(lm)
+    ws = h.CoopWorkspace(DEV, slab_floats=1 << 22)
+
+    def step():
+        h.gemv(x, wgu, M, 2 * I, H, h.EPI_SWIGLU, h.make_epi(out=out, ldo=I), coop=(1, 8, 8, 4), ws=ws)
+        h.gemv(x, wlm, M, V, H, h.EPI_ARGMAX, h.make_epi(keys=keys), coop=(1, 8, 4, 4), ws=ws)
+        h.argmax_finalize(keys, M, tok)
+
+    step()
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        step()
+    ref = F.silu(x.float() @ wg.float().T) * (x.float() @ wu.float().T)
+    logits = x.float() @ lm.float().T
+    for _ in range(3):
+        out.zero_()
+        tok.fill_(-1)
+        graph.replay()
+        torch.cuda.synchronize()
+        assert rel_err(out, ref) < 1e-2
+        chosen = logits.gather(1, tok.long()[:, None])[:, 0]
+        assert torch.all(logits.max(-1).values - chosen < 2e-2 * logits.abs().max())
+    assert int(ws.counters.abs().sum()) == 0
+
+
 @pytest.mark.parametrize("M", [1, 12, 64])
 def test_gemv_swiglu(M):
     h = hip()
@@ -111,14 +174,14 @@ def _rope_ref(t, pos, cos, sin):
     return torch.cat([t1 * c - t2 * s, t2 * c + t1 * s], dim=-1)
 
 
-@pytest.mark.parametrize("path", ["gemv", "gemm"])
+@pytest.mark.parametrize("path", ["gemv", "coop", "gemm"])
 @pytest.mark.parametrize("nh,nkv,hd", [(32, 32, 128), (8, 2, 64), (24, 8, 128)])
 def test_qkv_rope_kv_append(path, nh, nkv, hd):
     from llm_sharding_amd.config import tiny
     from llm_sharding_amd.models.rope import rope_table
     h = hip()
     H = 512
-    M = 5 if path == "gemv" else 150
+    M = {"gemv": 5, "coop": 40, "gemm": 150}[path]
     slots, T = 3, 256
     wq, wk, wv = _rnd(nh * hd, H, scale=0.05), _rnd(nkv * hd, H, scale=0.05), _rnd(nkv * hd, H, scale=0.05)
     x = _rnd(M, H)
@@ -135,6 +198,8 @@ def test_qkv_rope_kv_append(path, nh, nkv, hd):
                     n_heads=nh, n_kv=nkv, head_dim=hd, t_max=T)
     if path == "gemv":
         h.gemv(x, wp, M, N, H, h.EPI_QKV, ep)
+    elif path == "coop":
+        h.gemv(x, wp, M, N, H, h.EPI_QKV, ep, coop=(1, 8, 4, 2))
     else:
         h.gemm(x, wp, M, N, H, h.EPI_QKV, ep)
     xf = x.float()
