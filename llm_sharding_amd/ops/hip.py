@@ -56,11 +56,12 @@ def lib() -> ctypes.CDLL:
     L.lsa_gemv_coop.argtypes = [vp, i, vp, vp, i, i, i, i, f, i, ctypes.POINTER(EpiArgs), i, i, i, i, vp, vp, vp]
     L.lsa_gemm.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(EpiArgs), i, vp]
     L.lsa_attn_decode.argtypes = [vp, i, vp, vp, vp, vp, vp, i, i, i, i, i, f, i, i, vp, vp, vp, i, vp]
+    L.lsa_attn_prefill.argtypes = [vp, i, vp, vp, vp, i, i, i, i, i, f, i, vp, i, vp]
     L.lsa_embed.argtypes = [vp, i, vp, i, vp, i, vp]
     L.lsa_rmsnorm.argtypes = [vp, i, vp, i, i, f, vp, i, vp]
     L.lsa_argmax_finalize.argtypes = [vp, i, vp, vp, i, vp, i, i, vp, vp]
     L.lsa_pos_advance.argtypes = [vp, i, i, vp]
-    for name in ("lsa_gemv", "lsa_gemv_coop", "lsa_gemm", "lsa_attn_decode", "lsa_embed", "lsa_rmsnorm",
+    for name in ("lsa_gemv", "lsa_gemv_coop", "lsa_gemm", "lsa_attn_decode", "lsa_attn_prefill", "lsa_embed", "lsa_rmsnorm",
                  "lsa_argmax_finalize", "lsa_pos_advance", "lsa_version"):
         getattr(L, name).restype = ctypes.c_int
     _lib = L
@@ -202,6 +203,60 @@ def attn(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, slot: to
                                rows, n_heads, n_kv, head_dim, t_max, float(sc), nsplit, min_chunk,
                                _p(part_o), _p(part_lse), _p(out), out.stride(0), _stream())
     _check(rc, "lsa_attn_decode")
+
+
+PREFILL_TILE_ROWS = 64
+
+
+def build_prefill_tiles(slot, pos, kv_len=None, device=None):
+    """Host-side tile table for :func:`attn_prefill`: rows are grouped into runs of one
+    sequence (same slot, consecutive positions) and each run is cut into <= 64-row tiles
+    ``[row0, nrows, slot, pos0, kvlen, 0, 0, 0]`` (int32). Causal tiles get
+    ``kvlen = last position + 1``; with an explicit per-row ``kv_len`` (the reference's
+    unmasked prefill) every row of a run must share it. Heaviest tiles first (balance)."""
+    slot = [int(x) for x in (slot.tolist() if torch.is_tensor(slot) else slot)]
+    pos = [int(x) for x in (pos.tolist() if torch.is_tensor(pos) else pos)]
+    kvl = None if kv_len is None else [int(x) for x in (kv_len.tolist() if torch.is_tensor(kv_len) else kv_len)]
+    tiles = []
+    r, n = 0, len(slot)
+    while r < n:
+        e = r + 1
+        while (e < n and slot[e] == slot[r] and pos[e] == pos[e - 1] + 1 and e - r < PREFILL_TILE_ROWS
+               and (kvl is None or kvl[e] == kvl[r])):
+            e += 1
+        kv = pos[e - 1] + 1 if kvl is None else kvl[r]
+        tiles.append([r, e - r, slot[r], pos[r], kv, 0, 0, 0])
+        r = e
+    tiles.sort(key=lambda t: -t[4])
+    return torch.tensor(tiles, dtype=torch.int32, device=device)
+
+
+def attn_prefill(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, tiles: torch.Tensor,
+                 n_heads: int, n_kv: int, head_dim: int, out: torch.Tensor, causal: bool = True,
+                 scale: Optional[float] = None, tiles_host: Optional[torch.Tensor] = None) -> None:
+    """Flash prefill attention (attn_prefill.hip) for the rows described by ``tiles``
+    (:func:`build_prefill_tiles`), reading K/V already appended to the static cache."""
+    _req(_is_bf16_cuda(q, k_cache, v_cache, out), "attn_prefill: bf16 cuda tensors")
+    _req(k_cache.dim() == 4 and k_cache.shape == v_cache.shape, "attn_prefill: cache [slots, n_kv, T, hd]")
+    _req(k_cache.shape[1] == n_kv and k_cache.shape[3] == head_dim and head_dim in (64, 128), "attn_prefill: dims")
+    _req(n_heads % n_kv == 0 and q.shape[1] >= n_heads * head_dim and out.shape[1] >= n_heads * head_dim,
+         "attn_prefill: q/out width")
+    _req(tiles.dtype == torch.int32 and tiles.is_cuda and tiles.dim() == 2 and tiles.shape[1] == 8,
+         "attn_prefill: tiles int32 [n, 8]")
+    th = tiles.cpu() if tiles_host is None else tiles_host
+    slots, t_max = k_cache.shape[0], k_cache.shape[2]
+    if th.numel():
+        row0, nr, sl, p0, kv = (th[:, i] for i in range(5))
+        _req(bool((nr >= 1).all() and (nr <= PREFILL_TILE_ROWS).all()), "attn_prefill: tile rows")
+        _req(bool((row0 >= 0).all()) and int((row0 + nr).max()) <= min(q.shape[0], out.shape[0]),
+             "attn_prefill: tile rows out of range")
+        _req(bool((sl >= 0).all() and (sl < slots).all()), "attn_prefill: slot out of range")
+        _req(bool((p0 >= 0).all()) and int((p0 + nr).max()) <= t_max, "attn_prefill: positions beyond cache")
+        _req(bool((kv >= 1).all() and (kv <= t_max).all()), "attn_prefill: kvlen out of range")
+    sc = head_dim ** -0.5 if scale is None else scale
+    rc = lib().lsa_attn_prefill(_p(q), q.stride(0), _p(k_cache), _p(v_cache), _p(tiles), tiles.shape[0], n_heads,
+                                n_kv, head_dim, t_max, float(sc), int(causal), _p(out), out.stride(0), _stream())
+    _check(rc, "lsa_attn_prefill")
 
 
 # ------------------------------------------------------------------------------ elementwise

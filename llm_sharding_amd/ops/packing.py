@@ -124,6 +124,22 @@ def coop_slab_floats(n: int, rows: int, tnw: int, nw: int, kf: int, sk: int) -> 
     return sk * n * mr + sk * (n // 16 // (tnw * nw)) * mr
 
 
+def coop_workspace_need(shapes, max_rows: int = 64, even_n=()) -> tuple:
+    """(slab floats, counters) that the decode projections ``shapes`` = [(N, K), ...] need at
+    every row count up to ``max_rows`` under the configs :func:`proj_config` picks."""
+    floats, groups = 0, 0
+    for n, k in shapes:
+        for rows in (32, 64):
+            if rows - 16 > max_rows:
+                continue
+            algo, cfg = proj_config(n // 16, rows, need_even=(n, k) in even_n, k=k)
+            if algo == "coop":
+                tnw, nw, kf, sk = cfg
+                floats = max(floats, coop_slab_floats(n, rows, tnw, nw, kf, sk))
+                groups = max(groups, n // 16 // (tnw * nw))
+    return floats, groups
+
+
 def _tuned() -> dict:
     global _TUNED
     if _TUNED is None:

@@ -211,6 +211,14 @@ class StageEngine:
             self.ws_rows = ws_rows
             self.keys = torch.zeros(R, dtype=torch.int64, device=dev)
             self.tokens = torch.zeros(R, dtype=torch.int32, device=dev)
+            # split-K workspace of the cooperative decode GEMV (gemv_coop.hip), owned by the
+            # stage and allocated before any graph capture
+            from ..ops import hip
+            shapes = [(cfg.qkv_size, H), (H, cfg.q_size), (2 * I, H), (H, I)]
+            if self.has_head:
+                shapes.append((cfg.vocab_size, H))
+            floats, groups = packing.coop_workspace_need(shapes, self.DECODE_MAX_ROWS, even_n=((2 * I, H),))
+            self.coop_ws = hip.CoopWorkspace(dev, slab_floats=max(floats, 1 << 16), groups=max(groups, 4096))
 
     def memory_bytes(self) -> int:
         n = 0
@@ -260,7 +268,13 @@ class StageEngine:
         slot_t, pos_t = self._i32(slot), self._i32(pos)
         kvl_t = None if kv_len is None else self._i32(kv_len)
         if self.gpu:
-            return self._forward_hip(h, slot_t, pos_t, kvl_t, rows)
+            tiles = None
+            if rows > self.DECODE_MAX_ROWS:
+                # prefill: flash attention over per-sequence 64-row tiles (host-built table)
+                from ..ops import hip
+                th = hip.build_prefill_tiles(slot, pos, kv_len)
+                tiles = (th, th.to(self.device, non_blocking=True))
+            return self._forward_hip(h, slot_t, pos_t, kvl_t, rows, tiles=tiles)
         return self._forward_torch(h, slot_t.long(), pos_t.long(), None if kvl_t is None else kvl_t.long())
 
     def head(self, h: torch.Tensor, rows_idx=None) -> torch.Tensor:
@@ -279,7 +293,7 @@ class StageEngine:
                 keys = self.keys[:c]
                 keys.zero_()
                 ep = hip.make_epi(keys=keys)
-                hip.gemv(h, self.lm_head, c, self.cfg.vocab_size, self.cfg.hidden_size, hip.EPI_ARGMAX, ep,
+                hip.gemv(h, self.lm_head, c, self.cfg.vocab_size, self.cfg.hidden_size, hip.EPI_ARGMAX, ep, ws=self.coop_ws,
                          norm=True, eps=self.cfg.rms_norm_eps, a_rows=idx[c0:c0 + c])
                 hip.argmax_finalize(keys, c, self.tokens)
                 out[c0:c0 + c] = self.tokens[:c].long()
@@ -307,7 +321,7 @@ class StageEngine:
         want = max(1, min(8, ceil_div(kv_max, 512), ceil_div(1024, rows * self.cfg.num_key_value_heads)))
         return max(1, min(want, self.ws_rows // rows))
 
-    def _forward_hip(self, h, slot, pos, kv_len, rows, nsplit: Optional[int] = None) -> torch.Tensor:
+    def _forward_hip(self, h, slot, pos, kv_len, rows, nsplit: Optional[int] = None, tiles=None) -> torch.Tensor:
         from ..ops import hip
         cfg = self.cfg
         H, I, eps = cfg.hidden_size, cfg.intermediate_size, cfg.rms_norm_eps
@@ -320,27 +334,31 @@ class StageEngine:
         if h.data_ptr() != hbuf.data_ptr():
             hbuf.copy_(h)
         decode = rows <= self.DECODE_MAX_ROWS
-        if nsplit is None:
+        if nsplit is None and tiles is None:
             kv_max = self.max_seq if decode else (int(pos.max().item()) + 1 if kv_len is None else int(kv_len.max().item()))
             nsplit = self._attn_nsplit(rows, kv_max)
         q, attn_o, act, xn = self.buf_q[:rows], self.buf_attn[:rows], self.buf_act[:rows], self.buf_xn[:rows]
+        ws = self.coop_ws
         for li, lw in enumerate(self.layers):
             kc, vc = self.k_cache[li], self.v_cache[li]
             ep_qkv = hip.make_epi(out=q, k_cache=kc, v_cache=vc, slot=slot, pos=pos, cos=self.cos, sin=self.sin,
                                   ldo=q.stride(0), n_heads=nh, n_kv=nkv, head_dim=hd, t_max=self.max_seq)
             if decode:
-                hip.gemv(hbuf, lw.qkv, rows, cfg.qkv_size, H, hip.EPI_QKV, ep_qkv, norm=True, eps=eps)
+                hip.gemv(hbuf, lw.qkv, rows, cfg.qkv_size, H, hip.EPI_QKV, ep_qkv, norm=True, eps=eps, ws=ws)
             else:
                 hip.rmsnorm(hbuf, None, xn, rows, eps, H)
                 hip.gemm(xn, lw.qkv, rows, cfg.qkv_size, H, hip.EPI_QKV, ep_qkv)
-            hip.attn(q, kc, vc, slot, pos, rows, nh, nkv, hd, nsplit, self.part_o, self.part_lse, attn_o,
-                     kv_len=kv_len)
+            if tiles is not None:
+                hip.attn_prefill(q, kc, vc, tiles[1], nh, nkv, hd, attn_o, causal=kv_len is None, tiles_host=tiles[0])
+            else:
+                hip.attn(q, kc, vc, slot, pos, rows, nh, nkv, hd, nsplit, self.part_o, self.part_lse, attn_o,
+                         kv_len=kv_len)
             ep_o = hip.make_epi(out=hbuf, resid=hbuf, ldo=hbuf.stride(0), ldr=hbuf.stride(0))
             ep_gu = hip.make_epi(out=act, ldo=act.stride(0))
             if decode:
-                hip.gemv(attn_o, lw.o, rows, H, cfg.q_size, hip.EPI_RESID, ep_o)
-                hip.gemv(hbuf, lw.gate_up, rows, 2 * I, H, hip.EPI_SWIGLU, ep_gu, norm=True, eps=eps)
-                hip.gemv(act, lw.down, rows, H, I, hip.EPI_RESID, ep_o)
+                hip.gemv(attn_o, lw.o, rows, H, cfg.q_size, hip.EPI_RESID, ep_o, ws=ws)
+                hip.gemv(hbuf, lw.gate_up, rows, 2 * I, H, hip.EPI_SWIGLU, ep_gu, norm=True, eps=eps, ws=ws)
+                hip.gemv(act, lw.down, rows, H, I, hip.EPI_RESID, ep_o, ws=ws)
             else:
                 hip.gemm(attn_o, lw.o, rows, H, cfg.q_size, hip.EPI_RESID, ep_o)
                 hip.rmsnorm(hbuf, None, xn, rows, eps, H)
@@ -459,7 +477,7 @@ class DecodeGraph:
         eng._forward_hip(h, self.slot, self.pos, None, rows, nsplit=eng.decode_nsplit(rows))
         if self.mode in ("full", "last"):
             ep = hip.make_epi(keys=self.keys)
-            hip.gemv(h, eng.lm_head, rows, eng.cfg.vocab_size, eng.cfg.hidden_size, hip.EPI_ARGMAX, ep,
+            hip.gemv(h, eng.lm_head, rows, eng.cfg.vocab_size, eng.cfg.hidden_size, hip.EPI_ARGMAX, ep, ws=eng.coop_ws,
                      norm=True, eps=eng.cfg.rms_norm_eps)
             hip.argmax_finalize(self.keys, rows, self.tokens, self.pos, 1, self.history,
                                 self.step_ctr if self.history is not None else None)
