@@ -1,0 +1,167 @@
+#!/usr/bin/env python3
+"""Continuous-batching server over the layer-sharded pipeline, one process per GPU.
+
+    # 8 MI355X, Llama-2-7B shards (or --random for random-init weights of that architecture)
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29500 \\
+        serve.py --shards shards/Llama-2-7b-chat-hf_bfloat16 --port 40700
+    # client (any host): reference-style user_request message on the ingress port
+    python -c "from llm_sharding_amd.utils.node_worker import send_user_request; \\
+               send_user_request('127.0.0.1', 40700, text='Write a poem about the blue sky.')"
+
+    # self-contained load test: N synthetic requests, prints a JSON stats line and exits
+    python serve.py --random llama2-7b --requests 256 --prompt-len 128 --max-new-tokens 128
+
+Rank 0 (embedding stage) is the ingress: it accepts ``{"command": "user_request", "text" |
+"input_ids", "max_new_tokens", "reply_to"}`` messages (the reference's control-port JSON /
+our LSAM framing, see ``utils/node_worker.send_user_request``) on ``--port``, streams every
+finished request to stdout and, if ``reply_to`` is given, pushes ``{"request_id",
+"output_ids", "text", "ttft_ms", "tpot_ms"}`` back to that address. ``{"command":
+"shutdown"}`` drains the queue and stops every rank.
+"""
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from llm_sharding_amd.config import LlamaConfig, get_preset  # noqa: E402
+from llm_sharding_amd.parallel.scheduler import plan_stages  # noqa: E402
+from llm_sharding_amd.parallel.server import PipelineServer  # noqa: E402
+from llm_sharding_amd.runtime.engine import RandomSource, ShardFolderSource  # noqa: E402
+
+
+def _ingress(srv, port, tok, stop_evt, default_new):
+    from llm_sharding_amd.parallel import protocol
+    from llm_sharding_amd.parallel.transport import Again, PullSocket, PushSocket
+    sock = PullSocket(f"tcp://*:{port}")
+    print(f"[INFO] ingress listening on tcp://*:{sock.port}", flush=True)
+    replies = {}
+
+    def done(r, t):
+        if t in r.eos_ids or len(r.output_ids) >= r.max_new_tokens:
+            text = tok.decode(r.output_ids) if tok is not None else ""
+            print(f"[INFO] request {r.rid} done: {len(r.output_ids)} tokens  ttft {r.ttft_ms:.1f} ms  "
+                  f"output: {text!r}", flush=True)
+            if r.reply_to:
+                if r.reply_to not in replies:
+                    replies[r.reply_to] = PushSocket(r.reply_to)
+                replies[r.reply_to].send_bytes(protocol.encode({
+                    "request_id": r.rid, "output_ids": list(r.output_ids), "text": text,
+                    "ttft_ms": r.ttft_ms, "tpot_ms": r.tpot_ms}))
+
+    while not stop_evt.is_set():
+        try:
+            raw = sock.recv_bytes(timeout_ms=200)
+        except Again:
+            continue
+        msg = json.loads(raw) if protocol.is_json_message(raw) else protocol.decode(raw)
+        cmd = msg.get("command")
+        if cmd == "shutdown":
+            stop_evt.set()
+            break
+        if cmd != "user_request":
+            print(f"[WARNING] ingress: unknown message {cmd!r}", flush=True)
+            continue
+        n_new = int(msg.get("max_new_tokens") or default_new)
+        rows = msg.get("input_ids")
+        if rows is None:
+            if tok is None:
+                print("[ERROR] text request but no tokenizer", flush=True)
+                continue
+            rows = [tok.encode(msg.get("text", ""))]
+        elif rows and not isinstance(rows[0], (list, tuple)):
+            rows = [rows]
+        for ids in rows:
+            try:
+                srv.submit(ids, n_new, on_token=done, reply_to=msg.get("reply_to"))
+            except ValueError as e:
+                print(f"[ERROR] request rejected: {e}", flush=True)
+    sock.close()
+    for s in replies.values():
+        s.close()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shards", default="", help="shard folder (reference .pth / safetensors format)")
+    ap.add_argument("--random", default="", help="random-init weights of a preset (llama2-7b, llama2-70b, ...)")
+    ap.add_argument("--port", type=int, default=40700)
+    ap.add_argument("--batch", type=int, default=32, help="KV slots per micro-batch")
+    ap.add_argument("--microbatches", type=int, default=0, help="0 = max(2, stages)")
+    ap.add_argument("--max-seq", type=int, default=2048)
+    ap.add_argument("--prefill-budget", type=int, default=2048)
+    ap.add_argument("--max-new-tokens", type=int, default=128)
+    ap.add_argument("--requests", type=int, default=0, help="synthetic load test: N requests, then exit")
+    ap.add_argument("--prompt-len", type=int, default=128)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--seed", type=int, default=0)
+    a = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    gpu = torch.cuda.is_available()
+    dev = torch.device("cuda", local) if gpu else torch.device("cpu")
+    if gpu:
+        torch.cuda.set_device(local)
+    ctrl = None
+    if world > 1:
+        import torch.distributed as dist
+        if gpu:
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+        ctrl = dist.new_group(backend="gloo")
+    if a.shards:
+        cfg = LlamaConfig.from_pretrained(a.shards)
+        source = ShardFolderSource(a.shards, cfg)
+    else:
+        cfg = get_preset(a.random or "llama2-7b")
+        source = RandomSource(cfg, a.seed)
+    M = a.microbatches or max(2, world)
+    plan = plan_stages(cfg, world, kv_tokens=a.max_seq * a.batch * M)
+    st = plan.stages[rank]
+    if rank == 0:
+        print(f"[INFO] {cfg.name}: {world} stage(s) {plan.ranges()}, {M} x {a.batch} slots", flush=True)
+    srv = PipelineServer(cfg, source, rank, world, st.start, st.end, dev, batch=a.batch, microbatches=M,
+                         max_seq=a.max_seq, prefill_budget=a.prefill_budget, use_graph=not a.no_graph,
+                         dtype=torch.bfloat16 if gpu else torch.float32, ctrl_group=ctrl)
+    if rank != 0:
+        srv.serve()
+    elif a.requests:
+        g = torch.Generator().manual_seed(a.seed + 1)
+        for _ in range(a.requests):
+            ids = torch.randint(3, cfg.vocab_size, (a.prompt_len,), generator=g).tolist()
+            srv.submit(ids, a.max_new_tokens, eos_ids=())
+        t0 = time.perf_counter()
+        srv.t_start = t0
+        srv.serve(stop_when_idle=True)
+        s = srv.stats()
+        s.update({"metric": "serving_output_tokens_per_sec", "n_gpus": world, "model": cfg.name,
+                  "requests": a.requests, "prompt_len": a.prompt_len, "max_new_tokens": a.max_new_tokens,
+                  "slots": a.batch * M, "microbatches": M})
+        print(json.dumps(s), flush=True)
+    else:
+        tok = None
+        try:
+            from llm_sharding_amd.models.tokenizer import load_tokenizer
+            tok = load_tokenizer(a.shards) if a.shards else None
+        except Exception as e:  # noqa: BLE001
+            print(f"[WARNING] no tokenizer: {e}", flush=True)
+        stop_evt = threading.Event()
+        th = threading.Thread(target=_ingress, args=(srv, a.port, tok, stop_evt, a.max_new_tokens), daemon=True)
+        th.start()
+        srv.serve(stop_when_idle=False, should_stop=stop_evt.is_set)
+        th.join(timeout=5)
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
