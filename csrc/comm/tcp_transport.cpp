@@ -182,7 +182,7 @@ struct Pull {
 struct Push {
   std::string host;
   int port = 0;
-  int fd = -1;
+  std::atomic<int> fd{-1};  // written by the writer thread, read by lsa_push_connected (TSan)
   std::thread th;
   std::atomic<bool> stop{false};
   std::mutex mu;
@@ -190,10 +190,10 @@ struct Push {
   std::condition_variable drained;  // queue empty
   std::deque<std::string> q;        // framed messages
   uint64_t sent = 0, enqueued = 0;
-  // fault injection
-  int drop_every = 0;
-  int delay_ms = 0;
-  uint64_t attempt = 0;
+  // fault injection (set from the caller's thread while the writer runs)
+  std::atomic<int> drop_every{0};
+  std::atomic<int> delay_ms{0};
+  uint64_t attempt = 0;  // writer thread only
 
   ~Push() { shutdown(); }
 
@@ -265,8 +265,9 @@ struct Push {
       }
       backoff_ms = 5;
       ++attempt;
-      if (delay_ms > 0) std::this_thread::sleep_for(std::chrono::milliseconds(delay_ms));
-      const bool dropped = drop_every > 0 && (attempt % (uint64_t)drop_every) == 0;
+      const int dly = delay_ms.load(), every = drop_every.load();
+      if (dly > 0) std::this_thread::sleep_for(std::chrono::milliseconds(dly));
+      const bool dropped = every > 0 && (attempt % (uint64_t)every) == 0;
       if (!dropped && !write_all(msg)) {  // peer went away: reconnect and resend
         ::close(fd);
         fd = -1;

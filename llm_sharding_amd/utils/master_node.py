@@ -10,7 +10,11 @@ the master that calls ``ConfigSender``; the repository only ships a hand-written
 2. :func:`plan_stages` picks contiguous layer ranges minimising the bottleneck stage under
    the memory caps (exact DP);
 3. :meth:`deploy` sends the reference 6-key configs (ring chain, ingress = stage 0) through
-   ``ConfigSender``; :meth:`submit` / :meth:`shutdown` drive the deployed chain.
+   ``ConfigSender``; :meth:`submit` / :meth:`shutdown` drive the deployed chain;
+4. failure detection / elastic recovery: :meth:`health` pings every
+   controller's config port (``ping`` -> ``pong`` with its status); :meth:`failover` drops
+   the devices that stopped answering, re-plans the layers over the survivors and hot
+   re-configures them (the reference's live re-shard path, ``node_worker.py:445-474``).
 """
 from __future__ import annotations
 
@@ -19,7 +23,7 @@ from typing import List, Optional, Sequence
 from ..config import LlamaConfig
 from ..parallel.scheduler import DeviceSpec, Plan, build_chain_configs, plan_stages
 from .config_sender import ConfigSender
-from .node_worker import send_shutdown, send_user_request
+from .node_worker import ping_node, send_shutdown, send_user_request
 
 
 class MasterNode:
@@ -62,6 +66,29 @@ class MasterNode:
                 raise TimeoutError(f"config not delivered to {st.device.host}:{st.device.config_port}")
             self.senders.append(s)
         return cfgs
+
+    def health(self, timeout_ms: int = 2000) -> list:
+        """[(DeviceSpec, status dict | None)] for every device of the current plan."""
+        devs = [st.device for st in self.plan.stages] if self.plan is not None else self.devices
+        return [(d, ping_node(d.host, d.config_port, timeout_ms)) for d in devs]
+
+    def failover(self, timeout_ms: int = 2000) -> list:
+        """Ping the deployed chain; if any controller is dead, re-plan over the devices that
+        answered and redeploy. Returns the list of dropped devices (empty if all alive)."""
+        status = self.health(timeout_ms)
+        dead = [d for d, st in status if st is None]
+        if not dead:
+            return []
+        alive = [d for d, st in status if st is not None]
+        if not alive:
+            raise RuntimeError("[ERROR] every controller is unreachable")
+        self.devices = [d for d in self.devices if d not in dead]
+        self.plan = None
+        for s in self.senders:
+            s.close()
+        self.senders = []
+        self.deploy(timeout_ms=max(timeout_ms, 10000))
+        return dead
 
     def submit(self, text: str = "", input_ids=None) -> None:
         ing = self.plan.stages[0].device

@@ -39,7 +39,7 @@ from ..models.rope import full_cos_sin
 from ..models.tokenizer import load_tokenizer
 from ..parallel import protocol
 from ..parallel.communicator import Again, Communicator
-from ..parallel.transport import PullSocket, PushSocket, parse_addr
+from ..parallel.transport import PullSocket, PushSocket, local_ip, parse_addr
 from ..runtime.engine import ShardFolderSource, StageEngine, WeightSource
 from .forwarding_utils import build_position_ids
 
@@ -291,6 +291,8 @@ class NodeController:
         self.running = False
         self.finished_outputs: list = []
         self.node_worker: Optional[NodeWorker] = None
+        self.forwarded = 0
+        self.t_boot = time.monotonic()
         self.received_config = config if config is not None else (self._receive_config() if wait_config else None)
         if self.received_config is not None:
             self._apply_new_role(self.received_config)
@@ -310,7 +312,7 @@ class NodeController:
                     _log("[CONFIG] Waiting for configuration file from master node...")
                 raw = self.recv_config_socket.recv_bytes(-1)
             msg = json.loads(raw.decode())
-            if isinstance(msg, dict) and msg.get("command") in ("user_request", "shutdown"):
+            if isinstance(msg, dict) and msg.get("command") in ("user_request", "shutdown", "ping"):
                 self._handle_command(msg)
                 if no_block:
                     continue
@@ -326,6 +328,28 @@ class NodeController:
             self.running = False
         elif msg["command"] == "user_request":
             self.pending_requests.append(msg)
+        elif msg["command"] == "ping":
+            self._pong(msg)
+
+    def status(self) -> dict:
+        """Liveness / role snapshot (answered to ``ping``; SURVEY.md §5.3 stage-liveness)."""
+        w = self.node_worker
+        return {"listen_port": self.listen_port, "configured": w is not None,
+                "shards": [w.start, w.end] if w is not None else None,
+                "ingress": bool(w.can_receive_user_request) if w is not None else False,
+                "forwarded": self.forwarded, "finished_requests": len(self.finished_outputs),
+                "uptime_s": time.monotonic() - self.t_boot}
+
+    def _pong(self, msg: dict) -> None:
+        reply_to = msg.get("reply_to")
+        if not reply_to:
+            return
+        try:
+            s = PushSocket(reply_to)
+            s.send_bytes(json.dumps({"command": "pong", "nonce": msg.get("nonce"), **self.status()}).encode())
+            s.close(linger_ms=2000)
+        except OSError as e:
+            _log(f"[WARNING] pong to {reply_to} failed: {e}")
 
     def _apply_new_role(self, cfg: dict) -> None:
         for k in CONFIG_KEYS:
@@ -425,6 +449,7 @@ class NodeController:
                                f"Attributes: {attrs if attrs else 'No attributes found'}")
         processed = w.pass_through_shard(received_data)
         w.communicator.transfer_data(processed)
+        self.forwarded += 1
         if w.start != 0 and self.verbose:
             print("*", end=" ", flush=True)
         return True
@@ -468,13 +493,39 @@ def send_user_request(node_ip: str, port: int, text: str = "", input_ids=None, m
     s.close(linger_ms=5000)
 
 
+def ping_node(node_ip: str, port: int, timeout_ms: int = 2000) -> Optional[dict]:
+    """Liveness probe: send ``ping`` to a controller's config port and wait for its ``pong``
+    (its :meth:`NodeController.status`). Returns None if no answer within ``timeout_ms``."""
+    import secrets
+    reply = PullSocket("tcp://127.0.0.1:0" if node_ip in ("127.0.0.1", "localhost") else "tcp://*:0")
+    host = "127.0.0.1" if node_ip in ("127.0.0.1", "localhost") else local_ip()
+    nonce = secrets.randbits(31)
+    s = PushSocket(f"tcp://{node_ip}:{port}")
+    try:
+        s.send_bytes(json.dumps({"command": "ping", "nonce": nonce, "reply_to": f"tcp://{host}:{reply.port}"}).encode())
+        deadline = time.monotonic() + timeout_ms / 1e3
+        while True:
+            left = int((deadline - time.monotonic()) * 1e3)
+            if left <= 0:
+                return None
+            try:
+                msg = json.loads(reply.recv_bytes(timeout_ms=left).decode())
+            except Again:
+                return None
+            if msg.get("command") == "pong" and msg.get("nonce") == nonce:
+                return msg
+    finally:
+        s.close(linger_ms=0)
+        reply.close()
+
+
 def send_shutdown(node_ip: str, port: int) -> None:
     s = PushSocket(f"tcp://{node_ip}:{port}")
     s.send_bytes(json.dumps({"command": "shutdown"}).encode())
     s.close(linger_ms=5000)
 
 
-__all__ = ["Communicator", "NodeWorker", "NodeController", "send_user_request", "send_shutdown", "Again"]
+__all__ = ["Communicator", "NodeWorker", "NodeController", "send_user_request", "send_shutdown", "ping_node", "Again"]
 
 
 if __name__ == "__main__":

@@ -86,3 +86,66 @@ def test_two_node_processes_end_to_end(tiny_shards, tmp_path):
     want = ReferenceLlama(cfg, emb, layers, fn, lm).generate(ids, 6)[0].tolist()
     m = re.search(r"output:  ?(.*)", text)
     assert m and tok.decode(ids[0].tolist() + want) == m.group(1).rstrip("\n")
+
+
+@pytest.mark.slow
+def test_failure_detection_and_elastic_failover(tiny_shards, tmp_path):
+    """3 controllers deployed by the master; one process dies; health() notices (no pong),
+    failover() re-plans over the 2 survivors and hot re-configures them; a request then
+    produces the golden tokens."""
+    from llm_sharding_amd.utils.node_worker import ping_node
+    cports, dports = free_ports(3), free_ports(3)
+    env = dict(os.environ, PYTHONUNBUFFERED="1", PYTHONPATH=ROOT)
+    logs = [open(tmp_path / f"node{i}.log", "w") for i in range(3)]
+    procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "start_node.py"), "--port", str(cports[i]),
+                               "--shards", tiny_shards, "--device", "cpu", "--dtype", "float32",
+                               "--max-new-tokens", "5"], stdout=logs[i], stderr=subprocess.STDOUT, env=env)
+             for i in range(3)]
+    try:
+        # liveness before configuration
+        t0 = time.time()
+        while any(ping_node("127.0.0.1", p, 500) is None for p in cports):
+            assert time.time() - t0 < 120
+        devs = [DeviceSpec(host="127.0.0.1", config_port=cports[i], data_port=dports[i]) for i in range(3)]
+        m = MasterNode.from_shards(tiny_shards, devs)
+        m.deploy()
+        t0 = time.time()
+        while not all((st or {}).get("configured") for _, st in m.health(1000)):
+            assert time.time() - t0 < 120
+        assert m.failover(1000) == []
+        procs[1].kill()
+        procs[1].wait(timeout=30)
+        dropped = m.failover(1000)
+        assert [d.config_port for d in dropped] == [cports[1]]
+        assert len(m.plan.stages) == 2
+        t0 = time.time()
+        while True:
+            st = dict((d.config_port, s) for d, s in m.health(1000))
+            if all(s and s["configured"] and s["shards"] == [p.start, p.end]
+                   for p, s in ((p, st[p.device.config_port]) for p in m.plan.stages)):
+                break
+            assert time.time() - t0 < 120
+        m.submit(input_ids=[[1, 40, 41, 42]])
+        log0 = tmp_path / "node0.log"
+        t0 = time.time()
+        while time.time() - t0 < 120 and "output token number" not in log0.read_text():
+            time.sleep(0.2)
+        text = log0.read_text()
+        assert "output token number: 5" in text, text[-2000:]
+    finally:
+        for i, p in enumerate(cports):
+            if procs[i].poll() is None:
+                send_shutdown("127.0.0.1", p)
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+        for f in logs:
+            f.close()
+    cfg, emb, layers, fn, lm = W.load_full_model(tiny_shards)
+    want = ReferenceLlama(cfg, emb, layers, fn, lm).generate(torch.tensor([[1, 40, 41, 42]]), 5)[0].tolist()
+    from llm_sharding_amd.models.tokenizer import load_tokenizer
+    tok = load_tokenizer(tiny_shards)
+    m2 = re.search(r"output:  ?(.*)", text)
+    assert m2 and tok.decode([1, 40, 41, 42] + want) == m2.group(1).rstrip("\n")
