@@ -45,6 +45,7 @@ def parse():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--json-out", default="")
+    ap.add_argument("--trace", default="", help="write per-rank Chrome-trace timelines of the timed steps here")
     return ap.parse_args()
 
 
@@ -55,6 +56,8 @@ def main():
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
     if a.gpus > 1 and world == 1:
         raise SystemExit("multi-GPU runs must be launched with torch.distributed.run (one rank per GPU)")
+    if a.trace:
+        os.environ["LSA_TRACE"] = a.trace
     from llm_sharding_amd.parallel.pipeline import run_decode_benchmark
     res = run_decode_benchmark(model=a.model, n_gpus=a.gpus, steps=a.steps, warmup=a.warmup,
                                batch=a.batch, prompt_len=a.prompt_len, max_seq=a.max_seq,

@@ -26,6 +26,7 @@ import torch
 
 from ..config import get_preset
 from ..runtime.engine import DecodeGraph, EagerDecode, RandomSource, StageEngine
+from ..utils import tracing
 from .scheduler import plan_stages
 
 
@@ -103,6 +104,7 @@ class PipelineStage:
         self.graphs: list = []
         self.send_works: dict = {}
         self.tokens_ready = [True] * microbatches  # stage 0: next-step token ids are in place
+        self.tl = tracing.from_env(rank, self.device if self.gpu else "cpu")  # LSA_TRACE=dir
 
     # ---------------------------------------------------------------- p2p helpers
     def _send(self, t: torch.Tensor, dst: int, key):
@@ -141,7 +143,8 @@ class PipelineStage:
         else:
             h = torch.empty((B * P, H), dtype=self.dtype, device=self.device)
             self._recv(h, self.rank - 1)
-        h = eng.forward(h, slot, pos)
+        with self.tl.span("prefill", mb=mb, rows=B * P):
+            h = eng.forward(h, slot, pos)
         eng.advance(sl, [P] * B)
         if self.last:
             tok = eng.head(h, [i * P + P - 1 for i in range(B)]).to(torch.int32)
@@ -188,14 +191,17 @@ class PipelineStage:
 
     def step_mb(self, s: int, mb: int, events: Optional[list] = None) -> None:
         g = self.graphs[mb]
+        tl = self.tl
         if self.world > 1:
-            if self.first:
-                if not self.tokens_ready[mb]:
-                    self._recv(g.tokens, self.world - 1)
-                self.tokens_ready[mb] = False
-            else:
-                self._recv(g.h_in, self.rank - 1)
-        self._run_mb(g)
+            with tl.span("recv", mb=mb, step=s):
+                if self.first:
+                    if not self.tokens_ready[mb]:
+                        self._recv(g.tokens, self.world - 1)
+                    self.tokens_ready[mb] = False
+                else:
+                    self._recv(g.h_in, self.rank - 1)
+        with tl.span("decode", mb=mb, step=s):
+            self._run_mb(g)
         if events is not None and self.gpu:
             ev = torch.cuda.Event(enable_timing=True)
             ev.record()
@@ -350,6 +356,8 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
+    stage.tl.spans.clear()
+    stage.tl.start()  # ranks aligned on the barrier above
     events: list = []
     t_start = time.perf_counter()
     for s in range(steps):
@@ -395,6 +403,9 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
         "load_s": load_s,
         "plan": plan.ranges(),
     }
+    trace = tracing.export_env(stage.tl)
+    if trace and verbose:
+        print(f"[bench] rank {rank} timeline -> {trace}  {stage.tl.summary()}", flush=True)
     if stage.last and verbose:
         hist = stage.graphs[0].history[:8, :4].cpu().tolist() if stage.graphs[0].history is not None else []
         print(f"[bench] rank {rank} sample tokens (step x seq): {hist}", flush=True)

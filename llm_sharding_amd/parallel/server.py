@@ -34,6 +34,7 @@ from typing import Callable, Dict, List, Optional
 import torch
 
 from ..runtime.engine import DecodeGraph, StageEngine
+from ..utils import tracing
 from .pipeline import DistP2P, _percentile
 
 CMD_DECODE, CMD_PREFILL, CMD_STOP = 1, 2, 3
@@ -138,6 +139,7 @@ class PipelineServer:
         self._lock = threading.Lock()
         self.tokens_generated = 0
         self.t_start = None
+        self.tl = tracing.from_env(rank, self.device)  # LSA_TRACE=dir -> per-rank Chrome trace
 
     # ------------------------------------------------------------------ helpers
     def _slots(self, mb: int) -> list:
@@ -192,6 +194,11 @@ class PipelineServer:
     # ------------------------------------------------------------------ command execution (every rank)
     def _exec(self, cmd, mb, items, resets, ids=None):
         """Run one command on this stage. Returns the last stage's token ids (world == 1)."""
+        name = {CMD_PREFILL: "prefill", CMD_DECODE: "decode"}.get(cmd, "cmd")
+        with self.tl.span(name, mb=mb, items=len(items)):
+            return self._exec_body(cmd, mb, items, resets, ids)
+
+    def _exec_body(self, cmd, mb, items, resets, ids=None):
         eng, H = self.eng, self.cfg.hidden_size
         for s in resets:
             self._set_pos(s, 0)
@@ -438,6 +445,7 @@ class PipelineServer:
         self.stop()
 
     def stop(self) -> None:
+        tracing.export_env(self.tl)
         if self.first:
             self._bcast_header(self.hdr.pack(CMD_STOP, 0))
             for w, _ in self._ctrl_works:
@@ -463,6 +471,7 @@ class PipelineServer:
         self._flush_sends()
         if self.gpu:
             torch.cuda.synchronize(self.device)
+        tracing.export_env(self.tl)
 
     # ------------------------------------------------------------------ convenience
     def generate(self, prompts: List[List[int]], max_new_tokens: int = 32, eos_ids=()) -> List[List[int]]:

@@ -9,7 +9,10 @@
                send_user_request('127.0.0.1', 40700, text='Write a poem about the blue sky.')"
 
     # self-contained load test: N synthetic requests, prints a JSON stats line and exits
-    python serve.py --random llama2-7b --requests 256 --prompt-len 128 --max-new-tokens 128
+    python serve.py --model llama2-7b --requests 256 --prompt-len 128 --max-new-tokens 128
+
+All runtime knobs are RuntimeConfig fields (``--batch --microbatches --max-seq --prefill-budget
+--no-use-graph --no-causal --trace-dir --log-level ...``).
 
 Rank 0 (embedding stage) is the ingress: it accepts ``{"command": "user_request", "text" |
 "input_ids", "max_new_tokens", "reply_to"}`` messages (the reference's control-port JSON /
@@ -28,10 +31,10 @@ import time
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from llm_sharding_amd.config import LlamaConfig, get_preset  # noqa: E402
 from llm_sharding_amd.parallel.scheduler import plan_stages  # noqa: E402
 from llm_sharding_amd.parallel.server import PipelineServer  # noqa: E402
-from llm_sharding_amd.runtime.engine import RandomSource, ShardFolderSource  # noqa: E402
+from llm_sharding_amd.utils.log import get_logger  # noqa: E402
+from llm_sharding_amd.utils.runtime_config import RuntimeConfig  # noqa: E402
 
 
 def _ingress(srv, port, tok, stop_evt, default_new):
@@ -86,28 +89,27 @@ def _ingress(srv, port, tok, stop_evt, default_new):
 
 
 def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--shards", default="", help="shard folder (reference .pth / safetensors format)")
-    ap.add_argument("--random", default="", help="random-init weights of a preset (llama2-7b, llama2-70b, ...)")
-    ap.add_argument("--port", type=int, default=40700)
-    ap.add_argument("--batch", type=int, default=32, help="KV slots per micro-batch")
-    ap.add_argument("--microbatches", type=int, default=0, help="0 = max(2, stages)")
-    ap.add_argument("--max-seq", type=int, default=2048)
-    ap.add_argument("--prefill-budget", type=int, default=2048)
-    ap.add_argument("--max-new-tokens", type=int, default=128)
+    ap = argparse.ArgumentParser(description="continuous-batching pipeline server (one process per GPU)")
+    RuntimeConfig.add_arguments(ap)
+    ap.add_argument("--random", default="", help="alias of --model: random-init weights of a preset")
     ap.add_argument("--requests", type=int, default=0, help="synthetic load test: N requests, then exit")
     ap.add_argument("--prompt-len", type=int, default=128)
-    ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--seed", type=int, default=0)
     a = ap.parse_args()
+    if a.random:
+        a.model = a.random
+    rc = RuntimeConfig.from_args(a)
+    if rc.trace_dir:
+        os.environ["LSA_TRACE"] = rc.trace_dir
+    os.environ.setdefault("LSA_LOG_LEVEL", rc.log_level)
+    log = get_logger("serve")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    gpu = torch.cuda.is_available()
-    dev = torch.device("cuda", local) if gpu else torch.device("cpu")
+    dev = rc.torch_device(local)
+    gpu = dev.type == "cuda"
     if gpu:
-        torch.cuda.set_device(local)
+        torch.cuda.set_device(dev)
     ctrl = None
     if world > 1:
         import torch.distributed as dist
@@ -116,44 +118,39 @@ def main():
         else:
             dist.init_process_group("gloo")
         ctrl = dist.new_group(backend="gloo")
-    if a.shards:
-        cfg = LlamaConfig.from_pretrained(a.shards)
-        source = ShardFolderSource(a.shards, cfg)
-    else:
-        cfg = get_preset(a.random or "llama2-7b")
-        source = RandomSource(cfg, a.seed)
-    M = a.microbatches or max(2, world)
-    plan = plan_stages(cfg, world, kv_tokens=a.max_seq * a.batch * M)
+    cfg, source = rc.model_and_source()
+    M = rc.microbatches or max(2, world)
+    plan = plan_stages(cfg, world, kv_tokens=rc.max_seq * rc.batch * M)
     st = plan.stages[rank]
     if rank == 0:
-        print(f"[INFO] {cfg.name}: {world} stage(s) {plan.ranges()}, {M} x {a.batch} slots", flush=True)
-    srv = PipelineServer(cfg, source, rank, world, st.start, st.end, dev, batch=a.batch, microbatches=M,
-                         max_seq=a.max_seq, prefill_budget=a.prefill_budget, use_graph=not a.no_graph,
-                         dtype=torch.bfloat16 if gpu else torch.float32, ctrl_group=ctrl)
+        log.info(f"{cfg.name}: {world} stage(s) {plan.ranges()}, {M} x {rc.batch} slots")
+    srv = PipelineServer(cfg, source, rank, world, st.start, st.end, dev, batch=rc.batch, microbatches=M,
+                         max_seq=rc.max_seq, prefill_budget=rc.prefill_budget, use_graph=rc.use_graph,
+                         dtype=rc.torch_dtype(dev) if gpu else torch.float32, ctrl_group=ctrl, causal=rc.causal)
     if rank != 0:
         srv.serve()
     elif a.requests:
-        g = torch.Generator().manual_seed(a.seed + 1)
+        g = torch.Generator().manual_seed(rc.seed + 1)
         for _ in range(a.requests):
             ids = torch.randint(3, cfg.vocab_size, (a.prompt_len,), generator=g).tolist()
-            srv.submit(ids, a.max_new_tokens, eos_ids=())
+            srv.submit(ids, rc.max_new_tokens, eos_ids=())
         t0 = time.perf_counter()
         srv.t_start = t0
         srv.serve(stop_when_idle=True)
         s = srv.stats()
         s.update({"metric": "serving_output_tokens_per_sec", "n_gpus": world, "model": cfg.name,
-                  "requests": a.requests, "prompt_len": a.prompt_len, "max_new_tokens": a.max_new_tokens,
-                  "slots": a.batch * M, "microbatches": M})
+                  "requests": a.requests, "prompt_len": a.prompt_len, "max_new_tokens": rc.max_new_tokens,
+                  "slots": rc.batch * M, "microbatches": M})
         print(json.dumps(s), flush=True)
     else:
         tok = None
         try:
             from llm_sharding_amd.models.tokenizer import load_tokenizer
-            tok = load_tokenizer(a.shards) if a.shards else None
+            tok = load_tokenizer(rc.shards) if rc.shards else None
         except Exception as e:  # noqa: BLE001
-            print(f"[WARNING] no tokenizer: {e}", flush=True)
+            log.warning(f"no tokenizer: {e}")
         stop_evt = threading.Event()
-        th = threading.Thread(target=_ingress, args=(srv, a.port, tok, stop_evt, a.max_new_tokens), daemon=True)
+        th = threading.Thread(target=_ingress, args=(srv, rc.port, tok, stop_evt, rc.max_new_tokens), daemon=True)
         th.start()
         srv.serve(stop_when_idle=False, should_stop=stop_evt.is_set)
         th.join(timeout=5)
