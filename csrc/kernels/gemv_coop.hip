@@ -1,4 +1,4 @@
-// Cooperative split-K decode projection for 17..64 rows: y[M, N] = A[M, K] @ W^T.
+// Cooperative split-K projection for 17..128 rows (decode batches, short prefills): y[M, N] = A[M, K] @ W^T.
 //
 // Why (profiles/r1_gemv_o_proj_pmc.txt): in gemv.hip every workgroup re-reads all of A from
 // L2 (waves split K inside the workgroup, so A is never shared); at M >= 32 the L1->L2 request
@@ -306,7 +306,8 @@ int launch(bool norm, const bf16_raw* x, int ldx, const int* a_rows, const bf16_
 }
 
 #define LSA_COOP_CONFIGS(X) \
-  X(2, 1, 8, 8) X(4, 1, 8, 8) X(2, 1, 8, 4) X(4, 1, 8, 4) X(2, 2, 8, 4) X(4, 2, 8, 4) X(2, 2, 4, 4) X(4, 2, 4, 4)
+  X(2, 1, 8, 8) X(4, 1, 8, 8) X(2, 1, 8, 4) X(4, 1, 8, 4) X(2, 2, 8, 4) X(4, 2, 8, 4) X(2, 2, 4, 4) X(4, 2, 4, 4) \
+  X(8, 1, 8, 4) X(8, 1, 8, 2) X(8, 2, 4, 2)
 
 template <int EPI>
 int dispatch(int mb, int tnw, int nw, int kf, bool norm, const bf16_raw* x, int ldx, const int* a_rows, const bf16_raw* wp, int M, int N,
@@ -326,8 +327,8 @@ int dispatch(int mb, int tnw, int nw, int kf, bool norm, const bf16_raw* x, int 
 extern "C" int lsa_gemv_coop(const void* x, int ldx, const int* a_rows, const void* wp, int M, int N, int K, int norm, float eps,
                              int epi, const EpiArgs* ep, int tnw, int nw, int kf, int sk, float* slab, unsigned* counters,
                              hipStream_t stream) {
-  if (M < 1 || M > 64 || kf < 1 || K % (32 * kf) || ldx < K || sk < 1) return LSA_BAD_SHAPE;
-  const int mb = M <= 32 ? 2 : 4;
+  if (M < 1 || M > 128 || kf < 1 || K % (32 * kf) || ldx < K || sk < 1) return LSA_BAD_SHAPE;
+  const int mb = M <= 32 ? 2 : (M <= 64 ? 4 : 8);
   const int tg = nw * tnw;
   if (N % (16 * tg) || sk > K / (32 * kf)) return LSA_BAD_SHAPE;
   if (sk > 1 && (!slab || !counters)) return LSA_BAD_SHAPE;

@@ -126,14 +126,14 @@ def gemv(x: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep
          norm: bool = False, eps: float = 1e-5, a_rows: Optional[torch.Tensor] = None,
          tn: int = 0, nw: int = 0, u: int = 0, coop: Optional[tuple] = None,
          ws: Optional[CoopWorkspace] = None) -> None:
-    """Decode projection, M <= 64 rows. ``wp`` is ``pack_b(W)`` (``pack_b(fold_norm(W, g))``
+    """Decode / short-prefill projection, M <= 128 rows (> 64: coop kernel only). ``wp`` is ``pack_b(W)`` (``pack_b(fold_norm(W, g))``
     when ``norm``: RMSNorm of the A rows is then applied in-kernel), W: [N, K].
 
     Kernel choice: explicit ``tn/nw/u`` -> streaming GEMV (gemv.hip); explicit
     ``coop=(tnw, nw, kf, sk)`` -> cooperative split-K (gemv_coop.hip); neither -> the tuned
     choice of :func:`packing.proj_config`."""
     from .packing import GEMV_CONFIGS, coop_candidates, coop_slab_floats, proj_config, row_blocks
-    _req(1 <= M <= 64, f"gemv supports 1..64 rows, got {M}")
+    _req(1 <= M <= 128, f"gemv supports 1..128 rows, got {M}")
     _req(_is_bf16_cuda(x, wp), "gemv: bf16 cuda tensors required")
     _req(wp.numel() == N * K and N % 16 == 0 and K % 32 == 0, "gemv: packed weight shape")
     _req(x.dim() == 2 and x.shape[1] >= K and x.stride(1) == 1, "gemv: x must be [rows, >=K] row-major")

@@ -85,7 +85,7 @@ TUNING_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemv_tun
 
 
 def row_blocks(rows: int) -> int:
-    return 1 if rows <= 16 else (2 if rows <= 32 else 4)
+    return 1 if rows <= 16 else (2 if rows <= 32 else (4 if rows <= 64 else 8))
 
 
 def gemv_candidates(n_tiles: int, k: int, rows: int, need_even: bool = False) -> list:
@@ -96,12 +96,13 @@ def gemv_candidates(n_tiles: int, k: int, rows: int, need_even: bool = False) ->
 
 # (mb, tnw, nw, kf) instantiated in csrc/kernels/gemv_coop.hip (LSA_COOP_CONFIGS) - keep in sync.
 COOP_CONFIGS = [(2, 1, 8, 8), (4, 1, 8, 8), (2, 1, 8, 4), (4, 1, 8, 4), (2, 2, 8, 4), (4, 2, 8, 4),
-                (2, 2, 4, 4), (4, 2, 4, 4)]
+                (2, 2, 4, 4), (4, 2, 4, 4), (8, 1, 8, 4), (8, 1, 8, 2), (8, 2, 4, 2)]
+GEMV_MAX_ROWS = 128  # rows 65..128 are served by the coop kernel only
 COOP_SPLITS = (1, 2, 4, 8, 16)
 
 
 def coop_candidates(n_tiles: int, k: int, rows: int) -> list:
-    """(tnw, nw, kf, sk) for the cooperative split-K GEMV (rows 17..64): every split keeps at
+    """(tnw, nw, kf, sk) for the cooperative split-K GEMV (rows 17..128): every split keeps at
     least two K chunks of 32*kf so the register prefetch overlaps."""
     if rows <= 16:
         return []
@@ -129,8 +130,8 @@ def coop_workspace_need(shapes, max_rows: int = 64, even_n=()) -> tuple:
     every row count up to ``max_rows`` under the configs :func:`proj_config` picks."""
     floats, groups = 0, 0
     for n, k in shapes:
-        for rows in (32, 64):
-            if rows - 16 > max_rows:
+        for rows in (32, 64, 128):
+            if rows // 2 >= max_rows:
                 continue
             algo, cfg = proj_config(n // 16, rows, need_even=(n, k) in even_n, k=k)
             if algo == "coop":
@@ -163,12 +164,20 @@ def proj_config(n_tiles: int, rows: int, need_even: bool = False, k: int = 4096)
            (algo == "gemv" and cfg in gemv_candidates(n_tiles, k, rows, need_even)):
             return t
     if rows > 16:
-        cands = [c for c in coop_candidates(n_tiles, k, rows) if c[:3] == (1, 8, 8)]
+        allc = coop_candidates(n_tiles, k, rows)
+        cands = []
+        for pref in ((1, 8, 8), (1, 8, 4), (1, 8, 2)):
+            cands = [c for c in allc if c[:3] == pref]
+            if cands:
+                break
+        cands = cands or allc
         for c in cands:
             if (n_tiles // 8) * c[3] >= N_CU:
                 return ("coop", c)
         if cands:
             return ("coop", cands[-1])
+    if rows > 64:
+        raise ValueError(f"no projection config for {n_tiles * 16}x{k} at {rows} rows")
     return ("gemv", gemv_config(n_tiles, rows, need_even, k))
 
 

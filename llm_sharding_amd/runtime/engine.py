@@ -107,7 +107,7 @@ def _is_gpu(device: torch.device) -> bool:
 
 
 class StageEngine:
-    DECODE_MAX_ROWS = 64  # rows handled by the weight-streaming GEMV path
+    DECODE_MAX_ROWS = packing.GEMV_MAX_ROWS  # rows handled by the weight-streaming GEMV paths (128)
 
     def __init__(self, cfg: LlamaConfig, start: int, end: int, device="cpu",
                  dtype=torch.bfloat16, *, has_embed: bool = False, has_head: bool = False,

@@ -30,7 +30,8 @@ def main():
     lens = [int(x) for x in a.lengths.split(",")]
     t0 = time.perf_counter()
     eng = StageEngine(cfg, 0, cfg.num_hidden_layers, dev, torch.bfloat16, has_embed=True, has_head=True,
-                      source=RandomSource(cfg, 0), max_slots=16, max_seq=max(lens) + a.decode_steps + 8,
+                      source=RandomSource(cfg, 0), max_slots=max(int(x) for x in a.decode_batches.split(",")),
+                      max_seq=max(lens) + a.decode_steps + 8,
                       max_prefill_rows=max(lens))
     torch.cuda.synchronize()
     print(f"[sweep] {cfg.name} loaded in {time.perf_counter() - t0:.1f}s", flush=True)

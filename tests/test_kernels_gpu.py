@@ -42,7 +42,7 @@ def test_native_library_loaded_in_process():
     assert len(runtimes) == 1, runtimes
 
 
-@pytest.mark.parametrize("M", [1, 3, 16, 17, 40, 64])
+@pytest.mark.parametrize("M", [1, 3, 16, 17, 40, 64, 65, 128])
 @pytest.mark.parametrize("N,K", [(4096, 4096), (256, 11008), (512, 256)])
 def test_gemv_store(M, N, K):
     h = hip()
@@ -98,7 +98,7 @@ def test_gemv_coop_every_config(cfg):
     uneven chunk splits (K = 11008 -> 43 or 86 chunks)."""
     h = hip()
     mb, tnw, nw, kf = cfg
-    M = {2: 29, 4: 50}[mb]
+    M = {2: 29, 4: 50, 8: 100}[mb]
     N = 16 * tnw * nw * 3
     for K in (11008, 512):
         x = _rnd(M, K)
