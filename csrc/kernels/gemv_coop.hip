@@ -307,7 +307,7 @@ int launch(bool norm, const bf16_raw* x, int ldx, const int* a_rows, const bf16_
 
 #define LSA_COOP_CONFIGS(X) \
   X(2, 1, 8, 8) X(4, 1, 8, 8) X(2, 1, 8, 4) X(4, 1, 8, 4) X(2, 2, 8, 4) X(4, 2, 8, 4) X(2, 2, 4, 4) X(4, 2, 4, 4) \
-  X(8, 1, 8, 4) X(8, 1, 8, 2) X(8, 2, 4, 2)
+  X(8, 1, 8, 4) X(8, 1, 8, 2) X(8, 2, 4, 2) X(2, 1, 4, 4) X(4, 1, 4, 4) X(2, 1, 4, 8) X(8, 1, 4, 2)
 
 template <int EPI>
 int dispatch(int mb, int tnw, int nw, int kf, bool norm, const bf16_raw* x, int ldx, const int* a_rows, const bf16_raw* wp, int M, int N,

@@ -96,7 +96,8 @@ def gemv_candidates(n_tiles: int, k: int, rows: int, need_even: bool = False) ->
 
 # (mb, tnw, nw, kf) instantiated in csrc/kernels/gemv_coop.hip (LSA_COOP_CONFIGS) - keep in sync.
 COOP_CONFIGS = [(2, 1, 8, 8), (4, 1, 8, 8), (2, 1, 8, 4), (4, 1, 8, 4), (2, 2, 8, 4), (4, 2, 8, 4),
-                (2, 2, 4, 4), (4, 2, 4, 4), (8, 1, 8, 4), (8, 1, 8, 2), (8, 2, 4, 2)]
+                (2, 2, 4, 4), (4, 2, 4, 4), (8, 1, 8, 4), (8, 1, 8, 2), (8, 2, 4, 2), (2, 1, 4, 4), (4, 1, 4, 4),
+                (2, 1, 4, 8), (8, 1, 4, 2)]
 GEMV_MAX_ROWS = 128  # rows 65..128 are served by the coop kernel only
 COOP_SPLITS = (1, 2, 4, 8, 16)
 
