@@ -38,7 +38,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=64)
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--model", default="llama2-7b")
-    ap.add_argument("--batch", type=int, default=32, help="sequences per micro-batch (per GPU)")
+    ap.add_argument("--batch", type=int, default=64, help="sequences per micro-batch (per GPU)")
     ap.add_argument("--prompt-len", type=int, default=128)
     ap.add_argument("--max-seq", type=int, default=1024)
     ap.add_argument("--microbatches", type=int, default=0, help="0 = one per pipeline stage")

@@ -54,7 +54,7 @@ def lib() -> ctypes.CDLL:
     vp, i, f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
     L.lsa_gemv.argtypes = [vp, i, vp, vp, i, i, i, i, f, i, ctypes.POINTER(EpiArgs), i, i, i, vp]
     L.lsa_gemv_coop.argtypes = [vp, i, vp, vp, i, i, i, i, f, i, ctypes.POINTER(EpiArgs), i, i, i, i, vp, vp, vp]
-    L.lsa_gemm.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(EpiArgs), i, vp]
+    L.lsa_gemm.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(EpiArgs), i, i, vp, vp, vp]
     L.lsa_attn_decode.argtypes = [vp, i, vp, vp, vp, vp, vp, i, i, i, i, i, f, i, i, vp, vp, vp, i, vp]
     L.lsa_attn_prefill.argtypes = [vp, i, vp, vp, vp, i, i, i, i, i, f, i, vp, i, vp]
     L.lsa_embed.argtypes = [vp, i, vp, i, vp, i, vp]
@@ -168,9 +168,24 @@ def gemv(x: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep
     _check(rc, "lsa_gemv")
 
 
+def gemm_split(M: int, N: int, K: int, tn: int) -> int:
+    """Split-K factor for the prefill GEMM, fitted to the MI355X sweep
+    (profiles/r1_gemm_splitk_sweep.jsonl): small grids (few 128-row x 64*tn-col tiles) are split
+    over K until ~384*sqrt(K/4096) workgroups stream the weights (long-K shapes like down_proj
+    want more), at most 8 ways and >= 8 K-tiles of 64 per split."""
+    tiles = -(-M // 128) * (N // (64 * tn))
+    target = 384.0 * (K / 4096.0) ** 0.5
+    return int(max(1, min(8, int(target // tiles), (K // 64) // 8)))
+
+
+def gemm_slab_floats(M: int, N: int, sk: int) -> int:
+    return 0 if sk <= 1 else sk * (-(-M // 128) * 128) * N
+
+
 def gemm(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep: EpiArgs,
-         tn: int = 2) -> None:
-    """Prefill projection (any M). N must be a multiple of 64*tn, K of 64."""
+         tn: int = 2, sk: int = 0, ws: Optional["CoopWorkspace"] = None) -> None:
+    """Prefill projection (any M). N must be a multiple of 64*tn, K of 64. ``sk`` = split-K
+    factor (0 = :func:`gemm_split`; > 1 needs a workspace: ``ws`` or the per-stream default)."""
     _req(_is_bf16_cuda(a, wp), "gemm: bf16 cuda tensors required")
     _req(wp.numel() == N * K and K % 64 == 0, "gemm: packed weight shape")
     _req(a.dim() == 2 and a.shape[0] >= M and a.shape[1] >= K and a.stride(1) == 1, "gemm: A shape")
@@ -178,7 +193,21 @@ def gemm(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep
         tn = 1
     _req(N % (64 * tn) == 0, f"gemm: N={N} not a multiple of {64 * tn}")
     _req(not (epi == EPI_SWIGLU and tn != 2), "gemm: SwiGLU needs N % 128 == 0")
-    rc = lib().lsa_gemm(_p(a), a.stride(0), _p(wp), M, N, K, epi, ctypes.byref(ep), tn, _stream())
+    if sk == 0:
+        sk = gemm_split(M, N, K, tn)
+    _req(1 <= sk <= K // 64, f"gemm: split-K {sk} out of range")
+    slab = cnt = None
+    if sk > 1:
+        if ws is None:
+            ws = default_workspace(a.device)
+        need = gemm_slab_floats(M, N, sk)
+        tiles = -(-M // 128) * (N // (64 * tn))
+        if ws.slab.numel() < need or ws.counters.numel() < tiles:
+            sk = 1  # workspace too small for this call: fall back to the unsplit kernel
+        else:
+            slab, cnt = ws.slab, ws.counters
+    rc = lib().lsa_gemm(_p(a), a.stride(0), _p(wp), M, N, K, epi, ctypes.byref(ep), tn, sk, _p(slab), _p(cnt),
+                        _stream())
     _check(rc, "lsa_gemm")
 
 

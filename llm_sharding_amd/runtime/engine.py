@@ -218,7 +218,8 @@ class StageEngine:
             if self.has_head:
                 shapes.append((cfg.vocab_size, H))
             floats, groups = packing.coop_workspace_need(shapes, self.DECODE_MAX_ROWS, even_n=((2 * I, H),))
-            self.coop_ws = hip.CoopWorkspace(dev, slab_floats=max(floats, 1 << 16), groups=max(groups, 4096))
+            # the prefill GEMM's split-K slabs (small-M grids only) share it: <= 64 MB
+            self.coop_ws = hip.CoopWorkspace(dev, slab_floats=max(floats, 1 << 24), groups=max(groups, 4096))
 
     def memory_bytes(self) -> int:
         n = 0
@@ -347,7 +348,7 @@ class StageEngine:
                 hip.gemv(hbuf, lw.qkv, rows, cfg.qkv_size, H, hip.EPI_QKV, ep_qkv, norm=True, eps=eps, ws=ws)
             else:
                 hip.rmsnorm(hbuf, None, xn, rows, eps, H)
-                hip.gemm(xn, lw.qkv, rows, cfg.qkv_size, H, hip.EPI_QKV, ep_qkv)
+                hip.gemm(xn, lw.qkv, rows, cfg.qkv_size, H, hip.EPI_QKV, ep_qkv, ws=ws)
             if tiles is not None:
                 hip.attn_prefill(q, kc, vc, tiles[1], nh, nkv, hd, attn_o, causal=kv_len is None, tiles_host=tiles[0])
             else:
@@ -360,10 +361,10 @@ class StageEngine:
                 hip.gemv(hbuf, lw.gate_up, rows, 2 * I, H, hip.EPI_SWIGLU, ep_gu, norm=True, eps=eps, ws=ws)
                 hip.gemv(act, lw.down, rows, H, I, hip.EPI_RESID, ep_o, ws=ws)
             else:
-                hip.gemm(attn_o, lw.o, rows, H, cfg.q_size, hip.EPI_RESID, ep_o)
+                hip.gemm(attn_o, lw.o, rows, H, cfg.q_size, hip.EPI_RESID, ep_o, ws=ws)
                 hip.rmsnorm(hbuf, None, xn, rows, eps, H)
-                hip.gemm(xn, lw.gate_up, rows, 2 * I, H, hip.EPI_SWIGLU, ep_gu)
-                hip.gemm(act, lw.down, rows, H, I, hip.EPI_RESID, ep_o)
+                hip.gemm(xn, lw.gate_up, rows, 2 * I, H, hip.EPI_SWIGLU, ep_gu, ws=ws)
+                hip.gemm(act, lw.down, rows, H, I, hip.EPI_RESID, ep_o, ws=ws)
         return hbuf
 
     # ------------------------------------------------------------------------- torch path (CPU)

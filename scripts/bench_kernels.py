@@ -125,16 +125,24 @@ def attn_sweep(out_rows):
             out_rows.append(line)
 
 
-def gemm_sweep(out_rows):
+def gemm_sweep(out_rows, rows_list=(128, 256, 512, 1024, 2048, 8192)):
+    ws = hip.CoopWorkspace(DEV, slab_floats=1 << 26, groups=1 << 15)
     for (N, K) in ((12288, 4096), (4096, 4096), (22016, 4096), (4096, 11008)):
         w = packing.pack_b(torch.randn(N, K, device=DEV).mul_(0.02).to(torch.bfloat16))
-        for M in (128, 512, 2048, 8192):
+        for M in rows_list:
             a = torch.randn(M, K, device=DEV).to(torch.bfloat16)
             out = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
             ep = hip.make_epi(out=out, ldo=N)
-            us = timeit(lambda i: hip.gemm(a, w, M, N, K, hip.EPI_STORE, ep), reps=10)
-            line = {"kernel": "gemm", "N": N, "K": K, "M": M, "us": round(us, 1),
-                    "TFLOPs": round(2 * M * N * K / us / 1e6, 1)}
+            res = []
+            for sk in (1, 2, 3, 4, 6, 8):
+                if sk > 1 and hip.gemm_slab_floats(M, N, sk) > ws.slab.numel():
+                    continue
+                us = timeit(lambda i: hip.gemm(a, w, M, N, K, hip.EPI_STORE, ep, sk=sk, ws=ws), reps=10)
+                res.append((round(us, 1), sk))
+            res.sort()
+            auto = hip.gemm_split(M, N, K, 2 if N % 128 == 0 else 1)
+            line = {"kernel": "gemm", "N": N, "K": K, "M": M, "best_us": res[0][0], "best_sk": res[0][1],
+                    "auto_sk": auto, "TFLOPs": round(2 * M * N * K / res[0][0] / 1e6, 1), "all(us,sk)": res}
             print(json.dumps(line), flush=True)
             out_rows.append(line)
 
