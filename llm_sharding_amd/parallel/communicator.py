@@ -11,6 +11,12 @@ Same constructor and methods as the reference - ``Communicator(src_addr, dst_add
 * ``backend="local"``: in-process mailboxes keyed by address (several NodeWorkers in one
   process, like the reference's 4-stage loopback harness ``node_profiler.py:1174-1236``,
   without sockets).
+* ``backend="rccl"``: the message envelope still travels over the TCP transport, but every
+  tensor in it is replaced by a (shape, dtype) placeholder and its bytes go device-to-device
+  with ``torch.distributed`` send/recv to the neighbouring rank - RCCL over xGMI on MI355X
+  (gloo on CPU). Ranks default to the ring of a torchrun job in stage order (receive from
+  rank-1, send to rank+1); ``rccl_ranks=(src_rank, dst_rank)`` overrides. Received tensors
+  land on ``device``.
 
 ``receive_data(no_block=True)`` raises :class:`Again` when nothing is queued, like
 ``zmq.Again``; ``timeout_ms`` adds a bounded blocking wait (the reference only offers busy
@@ -45,15 +51,53 @@ def reset_local_transport() -> None:
         _LOCAL_BOXES.clear()
 
 
+_TENSOR_KEY = "__rccl_tensor__"
+
+
+def _extract_tensors(obj, out: list):
+    """Replace every tensor in a (nested) message by a placeholder; collect the tensors."""
+    import torch
+    if isinstance(obj, torch.Tensor):
+        out.append(obj)
+        return {_TENSOR_KEY: len(out) - 1, "shape": list(obj.shape), "dtype": str(obj.dtype).split(".")[-1]}
+    if isinstance(obj, dict):
+        return {k: _extract_tensors(v, out) for k, v in obj.items()}
+    if isinstance(obj, (list, tuple)):
+        r = [_extract_tensors(v, out) for v in obj]
+        return r if isinstance(obj, list) else tuple(r)
+    return obj
+
+
+def _restore_tensors(obj, fetch):
+    if isinstance(obj, dict):
+        if _TENSOR_KEY in obj:
+            return fetch(obj)
+        return {k: _restore_tensors(v, fetch) for k, v in obj.items()}
+    if isinstance(obj, list):
+        return [_restore_tensors(v, fetch) for v in obj]
+    if isinstance(obj, tuple):
+        return tuple(_restore_tensors(v, fetch) for v in obj)
+    return obj
+
+
 class Communicator:
-    def __init__(self, src_addr: str, dst_addr: str, backend: str = "tcp"):
+    def __init__(self, src_addr: str, dst_addr: str, backend: str = "tcp", device=None,
+                 rccl_ranks: Optional[tuple] = None):
         self.backend = backend
         self.src_addr = src_addr
         self.dst_addr = dst_addr
         self.sent_messages = 0
         self.received_messages = 0
         self._fault_drop = 0
-        if backend == "tcp":
+        self.device = device
+        self._pending_sends: list = []
+        if backend == "rccl":
+            import torch.distributed as dist
+            if not dist.is_initialized():
+                raise RuntimeError("rccl backend: torch.distributed is not initialised (launch with torchrun)")
+            r, w = dist.get_rank(), dist.get_world_size()
+            self.src_rank, self.dst_rank = rccl_ranks if rccl_ranks is not None else ((r - 1) % w, (r + 1) % w)
+        if backend in ("tcp", "rccl"):
             self.recv_socket = PullSocket(src_addr)
             self.actual_src_addr = self.recv_socket.last_endpoint
             self.send_socket = PushSocket(dst_addr)
@@ -66,7 +110,7 @@ class Communicator:
 
     # -- address changes (live re-configuration, reference :31-42) -----------------------
     def change_src_addr(self, new_src_addr: str) -> str:
-        if self.backend == "tcp":
+        if self.backend in ("tcp", "rccl"):
             if new_src_addr != self.src_addr:
                 self.recv_socket.close()
                 self.recv_socket = PullSocket(new_src_addr)
@@ -78,7 +122,7 @@ class Communicator:
         return self.src_addr
 
     def change_dst_addr(self, new_dst_addr: str) -> str:
-        if self.backend == "tcp" and new_dst_addr != self.dst_addr:
+        if self.backend in ("tcp", "rccl") and new_dst_addr != self.dst_addr:
             self.send_socket.close()
             self.send_socket = PushSocket(new_dst_addr)
         self.dst_addr = new_dst_addr
@@ -86,9 +130,14 @@ class Communicator:
 
     # -- data --------------------------------------------------------------------------
     def transfer_data(self, data, data_path: str = "results/send_data.pt", keep_data: bool = False):
+        tensors: list = []
+        if self.backend == "rccl":
+            data = _extract_tensors(data, tensors)
         payload = protocol.encode(data)
-        if self.backend == "tcp":
+        if self.backend in ("tcp", "rccl"):
             self.send_socket.send_bytes(payload)
+            if tensors:
+                self._send_tensors(tensors)
         else:
             _local_box(self.dst_addr).put(payload)
         self.sent_messages += 1
@@ -102,7 +151,7 @@ class Communicator:
     def receive_data(self, no_block: bool = False, data_path: str = "results/recv_data.pt",
                      keep_data: bool = False, timeout_ms: Optional[int] = None):
         tmo = 0 if no_block else (-1 if timeout_ms is None else int(timeout_ms))
-        if self.backend == "tcp":
+        if self.backend in ("tcp", "rccl"):
             payload = self.recv_socket.recv_bytes(tmo)
         else:
             try:
@@ -114,18 +163,48 @@ class Communicator:
             os.makedirs(os.path.dirname(data_path) or ".", exist_ok=True)
             with open(data_path, "wb") as f:
                 f.write(payload)
-        return protocol.decode(payload)
+        msg = protocol.decode(payload)
+        if self.backend == "rccl":
+            msg = _restore_tensors(msg, self._recv_tensor)
+        return msg
+
+    # -- rccl tensor side channel --------------------------------------------------------
+    def _send_tensors(self, tensors: list) -> None:
+        import torch.distributed as dist
+        for t in tensors:
+            t = t.contiguous()
+            if self.device is not None and t.device != self.device and str(self.device) != "cpu":
+                t = t.to(self.device)
+            self._pending_sends.append((dist.isend(t, self.dst_rank), t))
+        # bound the outstanding sends (their tensors must stay alive until complete)
+        while len(self._pending_sends) > 16:
+            w, _ = self._pending_sends.pop(0)
+            w.wait()
+
+    def _recv_tensor(self, ph: dict):
+        import torch
+        import torch.distributed as dist
+        dev = self.device if self.device is not None else "cpu"
+        t = torch.empty(ph["shape"], dtype=getattr(torch, ph["dtype"]), device=dev)
+        dist.recv(t, self.src_rank)
+        return t
 
     def flush(self, timeout_ms: int = 5000) -> bool:
-        return self.send_socket.flush(timeout_ms) if self.backend == "tcp" else True
+        for w, _ in self._pending_sends:
+            w.wait()
+        self._pending_sends.clear()
+        return self.send_socket.flush(timeout_ms) if self.backend in ("tcp", "rccl") else True
 
     def inject_faults(self, drop_every: int = 0, delay_ms: int = 0) -> None:
         """Test hook: drop every Nth outgoing message / delay each one (tcp backend)."""
-        if self.backend == "tcp":
+        if self.backend in ("tcp", "rccl"):
             self.send_socket.inject_faults(drop_every, delay_ms)
 
     def close(self) -> None:
-        if self.backend == "tcp":
+        if self.backend in ("tcp", "rccl"):
+            for w, _ in self._pending_sends:
+                w.wait()
+            self._pending_sends.clear()
             self.send_socket.close(linger_ms=1000)
             self.recv_socket.close()
 

@@ -65,8 +65,11 @@ class NodeWorker:
     def __init__(self, src_addr: str, dst_addr: str, can_receive_user_request: bool, shards_path: str,
                  device="cpu", dtype=torch.float16, backend: str = "tcp", max_batch: int = 8,
                  max_seq: int = 4096, noncausal_prefill: bool = False,
-                 source: Optional[WeightSource] = None, verbose: bool = True):
-        self.communicator = Communicator(src_addr=src_addr, dst_addr=dst_addr, backend=backend)
+                 source: Optional[WeightSource] = None, verbose: bool = True,
+                 rccl_ranks: Optional[tuple] = None):
+        # backend "rccl": envelopes over TCP, tensors device-to-device over torch.distributed
+        self.communicator = Communicator(src_addr=src_addr, dst_addr=dst_addr, backend=backend,
+                                         device=torch.device(device), rccl_ranks=rccl_ranks)
         self.can_receive_user_request = can_receive_user_request
         self.shards_path = shards_path
         self.device = torch.device(device)
@@ -359,9 +362,12 @@ class NodeController:
             self.node_worker.close()  # Q9: release the old sockets before rebinding
             self.node_worker = None
         self._set_first_node_addr(cfg)
+        kw = dict(self.worker_kwargs)
+        if cfg.get("rccl_ranks") is not None:  # optional extension key: (src_rank, dst_rank)
+            kw["rccl_ranks"] = tuple(cfg["rccl_ranks"])
         self.node_worker = NodeWorker(cfg["src_addr"], cfg["dst_addr"], cfg["can_receive_user_request"],
                                       self.shards_path, device=self.device, dtype=self.dtype, backend=self.backend,
-                                      verbose=self.verbose, **self.worker_kwargs)
+                                      verbose=self.verbose, **kw)
         self.node_worker.load_shards(cfg["shards_start"], cfg["shards_end"])
 
     def _set_first_node_addr(self, cfg: dict) -> None:

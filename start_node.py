@@ -3,6 +3,10 @@
 tcp://*:<port>, load the assigned layer range, serve the chain until shut down.
 
     python start_node.py [--port 40700 | 40700] [--shards DIR] [--device cuda:0] [--dtype bfloat16]
+
+    # one node, one controller per GPU, stage hand-off over RCCL (xGMI) instead of TCP:
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29500 \
+        start_node.py --backend rccl --port 40700 --shards DIR      # rank r listens on 40700 + r
 """
 import argparse
 import os
@@ -23,10 +27,23 @@ def main():
     ap.add_argument("--dtype", default="bfloat16")
     ap.add_argument("--max-new-tokens", type=int, default=512)
     ap.add_argument("--noncausal-prefill", action="store_true", help="reference-compatible unmasked prefill")
+    ap.add_argument("--backend", default="tcp", choices=("tcp", "rccl"),
+                    help="stage hand-off: tcp (reference-compatible) or rccl (torchrun, one rank per GPU)")
     a = ap.parse_args()
     port = a.port_pos if a.port_pos is not None else a.port
-    ctrl = NodeController(a.shards, device=a.device, dtype=getattr(torch, a.dtype), listen_port=port,
-                          worker_kwargs={"noncausal_prefill": a.noncausal_prefill})
+    device = a.device
+    if a.backend == "rccl":
+        import torch.distributed as dist
+        rank, local = int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))
+        if torch.cuda.is_available():
+            device = f"cuda:{local}"
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device(device))
+        else:
+            dist.init_process_group("gloo")
+        port += rank
+    ctrl = NodeController(a.shards, device=device, dtype=getattr(torch, a.dtype), listen_port=port,
+                          backend=a.backend, worker_kwargs={"noncausal_prefill": a.noncausal_prefill})
     ctrl.run_worker_loop(max_new_tokens=a.max_new_tokens)
     ctrl.close()
 

@@ -260,3 +260,70 @@ def test_worker_role_errors(tiny_shards):
     cmd = w.build_clear_KV_cache_command()
     assert NodeWorker.is_clear_KV_cache_command(cmd) and w.is_clear_KV_cache_command_origin(cmd)
     w.close()
+
+
+def _rccl_chain_worker(rank, port, ports, shards, n_new, q):
+    import torch.distributed as dist
+    from llm_sharding_amd.utils.node_worker import NodeWorker
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=2)
+    try:
+        w = NodeWorker(f"tcp://*:{ports[rank]}", f"tcp://127.0.0.1:{ports[1 - rank]}", rank == 0, shards,
+                       device="cpu", dtype=torch.float32, backend="rccl", verbose=False)
+        w.load_shards(0, 2) if rank == 0 else w.load_shards(2, 4)
+        if rank == 0:
+            d = w.receive_user_request(input_ids=torch.tensor([[1, 33, 44, 55, 66]]))
+            while True:
+                w.communicator.transfer_data(w.pass_through_shard(d))
+                tok = w.communicator.receive_data(timeout_ms=60000)
+                end, d = w.receive_next_token(tok, max_new_tokens=n_new)
+                if end:
+                    break
+            w.communicator.transfer_data({"command": "stop"})
+            q.put(w.output_ids()[0].tolist())
+        else:
+            while True:
+                x = w.communicator.receive_data(timeout_ms=60000)
+                if isinstance(x, dict) and x.get("command") == "stop":
+                    break
+                w.communicator.transfer_data(w.pass_through_shard(x))
+        w.communicator.flush()
+        w.close()
+    finally:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def test_communicator_rccl_backend_two_processes(tiny_shards):
+    """Reference-API NodeWorkers in two processes with backend="rccl": envelopes over TCP,
+    hidden states / token ids via torch.distributed send/recv (gloo here, RCCL on GPUs)."""
+    import multiprocessing as mp
+    import socket as _s
+    socks = [_s.socket() for _ in range(3)]
+    for s in socks:
+        s.bind(("127.0.0.1", 0))
+    ports = [s.getsockname()[1] for s in socks]
+    for s in socks:
+        s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    n_new = 5
+    ps = [ctx.Process(target=_rccl_chain_worker, args=(r, ports[2], ports[:2], tiny_shards, n_new, q))
+          for r in range(2)]
+    for p in ps:
+        p.start()
+    try:
+        got = q.get(timeout=240)
+    finally:
+        for p in ps:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+    cfg, emb, layers, fn, lm = W.load_full_model(tiny_shards)
+    prompt = torch.tensor([[1, 33, 44, 55, 66]])
+    want = ReferenceLlama(cfg, emb, layers, fn, lm).generate(prompt, n_new)[0].tolist()
+    eos = set(cfg.eos_ids)
+    if any(t in eos for t in want):
+        want = want[:next(i for i, t in enumerate(want) if t in eos) + 1]
+    assert got == prompt[0].tolist() + want
