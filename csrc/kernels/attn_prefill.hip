@@ -30,8 +30,9 @@ struct PrefillTile {
 
 template <int HD>
 LSA_DEVICE int k_off(int key, int c16) {  // K block [BK][HD] bf16, 16-B chunks swizzled per key
-  constexpr int NC = HD / 8;
-  return key * (HD * 2) + ((c16 ^ (key & (NC - 1))) << 4);
+  constexpr int NC = HD / 8;  // 16 (256-B rows): key & 15; 8 (128-B rows): (key >> 1) & 7
+  const int sw = NC >= 16 ? (key & 15) : ((key >> 1) & (NC - 1));
+  return key * (HD * 2) + ((c16 ^ sw) << 4);
 }
 template <int HD>
 LSA_DEVICE int vt_off(int dim, int g8) {  // V^T block [HD][BK] bf16, 8-B (4-key) granules swizzled per dim

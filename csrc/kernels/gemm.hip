@@ -19,7 +19,9 @@ namespace {
 constexpr int BM = 128, BK = 64, GWAVES = 4, GTHR = GWAVES * LSA_WAVE;
 
 LSA_DEVICE int lds_off(int row, int chunk) {  // byte offset of 16-B chunk in the A tile
-  return row * (BK * 2) + ((chunk ^ (row & 7)) << 4);
+  // 128-B rows: two rows share a 256-B bank line, so XOR with (row >> 1) & 7 makes the 16
+  // rows of one ds_read_b128 pass hit all 64 banks (row & 7 was 2-way conflicted)
+  return row * (BK * 2) + ((chunk ^ ((row >> 1) & 7)) << 4);
 }
 
 template <int TN, int EPI>

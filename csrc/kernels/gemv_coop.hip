@@ -18,8 +18,17 @@
 
 namespace {
 
+// A tile [MR][KC] bf16 in LDS, 16-B chunks XOR-swizzled so that the 16 lanes of one
+// ds_read_b128 pass (16 consecutive rows, same logical chunk) hit all 64 banks: rows of >= 16
+// chunks (>= 256 B) XOR with row & 15; 128-B rows pair up two rows per 256-B bank line, so
+// they XOR with (row >> 1) & 7 (measured: the old row & 7 swizzle was 2-way conflicted,
+// ~3 conflict cycles per LDS instruction in profiles/r1_coop_pmc_m64.txt).
 template <int KC>
-LSA_DEVICE int a_off(int row, int c16) { return row * (KC * 2) + ((c16 ^ (row & 7)) << 4); }
+LSA_DEVICE int a_off(int row, int c16) {
+  constexpr int C16 = KC / 8;
+  const int sw = C16 >= 16 ? (row & 15) : ((row >> 1) & (C16 - 1));
+  return row * (KC * 2) + ((c16 ^ sw) << 4);
+}
 
 template <int MB, int TNW, int NW, int KF, int EPI, bool NORM>
 __global__ __launch_bounds__(NW * 64) void gemv_coop_kernel(

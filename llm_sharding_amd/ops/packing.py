@@ -113,7 +113,7 @@ def coop_candidates(n_tiles: int, k: int, rows: int) -> list:
         if b != mb or n_tiles % (tnw * nw) or k % (32 * kf):
             continue
         for sk in COOP_SPLITS:
-            if k // (32 * kf) >= 2 * sk and (n_tiles // (tnw * nw)) * sk <= 4 * N_CU:
+            if k // (32 * kf) >= sk and (n_tiles // (tnw * nw)) * sk <= 4 * N_CU:
                 out.append((tnw, nw, kf, sk))
     return out
 
