@@ -86,7 +86,8 @@ class PipelineStage:
 
     def __init__(self, cfg, rank: int, world: int, start: int, end: int, device, batch: int,
                  microbatches: int, max_seq: int, source, use_graph: bool = True,
-                 max_prefill_rows: int = 2048, dtype=torch.bfloat16, p2p=None):
+                 max_prefill_rows: int = 2048, dtype=torch.bfloat16, p2p=None,
+                 split_head: Optional[bool] = None):
         self.cfg, self.rank, self.world = cfg, rank, world
         self.p2p = p2p if p2p is not None else DistP2P()
         self.first, self.last = rank == 0, rank == world - 1
@@ -95,12 +96,29 @@ class PipelineStage:
         self.gpu = self.device.type == "cuda"
         self.use_graph = use_graph and self.gpu
         self.dtype = torch.bfloat16 if self.gpu else dtype
+        # Split lm_head (GPU pipelines of >= 2 stages): the last stage covers vocab [0, V1), the
+        # first stage [V1, V). The ring back-edge then carries the raw final hidden + partial
+        # argmax keys instead of token ids, and the first stage completes the argmax at the
+        # start of its next step - the ~0.4-layer lm_head no longer sits on one stage only.
+        V = cfg.vocab_size
+        v1 = (V // 2) // 128 * 128
+        self.split = (world > 1 and v1 > 0) if split_head is None else split_head
+        head_cols = None
+        if self.split and self.last:
+            head_cols = (0, v1)
+        elif self.split and self.first:
+            head_cols = (v1, V)
         self.eng = StageEngine(cfg, start, end, device, self.dtype, has_embed=self.first,
-                               has_head=self.last, source=source, max_slots=batch * microbatches,
-                               max_seq=max_seq, max_prefill_rows=max(max_prefill_rows, batch))
+                               has_head=self.last or (self.split and self.first), source=source,
+                               max_slots=batch * microbatches, max_seq=max_seq,
+                               max_prefill_rows=max(max_prefill_rows, batch), head_cols=head_cols)
         H = cfg.hidden_size
         self.h_out = [torch.zeros((batch, H), dtype=self.dtype, device=self.device) for _ in range(microbatches)]
         self.tok_out = [torch.zeros(batch, dtype=torch.int32, device=self.device) for _ in range(microbatches)]
+        if self.split:
+            self.keys_out = [torch.zeros(batch, dtype=torch.int64, device=self.device) for _ in range(microbatches)]
+            self.seed = [None] * microbatches   # stage 0: (h_fin, keys) of each micro-batch's prefill
+            self.final_tokens = [None] * microbatches
         self.graphs: list = []
         self.send_works: dict = {}
         self.tokens_ready = [True] * microbatches  # stage 0: next-step token ids are in place
@@ -147,33 +165,69 @@ class PipelineStage:
             h = eng.forward(h, slot, pos)
         eng.advance(sl, [P] * B)
         if self.last:
-            tok = eng.head(h, [i * P + P - 1 for i in range(B)]).to(torch.int32)
-            if self.world == 1:
-                return tok
-            self._send(tok, 0, ("pf", mb))
-            self._wait_send(("pf", mb))
+            last_rows = [i * P + P - 1 for i in range(B)]
+            if self.split:
+                keys = eng.head_keys(h, last_rows)
+                hl = h[torch.tensor(last_rows, device=h.device)].contiguous()
+                self._send(hl, 0, ("pfh", mb))
+                self._send(keys, 0, ("pf", mb))
+                self._wait_send(("pfh", mb))
+                self._wait_send(("pf", mb))
+            else:
+                tok = eng.head(h, last_rows).to(torch.int32)
+                if self.world == 1:
+                    return tok
+                self._send(tok, 0, ("pf", mb))
+                self._wait_send(("pf", mb))
         else:
             self._send(h.clone(), self.rank + 1, ("pf", mb))
             self._wait_send(("pf", mb))
         if self.first and recv_token:
-            return self.recv_first_token()
+            return self.recv_first_token(mb)
         return None
 
-    def recv_first_token(self) -> torch.Tensor:
+    def recv_first_token(self, mb: int = 0) -> torch.Tensor:
+        if self.split:
+            hf = torch.zeros((self.B, self.cfg.hidden_size), dtype=self.dtype, device=self.device)
+            keys = torch.zeros(self.B, dtype=torch.int64, device=self.device)
+            self._recv(hf, self.world - 1)
+            self._recv(keys, self.world - 1)
+            self.seed[mb] = (hf, keys.clone())  # the decode graph recomputes token 0 from these
+            return self._complete(hf, keys)
         tok = torch.zeros(self.B, dtype=torch.int32, device=self.device)
         self._recv(tok, self.world - 1)
         return tok
 
+    def _complete(self, h_fin: torch.Tensor, keys: torch.Tensor) -> torch.Tensor:
+        """Stage 0 (split head): finish the argmax over its vocab slice -> token ids."""
+        k = self.eng.head_keys(h_fin, None, keys=keys.clone())
+        return self.eng.finalize_keys(k)
+
     # ---------------------------------------------------------------- decode
+    @property
+    def history_stage(self) -> bool:
+        """Does this stage hold the generated-token history (last stage, or stage 0 when the
+        lm_head is split)?"""
+        return self.first if self.split else self.last
+
     def build_graphs(self, first_tokens: Optional[list], history_len: int) -> None:
         mode = "full" if self.world == 1 else ("first" if self.first else ("last" if self.last else "mid"))
         self.mode = mode
         self.graphs = []
         for mb in range(self.M):
-            cls = DecodeGraph if self.gpu else EagerDecode
-            g = cls(self.eng, self.B, mode, slots=self.slots(mb), history_len=history_len if self.last else 0)
-            if first_tokens is not None and mode in ("full", "first"):
-                g.tokens.copy_(first_tokens[mb])
+            if self.split and mode in ("first", "last"):
+                # stage 0 re-derives token s at step s: one more history row than the last stage keeps
+                cls = DecodeGraph if self.gpu else EagerDecode
+                g = cls(self.eng, self.B, mode, slots=self.slots(mb),
+                        history_len=history_len + 1 if self.first else 0, split_head=True)
+                if self.first and self.seed[mb] is not None:
+                    g.h_fin.copy_(self.seed[mb][0])
+                    g.keys_in.copy_(self.seed[mb][1])
+            else:
+                cls = DecodeGraph if self.gpu else EagerDecode
+                g = cls(self.eng, self.B, mode, slots=self.slots(mb), history_len=history_len if self.last else 0)
+                if first_tokens is not None and mode in ("full", "first"):
+                    g.tokens.copy_(first_tokens[mb])
             if self.use_graph:
                 g.capture()
             self.graphs.append(g)
@@ -196,7 +250,11 @@ class PipelineStage:
             with tl.span("recv", mb=mb, step=s):
                 if self.first:
                     if not self.tokens_ready[mb]:
-                        self._recv(g.tokens, self.world - 1)
+                        if self.split:
+                            self._recv(g.h_fin, self.world - 1)
+                            self._recv(g.keys_in, self.world - 1)
+                        else:
+                            self._recv(g.tokens, self.world - 1)
                     self.tokens_ready[mb] = False
                 else:
                     self._recv(g.h_in, self.rank - 1)
@@ -207,7 +265,15 @@ class PipelineStage:
             ev.record()
             events.append((s, mb, ev))
         if self.world > 1:
-            if self.last:
+            if self.last and self.split:
+                # private copies: the next replay rewrites the engine's hidden buffer / keys
+                self._wait_send(("hb", mb))
+                self._wait_send(("tok", mb))
+                self.h_out[mb].copy_(g.out_hidden.reshape(self.h_out[mb].shape))
+                self.keys_out[mb].copy_(g.keys)
+                self._send(self.h_out[mb], 0, ("hb", mb))
+                self._send(self.keys_out[mb], 0, ("tok", mb))
+            elif self.last:
                 # the next replay rewrites g.tokens: send from a private copy, reused only
                 # after the previous send of this micro-batch completed
                 self._wait_send(("tok", mb))
@@ -224,7 +290,14 @@ class PipelineStage:
         if self.world > 1 and self.first:
             for mb, g in enumerate(self.graphs):
                 if not self.tokens_ready[mb]:
-                    self._recv(g.tokens, self.world - 1)
+                    if self.split:
+                        # the last step's keys: complete them eagerly; the inputs stay in
+                        # place, so a later replay re-derives the same token first
+                        self._recv(g.h_fin, self.world - 1)
+                        self._recv(g.keys_in, self.world - 1)
+                        self.final_tokens[mb] = self._complete(g.h_fin, g.keys_in)
+                    else:
+                        self._recv(g.tokens, self.world - 1)
                     self.tokens_ready[mb] = True
         for k in list(self.send_works):
             self._wait_send(k)
@@ -254,6 +327,12 @@ def run_pipeline_generate(cfg, source, prompts: Optional[torch.Tensor], n_new: i
     if stage.gpu:
         torch.cuda.synchronize()
     out = None
+    if stage.split:
+        if rank == 0:  # history rows: token s re-derived at step s (s = 0 .. n_new-2) + drained last
+            hist = torch.stack([g.history[:n_new - 1] for g in stage.graphs], dim=1).cpu()
+            last = torch.stack([t.cpu() for t in stage.final_tokens], dim=0)[None]
+            return torch.cat([hist, last], dim=0) if n_new > 1 else hist[:1]
+        return None
     if stage.last:
         hist = torch.stack([g.history for g in stage.graphs], dim=1).cpu()  # [n_new-1, M, B]
         out = hist
@@ -286,7 +365,7 @@ def drive_local_pipeline(cfg, source, prompts: torch.Tensor, n_new: int, n_stage
     for mb in range(microbatches):
         for st in stages:
             st.prefill_mb(mb, prompts if st.first else None, P, recv_token=False)
-        firsts.append(stages[0].recv_first_token())
+        firsts.append(stages[0].recv_first_token(mb))
     for st in stages:
         st.build_graphs(firsts if st.first else None, history_len=n_new - 1)
     for s in range(n_new - 1):
@@ -297,6 +376,10 @@ def drive_local_pipeline(cfg, source, prompts: torch.Tensor, n_new: int, n_stage
         st.drain()
     if stages[0].gpu:
         torch.cuda.synchronize()
+    if stages[0].split:
+        hist = torch.stack([g.history[:n_new - 1] for g in stages[0].graphs], dim=1).cpu()
+        last = torch.stack([t.cpu() for t in stages[0].final_tokens], dim=0)[None]
+        return torch.cat([hist, last], dim=0)
     hist = torch.stack([g.history for g in stages[-1].graphs], dim=1).cpu()
     first = torch.stack([f.cpu() for f in firsts], dim=0)[None]
     return torch.cat([first, hist], dim=0)
@@ -406,7 +489,7 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
     trace = tracing.export_env(stage.tl)
     if trace and verbose:
         print(f"[bench] rank {rank} timeline -> {trace}  {stage.tl.summary()}", flush=True)
-    if stage.last and verbose:
+    if stage.history_stage and verbose:
         hist = stage.graphs[0].history[:8, :4].cpu().tolist() if stage.graphs[0].history is not None else []
         print(f"[bench] rank {rank} sample tokens (step x seq): {hist}", flush=True)
     if dist:

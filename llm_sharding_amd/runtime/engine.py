@@ -106,6 +106,22 @@ def _is_gpu(device: torch.device) -> bool:
     return device.type == "cuda"
 
 
+_I64_MIN = -(1 << 63)
+
+
+def argmax_keys_torch(v: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
+    """CPU mirror of common.h ``argmax_key``: (order-preserving fp32 bits << 32) |
+    (0xffffffff - index), as the int64 bit pattern of the unsigned 64-bit key."""
+    u = v.float().contiguous().view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+    k = torch.where(u >= 0x80000000, (~u) & 0xFFFFFFFF, u | 0x80000000)
+    return (k << 32) | (0xFFFFFFFF - idx.to(torch.int64))
+
+
+def keys_max_torch(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """Elementwise UNSIGNED max of int64-stored 64-bit keys."""
+    return torch.where((a ^ _I64_MIN) >= (b ^ _I64_MIN), a, b)
+
+
 class StageEngine:
     DECODE_MAX_ROWS = packing.GEMV_MAX_ROWS  # rows handled by the weight-streaming GEMV paths (128)
 
@@ -113,7 +129,7 @@ class StageEngine:
                  dtype=torch.bfloat16, *, has_embed: bool = False, has_head: bool = False,
                  source: Optional[WeightSource] = None, max_slots: int = 1, max_seq: int = 2048,
                  max_prefill_rows: int = 2048, causal: bool = True, load: bool = True,
-                 verbose: bool = False):
+                 verbose: bool = False, head_cols: Optional[tuple] = None):
         if not (0 <= start < end <= cfg.num_hidden_layers):
             raise ValueError(f"[ERROR] invalid layer range [{start}, {end})")
         self.cfg = cfg
@@ -125,6 +141,11 @@ class StageEngine:
             raise ValueError("the HIP path computes in bfloat16 (pass dtype=torch.bfloat16)")
         self.dtype = dtype
         self.has_embed, self.has_head = has_embed, has_head
+        # vocab rows [v0, v1) of the lm_head held here (a pipeline may split the head between its
+        # last and first stage so that neither carries the whole 0.4-layer lm_head)
+        self.head_v0, self.head_v1 = head_cols if head_cols is not None else (0, cfg.vocab_size)
+        if not (0 <= self.head_v0 < self.head_v1 <= cfg.vocab_size) or (self.head_v1 - self.head_v0) % 16:
+            raise ValueError(f"bad head_cols {head_cols}")
         self.source = source
         self.max_slots = int(max_slots)
         self.max_seq = int(min(max_seq, cfg.max_position_embeddings))
@@ -166,6 +187,8 @@ class StageEngine:
             self._log("[INFO] loading final norm / lm_head...")
             self.final_norm = src.final_norm(dev, dt).contiguous()
             lm = src.lm_head(dev, dt)
+            if (self.head_v0, self.head_v1) != (0, self.cfg.vocab_size):
+                lm = lm[self.head_v0:self.head_v1]
             # GPU: final RMSNorm weight folded into the packed lm_head (fused norm+GEMV+argmax)
             self.lm_head = packing.pack_b(packing.fold_norm(lm, self.final_norm)) if self.gpu else lm.contiguous()
             del lm
@@ -216,7 +239,7 @@ class StageEngine:
             from ..ops import hip
             shapes = [(cfg.qkv_size, H), (H, cfg.q_size), (2 * I, H), (H, I)]
             if self.has_head:
-                shapes.append((cfg.vocab_size, H))
+                shapes.append((self.head_v1 - self.head_v0, H))
             floats, groups = packing.coop_workspace_need(shapes, self.DECODE_MAX_ROWS, even_n=((2 * I, H),))
             # the prefill GEMM's split-K slabs (small-M grids only) share it: <= 64 MB
             self.coop_ws = hip.CoopWorkspace(dev, slab_floats=max(floats, 1 << 24), groups=max(groups, 4096))
@@ -286,22 +309,57 @@ class StageEngine:
             rows_idx = list(range(h.shape[0]))
         if self.gpu:
             from ..ops import hip
-            idx = self._i32(rows_idx)
-            n = idx.numel()
+            if (self.head_v0, self.head_v1) != (0, self.cfg.vocab_size):
+                raise RuntimeError("head(): this stage holds only part of the lm_head (use head_keys)")
+            keys = self.head_keys(h, rows_idx)
+            n = keys.numel()
             out = torch.empty(n, dtype=torch.int64, device=self.device)
             for c0 in range(0, n, self.DECODE_MAX_ROWS):
                 c = min(self.DECODE_MAX_ROWS, n - c0)
-                keys = self.keys[:c]
-                keys.zero_()
-                ep = hip.make_epi(keys=keys)
-                hip.gemv(h, self.lm_head, c, self.cfg.vocab_size, self.cfg.hidden_size, hip.EPI_ARGMAX, ep, ws=self.coop_ws,
-                         norm=True, eps=self.cfg.rms_norm_eps, a_rows=idx[c0:c0 + c])
-                hip.argmax_finalize(keys, c, self.tokens)
+                hip.argmax_finalize(keys[c0:c0 + c], c, self.tokens)
                 out[c0:c0 + c] = self.tokens[:c].long()
             return out
         hs = h[torch.as_tensor(rows_idx, device=h.device, dtype=torch.long)]
         lg = self.logits_torch(hs)
         return torch.argmax(lg, dim=-1)
+
+    def head_keys(self, h: torch.Tensor, rows_idx=None, keys: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Fused final-norm + (partial) lm_head + argmax KEYS of the selected rows over this
+        stage's vocab slice [head_v0, head_v1): the 64-bit (ordered logit, inverted index) keys of
+        common.h ``argmax_key``, so two slices combine by an unsigned max. ``keys`` (int64 [n]:
+        pass the other slice's keys to complete them) defaults to zeros. Returns keys."""
+        if rows_idx is None:
+            rows_idx = list(range(h.shape[0]))
+        if not self.gpu:
+            hs = h[torch.as_tensor(rows_idx, device=h.device, dtype=torch.long)]
+            v, i = self.logits_torch(hs).max(-1)
+            new = argmax_keys_torch(v, i + self.head_v0)
+            return new if keys is None else keys_max_torch(keys, new)
+        from ..ops import hip
+        idx = self._i32(rows_idx)
+        n = idx.numel()
+        if keys is None:
+            keys = torch.zeros(n, dtype=torch.int64, device=self.device)
+        for c0 in range(0, n, self.DECODE_MAX_ROWS):
+            c = min(self.DECODE_MAX_ROWS, n - c0)
+            ep = hip.make_epi(keys=keys[c0:c0 + c], col_offset=self.head_v0)
+            hip.gemv(h, self.lm_head, c, self.head_v1 - self.head_v0, self.cfg.hidden_size, hip.EPI_ARGMAX, ep,
+                     ws=self.coop_ws, norm=True, eps=self.cfg.rms_norm_eps, a_rows=idx[c0:c0 + c])
+        return keys
+
+    def finalize_keys(self, keys: torch.Tensor) -> torch.Tensor:
+        """argmax keys -> token ids (int32, device); resets ``keys``."""
+        if not self.gpu:
+            tok = (0xFFFFFFFF - (keys & 0xFFFFFFFF)).to(torch.int32)
+            keys.zero_()
+            return tok
+        from ..ops import hip
+        n = keys.numel()
+        out = torch.empty(n, dtype=torch.int32, device=self.device)
+        for c0 in range(0, n, self.DECODE_MAX_ROWS):
+            c = min(self.DECODE_MAX_ROWS, n - c0)
+            hip.argmax_finalize(keys[c0:c0 + c], c, out[c0:c0 + c])
+        return out
 
     def logits_torch(self, hs: torch.Tensor) -> torch.Tensor:
         from ..models.reference import rmsnorm
@@ -449,7 +507,7 @@ class DecodeGraph:
     """
 
     def __init__(self, eng: StageEngine, rows: int, mode: str, slots: Optional[list] = None,
-                 history_len: int = 0):
+                 history_len: int = 0, split_head: bool = False):
         from ..ops import hip
         if not eng.gpu:
             raise RuntimeError("DecodeGraph needs a GPU stage")
@@ -467,16 +525,38 @@ class DecodeGraph:
         self.step_ctr = torch.zeros(1, dtype=torch.int32, device=dev)
         self.graph = None
         self._hip = hip
+        # split lm_head (pipeline): "last" leaves partial keys over its vocab slice + the raw
+        # final hidden; "first" completes the PREVIOUS step's keys over its slice from
+        # (h_fin, keys_in), finalises the token ids (and history) and then embeds them
+        self.split_head = split_head
+        if split_head:
+            if mode not in ("first", "last"):
+                raise ValueError("split_head needs mode 'first' or 'last'")
+            self.h_fin = torch.zeros((rows, eng.cfg.hidden_size), dtype=torch.bfloat16, device=dev)
+            self.keys_in = torch.zeros(rows, dtype=torch.int64, device=dev)
 
     def _body(self) -> None:
         hip, eng, rows = self._hip, self.eng, self.rows
         h = eng.buf_h[:rows]
+        if self.split_head and self.mode == "first":
+            self.keys.copy_(self.keys_in)
+            ep = hip.make_epi(keys=self.keys, col_offset=eng.head_v0)
+            hip.gemv(self.h_fin, eng.lm_head, rows, eng.head_v1 - eng.head_v0, eng.cfg.hidden_size, hip.EPI_ARGMAX,
+                     ep, ws=eng.coop_ws, norm=True, eps=eng.cfg.rms_norm_eps)
+            hip.argmax_finalize(self.keys, rows, self.tokens, None, 1, self.history,
+                                self.step_ctr if self.history is not None else None)
         if self.mode in ("full", "first"):
             hip.embed(self.tokens, eng.embed_w, h)
         else:
             h.copy_(self.h_in)
         eng._forward_hip(h, self.slot, self.pos, None, rows, nsplit=eng.decode_nsplit(rows))
-        if self.mode in ("full", "last"):
+        if self.split_head and self.mode == "last":
+            self.keys.zero_()
+            ep = hip.make_epi(keys=self.keys, col_offset=eng.head_v0)
+            hip.gemv(h, eng.lm_head, rows, eng.head_v1 - eng.head_v0, eng.cfg.hidden_size, hip.EPI_ARGMAX, ep,
+                     ws=eng.coop_ws, norm=True, eps=eng.cfg.rms_norm_eps)
+            hip.pos_advance(self.pos, rows, 1)
+        elif self.mode in ("full", "last"):
             ep = hip.make_epi(keys=self.keys)
             hip.gemv(h, eng.lm_head, rows, eng.cfg.vocab_size, eng.cfg.hidden_size, hip.EPI_ARGMAX, ep, ws=eng.coop_ws,
                      norm=True, eps=eng.cfg.rms_norm_eps)
@@ -492,6 +572,7 @@ class DecodeGraph:
     def capture(self, warmup: bool = True) -> "DecodeGraph":
         """Capture the step. The warm-up replay (if any) is undone (positions restored)."""
         pos0, tok0 = self.pos.clone(), self.tokens.clone()
+        kin0 = self.keys_in.clone() if self.split_head else None
         s = torch.cuda.Stream(device=self.eng.device)
         s.wait_stream(torch.cuda.current_stream(self.eng.device))
         with torch.cuda.stream(s):
@@ -506,6 +587,10 @@ class DecodeGraph:
         self.tokens.copy_(tok0)
         self.keys.zero_()
         self.step_ctr.zero_()
+        if kin0 is not None:
+            self.keys_in.copy_(kin0)
+        if self.history is not None:
+            self.history.zero_()
         return self
 
     def replay(self) -> None:
@@ -525,7 +610,7 @@ class EagerDecode:
     used by the multi-process gloo tests): one decode step per ``_body()`` call."""
 
     def __init__(self, eng: StageEngine, rows: int, mode: str, slots: Optional[list] = None,
-                 history_len: int = 0):
+                 history_len: int = 0, split_head: bool = False):
         self.eng, self.rows, self.mode = eng, rows, mode
         self.slots = list(range(rows)) if slots is None else list(slots)
         self.tokens = torch.zeros(rows, dtype=torch.int32)
@@ -533,14 +618,25 @@ class EagerDecode:
         self.history = torch.zeros((history_len, rows), dtype=torch.int32) if history_len else None
         self.step = 0
         self._out = None
+        self.split_head = split_head
+        self.keys = torch.zeros(rows, dtype=torch.int64)
+        self.h_fin = torch.zeros((rows, eng.cfg.hidden_size), dtype=eng.dtype)
+        self.keys_in = torch.zeros(rows, dtype=torch.int64)
 
     def _body(self) -> None:
         eng = self.eng
+        if self.split_head and self.mode == "first":  # complete the previous step's argmax
+            self.tokens.copy_(eng.finalize_keys(eng.head_keys(self.h_fin, None, keys=self.keys_in.clone())))
+            if self.history is not None and self.step < self.history.shape[0]:
+                self.history[self.step] = self.tokens
+            self.step += 1
         h = eng.embed(self.tokens) if self.mode in ("full", "first") else self.h_in
         slot, pos = eng.prefill_rows(self.slots, [1] * self.rows)
         h = eng.forward(h, slot, pos)
         eng.advance(self.slots, [1] * self.rows)
-        if self.mode in ("full", "last"):
+        if self.split_head and self.mode == "last":
+            self.keys.copy_(eng.head_keys(h))
+        elif self.mode in ("full", "last"):
             self.tokens.copy_(eng.head(h).to(torch.int32))
             if self.history is not None and self.step < self.history.shape[0]:
                 self.history[self.step] = self.tokens
