@@ -310,7 +310,7 @@ def run_pipeline_generate(cfg, source, prompts: Optional[torch.Tensor], n_new: i
     initialised; gloo on CPU or nccl/RCCL on GPUs). ``prompts`` [M, B, P] on rank 0.
     Returns [n_new, M, B] generated ids on rank 0 (gathered from the last stage)."""
     import torch.distributed as dist
-    plan = plan or plan_stages(cfg, world)
+    plan = plan or plan_stages(cfg, world, head_split=world > 1)
     st = plan.stages[rank]
     P = int(prompts.shape[-1]) if prompts is not None else 0
     if world > 1:
@@ -402,7 +402,7 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
     M = microbatches or world
-    plan = plan_stages(cfg, world, kv_tokens=max_seq * batch * M)
+    plan = plan_stages(cfg, world, kv_tokens=max_seq * batch * M, head_split=world > 1)
     st = plan.stages[rank]
     need = prompt_len + warmup + steps + 1
     if need > max_seq:

@@ -77,8 +77,10 @@ def default_costs(cfg: LlamaConfig, elem_bytes: int = 2) -> tuple:
 def plan_stages(cfg: LlamaConfig, devices: Sequence[DeviceSpec] | int, *,
                 layer_costs: Optional[Sequence[float]] = None, embed_cost: Optional[float] = None,
                 head_cost: Optional[float] = None, kv_tokens: int = 0, elem_bytes: int = 2,
-                min_layers: int = 1) -> Plan:
-    """Exact min-max contiguous partition. ``devices`` is a list (chain order) or a count."""
+                min_layers: int = 1, head_split: bool = False) -> Plan:
+    """Exact min-max contiguous partition. ``devices`` is a list (chain order) or a count.
+    ``head_split``: the lm_head is shared by the last and the first stage (pipeline.py), so each
+    carries half of its cost and memory."""
     if isinstance(devices, int):
         devices = [DeviceSpec() for _ in range(devices)]
     n, L = len(devices), cfg.num_hidden_layers
@@ -97,20 +99,24 @@ def plan_stages(cfg: LlamaConfig, devices: Sequence[DeviceSpec] | int, *,
     for c in lc:
         pre.append(pre[-1] + c)
 
+    split = head_split and n > 1
+    hfrac_last = 0.5 if split else 1.0
+
     def stage_cost(k: int, a: int, b: int) -> float:
         t = pre[b] - pre[a]
         if k == 0:
-            t += ec
+            t += ec + (hc * 0.5 if split else 0.0)
         if k == n - 1:
-            t += hc
+            t += hc * hfrac_last
         return t * devices[k].speed
 
     def stage_mem(k: int, a: int, b: int) -> float:
         m = (b - a) * (lbytes + kv_per_layer)
         if k == 0:
-            m += emb_bytes
+            m += emb_bytes + (emb_bytes * 0.5 if split else 0.0)
         if k == n - 1:
-            m += head_bytes + cfg.hidden_size * elem_bytes
+            m += (emb_bytes * hfrac_last if not cfg.tie_word_embeddings or split else head_bytes) \
+                + cfg.hidden_size * elem_bytes
         return m
 
     def fits(k: int, a: int, b: int) -> bool:
