@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--json-out", default="")
     ap.add_argument("--trace", default="", help="write per-rank Chrome-trace timelines of the timed steps here")
+    ap.add_argument("--weight-dtype", default="bf16", choices=("bf16", "fp8"),
+                    help="fp8: OCP e4m3 projection/lm_head weights with per-row scales (W8A16, not the headline)")
     return ap.parse_args()
 
 
@@ -61,7 +63,8 @@ def main():
     from llm_sharding_amd.parallel.pipeline import run_decode_benchmark
     res = run_decode_benchmark(model=a.model, n_gpus=a.gpus, steps=a.steps, warmup=a.warmup,
                                batch=a.batch, prompt_len=a.prompt_len, max_seq=a.max_seq,
-                               microbatches=a.microbatches, seed=a.seed, use_graph=not a.no_graph)
+                               microbatches=a.microbatches, seed=a.seed, use_graph=not a.no_graph,
+                               weight_dtype=a.weight_dtype)
     if res is None:  # non-zero ranks
         return
     line = {
@@ -75,7 +78,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": (round(res["tok_s"] / BASELINE_TOK_S, 3) if BASELINE_TOK_S else None),
-        "dtype": "bf16",
+        "dtype": "bf16" if a.weight_dtype == "bf16" else "bf16 activations, fp8-e4m3 weights (W8A16)",
         "data": "synthetic prompts, random-init weights (Llama-2-7B architecture)",
         "config": {"model": res["model_name"], "global_batch": res["global_batch"],
                    "seq_len": a.prompt_len + a.warmup + a.steps,

@@ -54,6 +54,8 @@ def lib() -> ctypes.CDLL:
     vp, i, f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
     L.lsa_gemv.argtypes = [vp, i, vp, vp, i, i, i, i, f, i, ctypes.POINTER(EpiArgs), i, i, i, vp]
     L.lsa_gemv_coop.argtypes = [vp, i, vp, vp, i, i, i, i, f, i, ctypes.POINTER(EpiArgs), i, i, i, i, vp, vp, vp]
+    L.lsa_gemv_fp8.argtypes = [vp, i, vp, vp, vp, i, i, i, i, f, i, ctypes.POINTER(EpiArgs), i, i, i, vp]
+    L.lsa_dequant_fp8_packed.argtypes = [vp, vp, vp, i, i, vp]
     L.lsa_gemm.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(EpiArgs), i, i, vp, vp, vp]
     L.lsa_attn_decode.argtypes = [vp, i, vp, vp, vp, vp, vp, i, i, i, i, i, f, i, i, vp, vp, vp, i, vp]
     L.lsa_attn_prefill.argtypes = [vp, i, vp, vp, vp, i, i, i, i, i, f, i, vp, i, vp]
@@ -61,7 +63,7 @@ def lib() -> ctypes.CDLL:
     L.lsa_rmsnorm.argtypes = [vp, i, vp, i, i, f, vp, i, vp]
     L.lsa_argmax_finalize.argtypes = [vp, i, vp, vp, i, vp, i, i, vp, vp]
     L.lsa_pos_advance.argtypes = [vp, i, i, vp]
-    for name in ("lsa_gemv", "lsa_gemv_coop", "lsa_gemm", "lsa_attn_decode", "lsa_attn_prefill", "lsa_embed", "lsa_rmsnorm",
+    for name in ("lsa_gemv", "lsa_gemv_coop", "lsa_gemv_fp8", "lsa_dequant_fp8_packed", "lsa_gemm", "lsa_attn_decode", "lsa_attn_prefill", "lsa_embed", "lsa_rmsnorm",
                  "lsa_argmax_finalize", "lsa_pos_advance", "lsa_version"):
         getattr(L, name).restype = ctypes.c_int
     _lib = L
@@ -166,6 +168,38 @@ def gemv(x: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep
     rc = lib().lsa_gemv(_p(x), x.stride(0), _p(a_rows), _p(wp), M, N, K, int(norm), float(eps), epi,
                         ctypes.byref(ep), tn, nw, u, _stream())
     _check(rc, "lsa_gemv")
+
+
+def gemv_fp8(x: torch.Tensor, wq: torch.Tensor, wscale: torch.Tensor, M: int, N: int, K: int, epi: int,
+             ep: EpiArgs, norm: bool = False, eps: float = 1e-5, a_rows: Optional[torch.Tensor] = None,
+             cfg: Optional[tuple] = None) -> None:
+    """W8A16 decode projection (gemv_fp8.hip), M <= 64: ``wq`` = pack_b_fp8(q) (uint8),
+    ``wscale`` fp32 [N] per-row scale (the RMSNorm weight folded in before quantisation)."""
+    from .packing import FP8_CONFIGS, fp8_config, row_blocks
+    _req(1 <= M <= 64, f"gemv_fp8 supports 1..64 rows, got {M}")
+    _req(_is_bf16_cuda(x), "gemv_fp8: bf16 cuda activations")
+    _req(wq.is_cuda and wq.dtype == torch.uint8 and wq.numel() == N * K, "gemv_fp8: packed fp8 weights [N*K] uint8")
+    _req(wscale.is_cuda and wscale.dtype == torch.float32 and wscale.numel() >= N, "gemv_fp8: fp32 scales [N]")
+    _req(N % 16 == 0 and K % 64 == 0, "gemv_fp8: N % 16, K % 64")
+    _req(x.dim() == 2 and x.shape[1] >= K and x.stride(1) == 1, "gemv_fp8: x must be [rows, >=K] row-major")
+    if a_rows is None:
+        _req(x.shape[0] >= M, "gemv_fp8: x has fewer rows than M")
+    else:
+        _req(a_rows.dtype == torch.int32 and a_rows.is_cuda and a_rows.numel() >= M, "gemv_fp8: a_rows")
+    tn, nw, u2 = cfg if cfg is not None else fp8_config(N // 16, M, need_even=(epi == EPI_SWIGLU), k=K)
+    _req((tn, row_blocks(M), nw, u2) in FP8_CONFIGS, f"gemv_fp8: config {(tn, nw, u2)} not built for {M} rows")
+    rc = lib().lsa_gemv_fp8(_p(x), x.stride(0), _p(a_rows), _p(wq), _p(wscale), M, N, K, int(norm), float(eps), epi,
+                            ctypes.byref(ep), tn, nw, u2, _stream())
+    _check(rc, "lsa_gemv_fp8")
+
+
+def dequant_fp8_packed(wq: torch.Tensor, wscale: torch.Tensor, out: torch.Tensor, N: int, K: int) -> torch.Tensor:
+    """Packed fp8 (+ row scales) -> packed bf16 (pack_b layout) in ``out`` (>= N*K bf16)."""
+    _req(wq.is_cuda and wq.dtype == torch.uint8 and wq.numel() == N * K, "dequant_fp8: weights")
+    _req(wscale.dtype == torch.float32 and wscale.numel() >= N, "dequant_fp8: scales")
+    _req(_is_bf16_cuda(out) and out.numel() >= N * K, "dequant_fp8: out")
+    _check(lib().lsa_dequant_fp8_packed(_p(wq), _p(wscale), _p(out), N, K, _stream()), "lsa_dequant_fp8_packed")
+    return out.view(-1)[:N * K].view(N // 16, K // 32, 64, 8)
 
 
 def gemm_split(M: int, N: int, K: int, tn: int) -> int:

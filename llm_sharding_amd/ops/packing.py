@@ -70,6 +70,56 @@ def fold_norm(w: torch.Tensor, g: torch.Tensor) -> torch.Tensor:
 
 N_CU = 256  # MI355X compute units
 
+FP8 = getattr(torch, "float8_e4m3fn", None)  # OCP e4m3: the MI355X (gfx950) native fp8 encoding
+
+
+def quantize_fp8_rows(w: torch.Tensor) -> tuple:
+    """Per-output-row symmetric OCP e4m3: w ~= q * scale[:, None]. Returns (q uint8 [N, K], scale fp32 [N])."""
+    amax = w.float().abs().amax(dim=1).clamp(min=1e-12)
+    scale = amax / 448.0
+    q = (w.float() / scale[:, None]).clamp(-448.0, 448.0).to(FP8)
+    return q.view(torch.uint8), scale.float()
+
+
+def dequantize_fp8_rows(q: torch.Tensor, scale: torch.Tensor) -> torch.Tensor:
+    return q.view(FP8).float() * scale.float()[:, None]
+
+
+def pack_b_fp8(q: torch.Tensor) -> torch.Tensor:
+    """fp8 bytes [N, K] (K % 64 == 0) -> Wq[nt][kt/2][lane][16]: per lane and 16-B load, the
+    8 elements of MFMA B fragment 2*kt2 (bytes 0-7) and of fragment 2*kt2+1 (bytes 8-15), each
+    in pack_b's element order."""
+    N, K = q.shape
+    if N % 16 or K % 64:
+        raise ValueError(f"pack_b_fp8 needs N%16==0 and K%64==0, got {tuple(q.shape)}")
+    p = q.contiguous().view(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).reshape(N // 16, K // 32, 64, 8)
+    return p.view(N // 16, K // 64, 2, 64, 8).permute(0, 1, 3, 2, 4).reshape(N // 16, K // 64, 64, 16).contiguous()
+
+
+# (tn, mb, nw, u2) instantiated in csrc/kernels/gemv_fp8.hip (LSA_FP8_CONFIGS) - keep in sync.
+FP8_CONFIGS = [(1, 1, 4, 2), (1, 1, 8, 2), (1, 1, 4, 4), (2, 1, 4, 2), (2, 1, 8, 2), (4, 1, 4, 1),
+               (1, 2, 4, 2), (1, 2, 8, 2), (2, 2, 4, 1), (2, 2, 8, 1), (1, 4, 4, 1), (1, 4, 8, 1), (2, 4, 4, 1),
+               (2, 4, 8, 1)]
+
+
+def fp8_config(n_tiles: int, rows: int, need_even: bool = False, k: int = 4096) -> tuple:
+    """(tn, nw, u2) for the fp8 GEMV: the tuning table entry ("fp8" algo) if measured, else the
+    candidate giving >= 256 workgroups with the most weight bytes in flight per wave."""
+    mb = row_blocks(rows)
+    t = _tuned().get((n_tiles * 16, k, mb, bool(need_even)) + ("fp8",))
+    cands = [(tn, nw, u2) for (tn, b, nw, u2) in FP8_CONFIGS
+             if b == mb and n_tiles % tn == 0 and (not need_even or tn % 2 == 0) and (k // 32) % (2 * u2) == 0]
+    if t is not None and t in cands:
+        return t
+    if not cands:
+        raise ValueError(f"no fp8 GEMV config for {n_tiles} tiles, K={k}, rows={rows}")
+    def cost(c):
+        tn, nw, u2 = c
+        g = n_tiles // tn
+        eff = g / (N_CU * -(-g // N_CU))
+        return (1.0 + 0.4 * rows / (16.0 * tn)) / eff - 0.01 * (nw * u2 / 16.0)
+    return min(cands, key=cost)
+
 
 # (tn, mb, nw, u) instantiated in csrc/kernels/gemv.hip (LSA_GEMV_CONFIGS) - keep in sync.
 GEMV_CONFIGS = [
@@ -149,7 +199,10 @@ def _tuned() -> dict:
         if os.path.exists(TUNING_FILE):
             with open(TUNING_FILE) as f:
                 for e in json.load(f).get("entries", []):
-                    _TUNED[(e["N"], e["K"], e["mb"], bool(e["even"]))] = (e.get("algo", "gemv"), tuple(e["cfg"]))
+                    if e.get("algo") == "fp8":
+                        _TUNED[(e["N"], e["K"], e["mb"], bool(e["even"]), "fp8")] = tuple(e["cfg"])
+                    else:
+                        _TUNED[(e["N"], e["K"], e["mb"], bool(e["even"]))] = (e.get("algo", "gemv"), tuple(e["cfg"]))
     return _TUNED
 
 

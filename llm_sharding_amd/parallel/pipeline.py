@@ -87,7 +87,7 @@ class PipelineStage:
     def __init__(self, cfg, rank: int, world: int, start: int, end: int, device, batch: int,
                  microbatches: int, max_seq: int, source, use_graph: bool = True,
                  max_prefill_rows: int = 2048, dtype=torch.bfloat16, p2p=None,
-                 split_head: Optional[bool] = None):
+                 split_head: Optional[bool] = None, weight_dtype: str = "bf16"):
         self.cfg, self.rank, self.world = cfg, rank, world
         self.p2p = p2p if p2p is not None else DistP2P()
         self.first, self.last = rank == 0, rank == world - 1
@@ -111,7 +111,8 @@ class PipelineStage:
         self.eng = StageEngine(cfg, start, end, device, self.dtype, has_embed=self.first,
                                has_head=self.last or (self.split and self.first), source=source,
                                max_slots=batch * microbatches, max_seq=max_seq,
-                               max_prefill_rows=max(max_prefill_rows, batch), head_cols=head_cols)
+                               max_prefill_rows=max(max_prefill_rows, batch), head_cols=head_cols,
+                               weight_dtype=weight_dtype)
         H = cfg.hidden_size
         self.h_out = [torch.zeros((batch, H), dtype=self.dtype, device=self.device) for _ in range(microbatches)]
         self.tok_out = [torch.zeros(batch, dtype=torch.int32, device=self.device) for _ in range(microbatches)]
@@ -388,7 +389,7 @@ def drive_local_pipeline(cfg, source, prompts: torch.Tensor, n_new: int, n_stage
 def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int = 64, warmup: int = 8,
                          batch: int = 16, prompt_len: int = 128, max_seq: int = 1024,
                          microbatches: int = 0, seed: int = 0, use_graph: bool = True,
-                         verbose: bool = True) -> Optional[dict]:
+                         verbose: bool = True, weight_dtype: str = "bf16") -> Optional[dict]:
     cfg = get_preset(model)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -412,7 +413,7 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
     t0 = time.perf_counter()
     stage = PipelineStage(cfg, rank, world, st.start, st.end, dev, batch, M, max_seq,
                           RandomSource(cfg, seed), use_graph=use_graph,
-                          max_prefill_rows=batch * prompt_len)
+                          max_prefill_rows=batch * prompt_len, weight_dtype=weight_dtype)
     torch.cuda.synchronize()
     load_s = time.perf_counter() - t0
     if dist:

@@ -100,6 +100,11 @@ class LayerWeights:
     ln_in: torch.Tensor
     ln_post: torch.Tensor
     raw: Optional[dict] = None  # CPU path keeps the reference state dict
+    # fp8 weights (weight_dtype="fp8"): per-output-row fp32 scales of the packed e4m3 tensors
+    qkv_s: Optional[torch.Tensor] = None
+    o_s: Optional[torch.Tensor] = None
+    gate_up_s: Optional[torch.Tensor] = None
+    down_s: Optional[torch.Tensor] = None
 
 
 def _is_gpu(device: torch.device) -> bool:
@@ -129,7 +134,7 @@ class StageEngine:
                  dtype=torch.bfloat16, *, has_embed: bool = False, has_head: bool = False,
                  source: Optional[WeightSource] = None, max_slots: int = 1, max_seq: int = 2048,
                  max_prefill_rows: int = 2048, causal: bool = True, load: bool = True,
-                 verbose: bool = False, head_cols: Optional[tuple] = None):
+                 verbose: bool = False, head_cols: Optional[tuple] = None, weight_dtype: str = "bf16"):
         if not (0 <= start < end <= cfg.num_hidden_layers):
             raise ValueError(f"[ERROR] invalid layer range [{start}, {end})")
         self.cfg = cfg
@@ -141,6 +146,13 @@ class StageEngine:
             raise ValueError("the HIP path computes in bfloat16 (pass dtype=torch.bfloat16)")
         self.dtype = dtype
         self.has_embed, self.has_head = has_embed, has_head
+        if weight_dtype not in ("bf16", "fp8"):
+            raise ValueError(f"weight_dtype must be bf16 or fp8, got {weight_dtype!r}")
+        # fp8: projection + lm_head weights kept as OCP e4m3 with per-row scales (W8A16); decode
+        # batches <= 64 stream them natively (gemv_fp8.hip), larger row counts dequantise one
+        # projection at a time into a scratch buffer for the bf16 coop / GEMM kernels
+        self.fp8 = weight_dtype == "fp8" and self.gpu
+        self.lm_head_s = None
         # vocab rows [v0, v1) of the lm_head held here (a pipeline may split the head between its
         # last and first stage so that neither carries the whole 0.4-layer lm_head)
         self.head_v0, self.head_v1 = head_cols if head_cols is not None else (0, cfg.vocab_size)
@@ -190,7 +202,11 @@ class StageEngine:
             if (self.head_v0, self.head_v1) != (0, self.cfg.vocab_size):
                 lm = lm[self.head_v0:self.head_v1]
             # GPU: final RMSNorm weight folded into the packed lm_head (fused norm+GEMV+argmax)
-            self.lm_head = packing.pack_b(packing.fold_norm(lm, self.final_norm)) if self.gpu else lm.contiguous()
+            if self.fp8:
+                q, self.lm_head_s = packing.quantize_fp8_rows(packing.fold_norm(lm, self.final_norm))
+                self.lm_head = packing.pack_b_fp8(q)
+            else:
+                self.lm_head = packing.pack_b(packing.fold_norm(lm, self.final_norm)) if self.gpu else lm.contiguous()
             del lm
         self._alloc_runtime()
 
@@ -200,6 +216,16 @@ class StageEngine:
                                lw["self_attn.v_proj.weight"], cfg.num_attention_heads,
                                cfg.num_key_value_heads, cfg.head_dim)
         gu = packing.fuse_gate_up(lw["mlp.gate_proj.weight"], lw["mlp.up_proj.weight"])
+        if self.gpu and self.fp8:
+            ln_in, ln_post = lw["input_layernorm.weight"], lw["post_attention_layernorm.weight"]
+            parts = []
+            for wt in (packing.fold_norm(qkv, ln_in), lw["self_attn.o_proj.weight"], packing.fold_norm(gu, ln_post),
+                       lw["mlp.down_proj.weight"]):
+                q, sc = packing.quantize_fp8_rows(wt)
+                parts.append((packing.pack_b_fp8(q), sc))
+            return LayerWeights(parts[0][0], parts[1][0], parts[2][0], parts[3][0], ln_in.contiguous(),
+                                ln_post.contiguous(), qkv_s=parts[0][1], o_s=parts[1][1], gate_up_s=parts[2][1],
+                                down_s=parts[3][1])
         if self.gpu:
             # RMSNorm weights are folded into the projections that consume the normed input
             ln_in, ln_post = lw["input_layernorm.weight"], lw["post_attention_layernorm.weight"]
@@ -243,11 +269,15 @@ class StageEngine:
             floats, groups = packing.coop_workspace_need(shapes, self.DECODE_MAX_ROWS, even_n=((2 * I, H),))
             # the prefill GEMM's split-K slabs (small-M grids only) share it: <= 64 MB
             self.coop_ws = hip.CoopWorkspace(dev, slab_floats=max(floats, 1 << 24), groups=max(groups, 4096))
+            self.w_scratch = None
+            if self.fp8:  # one projection's bf16 weights, for the >64-row paths
+                self.w_scratch = torch.empty(max(n * k for n, k in shapes), dtype=torch.bfloat16, device=dev)
 
     def memory_bytes(self) -> int:
         n = 0
         for lw in self.layers:
-            for t in (lw.qkv, lw.o, lw.gate_up, lw.down, lw.ln_in, lw.ln_post):
+            for t in (lw.qkv, lw.o, lw.gate_up, lw.down, lw.ln_in, lw.ln_post, lw.qkv_s, lw.o_s, lw.gate_up_s,
+                      lw.down_s):
                 if t is not None:
                     n += t.numel() * t.element_size()
             if lw.raw is not None:
@@ -340,12 +370,23 @@ class StageEngine:
         n = idx.numel()
         if keys is None:
             keys = torch.zeros(n, dtype=torch.int64, device=self.device)
-        for c0 in range(0, n, self.DECODE_MAX_ROWS):
-            c = min(self.DECODE_MAX_ROWS, n - c0)
-            ep = hip.make_epi(keys=keys[c0:c0 + c], col_offset=self.head_v0)
-            hip.gemv(h, self.lm_head, c, self.head_v1 - self.head_v0, self.cfg.hidden_size, hip.EPI_ARGMAX, ep,
-                     ws=self.coop_ws, norm=True, eps=self.cfg.rms_norm_eps, a_rows=idx[c0:c0 + c])
+        step = 64 if self.fp8 else self.DECODE_MAX_ROWS
+        for c0 in range(0, n, step):
+            c = min(step, n - c0)
+            self.head_gemv(h, c, keys[c0:c0 + c], a_rows=idx[c0:c0 + c])
         return keys
+
+    def head_gemv(self, h: torch.Tensor, rows: int, keys: torch.Tensor, a_rows=None) -> None:
+        """Fused final RMSNorm + lm_head slice + argmax keys (atomicMax into ``keys``)."""
+        from ..ops import hip
+        ep = hip.make_epi(keys=keys, col_offset=self.head_v0)
+        N, H, eps = self.head_v1 - self.head_v0, self.cfg.hidden_size, self.cfg.rms_norm_eps
+        if self.lm_head_s is not None:
+            hip.gemv_fp8(h, self.lm_head.view(-1), self.lm_head_s, rows, N, H, hip.EPI_ARGMAX, ep, norm=True, eps=eps,
+                         a_rows=a_rows)
+        else:
+            hip.gemv(h, self.lm_head, rows, N, H, hip.EPI_ARGMAX, ep, ws=self.coop_ws, norm=True, eps=eps,
+                     a_rows=a_rows)
 
     def finalize_keys(self, keys: torch.Tensor) -> torch.Tensor:
         """argmax keys -> token ids (int32, device); resets ``keys``."""
@@ -398,15 +439,29 @@ class StageEngine:
             nsplit = self._attn_nsplit(rows, kv_max)
         q, attn_o, act, xn = self.buf_q[:rows], self.buf_attn[:rows], self.buf_act[:rows], self.buf_xn[:rows]
         ws = self.coop_ws
+        native_fp8 = self.fp8 and rows <= 64
+
+        def wbf(w, s, N, K):  # packed bf16 weights (fp8 -> scratch for the >64-row kernels)
+            return w if s is None else hip.dequant_fp8_packed(w.view(-1), s, self.w_scratch, N, K)
+
+        def dec(x, w, s, N, K, epi, ep, norm=False):
+            if native_fp8:
+                hip.gemv_fp8(x, w.view(-1), s, rows, N, K, epi, ep, norm=norm, eps=eps)
+            else:
+                hip.gemv(x, wbf(w, s, N, K), rows, N, K, epi, ep, norm=norm, eps=eps, ws=ws)
+
+        def pre(x, w, s, N, K, epi, ep):
+            hip.gemm(x, wbf(w, s, N, K), rows, N, K, epi, ep, ws=ws)
+
         for li, lw in enumerate(self.layers):
             kc, vc = self.k_cache[li], self.v_cache[li]
             ep_qkv = hip.make_epi(out=q, k_cache=kc, v_cache=vc, slot=slot, pos=pos, cos=self.cos, sin=self.sin,
                                   ldo=q.stride(0), n_heads=nh, n_kv=nkv, head_dim=hd, t_max=self.max_seq)
             if decode:
-                hip.gemv(hbuf, lw.qkv, rows, cfg.qkv_size, H, hip.EPI_QKV, ep_qkv, norm=True, eps=eps, ws=ws)
+                dec(hbuf, lw.qkv, lw.qkv_s, cfg.qkv_size, H, hip.EPI_QKV, ep_qkv, norm=True)
             else:
                 hip.rmsnorm(hbuf, None, xn, rows, eps, H)
-                hip.gemm(xn, lw.qkv, rows, cfg.qkv_size, H, hip.EPI_QKV, ep_qkv, ws=ws)
+                pre(xn, lw.qkv, lw.qkv_s, cfg.qkv_size, H, hip.EPI_QKV, ep_qkv)
             if tiles is not None:
                 hip.attn_prefill(q, kc, vc, tiles[1], nh, nkv, hd, attn_o, causal=kv_len is None, tiles_host=tiles[0])
             else:
@@ -415,14 +470,14 @@ class StageEngine:
             ep_o = hip.make_epi(out=hbuf, resid=hbuf, ldo=hbuf.stride(0), ldr=hbuf.stride(0))
             ep_gu = hip.make_epi(out=act, ldo=act.stride(0))
             if decode:
-                hip.gemv(attn_o, lw.o, rows, H, cfg.q_size, hip.EPI_RESID, ep_o, ws=ws)
-                hip.gemv(hbuf, lw.gate_up, rows, 2 * I, H, hip.EPI_SWIGLU, ep_gu, norm=True, eps=eps, ws=ws)
-                hip.gemv(act, lw.down, rows, H, I, hip.EPI_RESID, ep_o, ws=ws)
+                dec(attn_o, lw.o, lw.o_s, H, cfg.q_size, hip.EPI_RESID, ep_o)
+                dec(hbuf, lw.gate_up, lw.gate_up_s, 2 * I, H, hip.EPI_SWIGLU, ep_gu, norm=True)
+                dec(act, lw.down, lw.down_s, H, I, hip.EPI_RESID, ep_o)
             else:
-                hip.gemm(attn_o, lw.o, rows, H, cfg.q_size, hip.EPI_RESID, ep_o, ws=ws)
+                pre(attn_o, lw.o, lw.o_s, H, cfg.q_size, hip.EPI_RESID, ep_o)
                 hip.rmsnorm(hbuf, None, xn, rows, eps, H)
-                hip.gemm(xn, lw.gate_up, rows, 2 * I, H, hip.EPI_SWIGLU, ep_gu, ws=ws)
-                hip.gemm(act, lw.down, rows, H, I, hip.EPI_RESID, ep_o, ws=ws)
+                pre(xn, lw.gate_up, lw.gate_up_s, 2 * I, H, hip.EPI_SWIGLU, ep_gu)
+                pre(act, lw.down, lw.down_s, H, I, hip.EPI_RESID, ep_o)
         return hbuf
 
     # ------------------------------------------------------------------------- torch path (CPU)
@@ -540,9 +595,9 @@ class DecodeGraph:
         h = eng.buf_h[:rows]
         if self.split_head and self.mode == "first":
             self.keys.copy_(self.keys_in)
-            ep = hip.make_epi(keys=self.keys, col_offset=eng.head_v0)
-            hip.gemv(self.h_fin, eng.lm_head, rows, eng.head_v1 - eng.head_v0, eng.cfg.hidden_size, hip.EPI_ARGMAX,
-                     ep, ws=eng.coop_ws, norm=True, eps=eng.cfg.rms_norm_eps)
+            for c0 in range(0, rows, 64 if eng.fp8 else rows):
+                c = min(64 if eng.fp8 else rows, rows - c0)
+                eng.head_gemv(self.h_fin[c0:c0 + c], c, self.keys[c0:c0 + c])
             hip.argmax_finalize(self.keys, rows, self.tokens, None, 1, self.history,
                                 self.step_ctr if self.history is not None else None)
         if self.mode in ("full", "first"):
@@ -552,14 +607,17 @@ class DecodeGraph:
         eng._forward_hip(h, self.slot, self.pos, None, rows, nsplit=eng.decode_nsplit(rows))
         if self.split_head and self.mode == "last":
             self.keys.zero_()
-            ep = hip.make_epi(keys=self.keys, col_offset=eng.head_v0)
-            hip.gemv(h, eng.lm_head, rows, eng.head_v1 - eng.head_v0, eng.cfg.hidden_size, hip.EPI_ARGMAX, ep,
-                     ws=eng.coop_ws, norm=True, eps=eng.cfg.rms_norm_eps)
+            for c0 in range(0, rows, 64 if eng.fp8 else rows):
+                c = min(64 if eng.fp8 else rows, rows - c0)
+                eng.head_gemv(h[c0:c0 + c], c, self.keys[c0:c0 + c])
             hip.pos_advance(self.pos, rows, 1)
         elif self.mode in ("full", "last"):
-            ep = hip.make_epi(keys=self.keys)
-            hip.gemv(h, eng.lm_head, rows, eng.cfg.vocab_size, eng.cfg.hidden_size, hip.EPI_ARGMAX, ep, ws=eng.coop_ws,
-                     norm=True, eps=eng.cfg.rms_norm_eps)
+            if eng.fp8 and rows > 64:
+                for c0 in range(0, rows, 64):
+                    c = min(64, rows - c0)
+                    eng.head_gemv(h[c0:c0 + c], c, self.keys[c0:c0 + c])
+            else:
+                eng.head_gemv(h, rows, self.keys)
             hip.argmax_finalize(self.keys, rows, self.tokens, self.pos, 1, self.history,
                                 self.step_ctr if self.history is not None else None)
         else:

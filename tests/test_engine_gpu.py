@@ -271,3 +271,42 @@ def test_pipeline_server_graph_mode_on_gpu():
         agree += sum(int(a == b) for a, b in zip(o, want))
         tot += len(want)
     assert agree / tot >= 0.8
+
+
+def test_fp8_weights_engine():
+    """weight_dtype="fp8" (W8A16): prefill (dequantised scratch + bf16 GEMM), decode rows <= 64
+    (native fp8 GEMV) and > 64 (scratch + coop) against the bf16 engine on the same weights."""
+    cfg = _mid_cfg()
+    src = CpuGenSource(cfg, 3)
+    kw = dict(has_embed=True, has_head=True, source=src, max_slots=80, max_seq=256, max_prefill_rows=256)
+    e16 = StageEngine(cfg, 0, cfg.num_hidden_layers, DEV, torch.bfloat16, **kw)
+    e8 = StageEngine(cfg, 0, cfg.num_hidden_layers, DEV, torch.bfloat16, weight_dtype="fp8", **kw)
+    assert e8.memory_bytes() < 0.8 * e16.memory_bytes()
+    g = torch.Generator().manual_seed(1)
+    ids = torch.randint(3, cfg.vocab_size, (100,), generator=g)
+    outs = []
+    for e in (e16, e8):
+        sl, po = e.prefill_rows([0], [100])
+        outs.append(e.forward(e.embed(ids.to(DEV)), sl, po).clone())
+        e.advance([0], [100])
+    assert rel_err(outs[1], outs[0]) < 0.15  # e4m3 per-channel rounding over 2 layers
+    for rows in (5, 80):
+        toks = torch.randint(3, cfg.vocab_size, (rows,), generator=g)
+        hs, heads = [], []
+        for e in (e16, e8):
+            slots = list(range(rows))
+            for s_ in slots[1:]:
+                e.seq_len[s_] = 0
+            sl, po = e.prefill_rows(slots, [1] * rows)
+            h = e.forward(e.embed(toks.to(DEV)), sl, po)
+            e.advance(slots, [1] * rows)
+            hs.append(h.clone())
+            heads.append(e.head(h).cpu())
+        assert rel_err(hs[1], hs[0]) < 0.15, rows
+        assert (heads[0] == heads[1]).float().mean() >= 0.5, rows
+    # fp8 decode graph (native fp8 GEMVs + fp8 lm_head) replays and produces valid ids
+    dg = DecodeGraph(e8, 8, "full", slots=list(range(8)), history_len=3).capture()
+    for _ in range(3):
+        dg.replay()
+    torch.cuda.synchronize()
+    assert bool(((dg.history >= 0) & (dg.history < cfg.vocab_size)).all())

@@ -388,3 +388,56 @@ def test_attention_prefill_flash(nh, nkv, hd, causal):
     # per-row check too: no row may be garbage even if the aggregate is fine
     per_row = ((out.float() - ref).norm(dim=1) / ref.norm(dim=1))
     assert float(per_row.max()) < 3e-2
+
+
+@pytest.mark.parametrize("cfg", packing.FP8_CONFIGS)
+def test_gemv_fp8_every_config(cfg):
+    """W8A16 GEMV (OCP e4m3 weights, per-row scales, bf16 MFMA after in-register conversion)
+    against fp32 math on the dequantised weights, with the fused RMSNorm + residual epilogue."""
+    h = hip()
+    tn, mb, nw, u2 = cfg
+    M = {1: 7, 2: 29, 4: 50}[mb]
+    N = 16 * tn * 6
+    for K in (4096, 64 * 2 * u2 * 3):
+        if (K // 32) % (2 * u2):
+            continue
+        x = _rnd(M, K)
+        g = (1 + 0.1 * torch.randn(K, device=DEV)).to(torch.bfloat16)
+        w = _rnd(N, K, scale=0.03)
+        q, sc = packing.quantize_fp8_rows(packing.fold_norm(w, g))
+        wd = packing.dequantize_fp8_rows(q, sc)  # exactly what the kernel multiplies by
+        resid = _rnd(M, N)
+        out = resid.clone()
+        xn = x.float() * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + 1e-5)
+        ref = resid.float() + xn @ wd.T
+        h.gemv_fp8(x, packing.pack_b_fp8(q).view(-1), sc, M, N, K, h.EPI_RESID,
+                   h.make_epi(out=out, resid=out, ldo=N, ldr=N), norm=True, cfg=(tn, nw, u2))
+        assert rel_err(out, ref) < 8e-3, (cfg, K)
+
+
+def test_gemv_fp8_swiglu_argmax_and_dequant():
+    h = hip()
+    M, I, H, V = 5, 512, 1024, 2048
+    x = _rnd(M, H)
+    wg, wu = _rnd(I, H, scale=0.05), _rnd(I, H, scale=0.05)
+    q, sc = packing.quantize_fp8_rows(packing.fuse_gate_up(wg, wu))
+    wd = packing.dequantize_fp8_rows(q, sc)
+    out = torch.zeros(M, I, dtype=torch.bfloat16, device=DEV)
+    h.gemv_fp8(x, packing.pack_b_fp8(q).view(-1), sc, M, 2 * I, H, h.EPI_SWIGLU, h.make_epi(out=out, ldo=I))
+    gu = (x.float() @ wd.T).view(M, I // 16, 2, 16)
+    ref = (F.silu(gu[:, :, 0]) * gu[:, :, 1]).reshape(M, I)
+    assert rel_err(out, ref) < 1e-2
+    # argmax over a vocab with column offset
+    lm = _rnd(V, H, scale=0.02)
+    ql, sl = packing.quantize_fp8_rows(lm)
+    keys = torch.zeros(M, dtype=torch.int64, device=DEV)
+    h.gemv_fp8(x, packing.pack_b_fp8(ql).view(-1), sl, M, V, H, h.EPI_ARGMAX, h.make_epi(keys=keys))
+    tok = torch.zeros(M, dtype=torch.int32, device=DEV)
+    h.argmax_finalize(keys, M, tok)
+    logits = x.float() @ packing.dequantize_fp8_rows(ql, sl).T
+    chosen = logits.gather(1, tok.long()[:, None])[:, 0]
+    assert torch.all(logits.max(-1).values - chosen < 2e-2 * logits.abs().max())
+    # scratch dequantisation reproduces pack_b of the dequantised weights (bf16-rounded)
+    scratch = torch.empty(V * H, dtype=torch.bfloat16, device=DEV)
+    wp = h.dequant_fp8_packed(packing.pack_b_fp8(ql).view(-1), sl, scratch, V, H)
+    assert torch.equal(wp, packing.pack_b(packing.dequantize_fp8_rows(ql, sl).to(torch.bfloat16)))
