@@ -30,10 +30,21 @@ LSA_DEVICE int a_off(int row, int c16) {
   return row * (KC * 2) + ((c16 ^ sw) << 4);
 }
 
-template <int MB, int TNW, int NW, int KF, int EPI, bool NORM>
+// 8 OCP fp8 e4m3 (two dwords) -> 8 bf16 (v_cvt_scalef32_pk_bf16_fp8, gfx950)
+LSA_DEVICE u32x4_t fp8x8_to_bf16(unsigned lo, unsigned hi) {
+  u32x4_t r;
+  r[0] = __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(lo, 1.0f, false));
+  r[1] = __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(lo, 1.0f, true));
+  r[2] = __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(hi, 1.0f, false));
+  r[3] = __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(hi, 1.0f, true));
+  return r;
+}
+
+template <int MB, int TNW, int NW, int KF, int EPI, bool NORM, bool FP8>
 __global__ __launch_bounds__(NW * 64) void gemv_coop_kernel(
     const bf16_raw* __restrict__ x, int ldx, const int* __restrict__ a_rows, const bf16_raw* __restrict__ wp,
-    int M, int N, int K, int SK, float eps, EpiArgs ep, float* __restrict__ slab, unsigned* __restrict__ counters) {
+    int M, int N, int K, int SK, float eps, EpiArgs ep, float* __restrict__ slab, unsigned* __restrict__ counters,
+    const float* __restrict__ wscale) {
   constexpr int NTHR = NW * 64;
   constexpr int KC = 32 * KF;                   // k per chunk (KF MFMA k-fragments)
   constexpr int C16 = KC / 8;                   // 16-B pieces per A row
@@ -104,13 +115,22 @@ __global__ __launch_bounds__(NW * 64) void gemv_coop_kernel(
       *reinterpret_cast<u32x4_t*>(smem + buf * ABUF + a_off<KC>(arow + i * RSTEP, ac16)) = a.v[i];
     }
   };
-  auto load_b = [&](int c, u32x4_t (&b)[KF][TNW]) {
+  // B fragments: bf16 -> one 16-B load per k-fragment; FP8 (W8A16, packed as in gemv_fp8.hip)
+  // -> one 16-B load per PAIR of k-fragments, converted to bf16 in registers right before the
+  // MFMAs (the per-row scale is applied in fp32 in the epilogue)
+  constexpr int BL = FP8 ? KF / 2 : KF;
+  auto load_b = [&](int c, u32x4_t (&b)[BL][TNW]) {
 #pragma unroll
-    for (int kf = 0; kf < KF; ++kf)
+    for (int p = 0; p < BL; ++p)
 #pragma unroll
-      for (int t = 0; t < TNW; ++t)
-        b[kf][t] = __builtin_amdgcn_raw_buffer_load_b128(
-            wr, lane16, (((nt0 + t) * KT + kt0 + c * KF + kf) * 512) * 2, 2);
+      for (int t = 0; t < TNW; ++t) {
+        if constexpr (FP8)
+          b[p][t] = __builtin_amdgcn_raw_buffer_load_b128(
+              wr, lane16, ((nt0 + t) * (KT >> 1) + ((kt0 + c * KF) >> 1) + p) * 1024, 2);
+        else
+          b[p][t] = __builtin_amdgcn_raw_buffer_load_b128(
+              wr, lane16, (((nt0 + t) * KT + kt0 + c * KF + p) * 512) * 2, 2);
+      }
   };
 
   f32x4_t acc[MB][TNW];
@@ -119,17 +139,27 @@ __global__ __launch_bounds__(NW * 64) void gemv_coop_kernel(
 #pragma unroll
     for (int t = 0; t < TNW; ++t) acc[rb][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  auto compute = [&](int buf, u32x4_t (&b)[KF][TNW]) {
+  auto compute = [&](int buf, u32x4_t (&b)[BL][TNW]) {
     const unsigned char* base = smem + buf * ABUF;
 #pragma unroll
-    for (int kf = 0; kf < KF; ++kf)
+    for (int kf = 0; kf < KF; ++kf) {
+      u32x4_t bk[TNW];
+#pragma unroll
+      for (int t = 0; t < TNW; ++t) {
+        if constexpr (FP8)
+          bk[t] = (kf & 1) ? fp8x8_to_bf16(b[kf >> 1][t][2], b[kf >> 1][t][3])
+                           : fp8x8_to_bf16(b[kf >> 1][t][0], b[kf >> 1][t][1]);
+        else
+          bk[t] = b[kf][t];
+      }
 #pragma unroll
       for (int rb = 0; rb < MB; ++rb) {
         const int row = rb * 16 + (lane & 15);
         const u32x4_t a = *reinterpret_cast<const u32x4_t*>(base + a_off<KC>(row, kf * 4 + (lane >> 4)));
 #pragma unroll
-        for (int t = 0; t < TNW; ++t) acc[rb][t] = mfma16(a, b[kf][t], acc[rb][t]);
+        for (int t = 0; t < TNW; ++t) acc[rb][t] = mfma16(a, bk[t], acc[rb][t]);
       }
+    }
   };
 
   {
@@ -139,7 +169,7 @@ __global__ __launch_bounds__(NW * 64) void gemv_coop_kernel(
     // issued before B(c+1) - otherwise waiting for A would drain the B prefetch too. Loads
     // are unconditional (tail chunk indices clamped, duplicates hit L2) so every s_waitcnt
     // is a static count, never vmcnt(0).
-    u32x4_t bX[KF][TNW], bY[KF][TNW], bZ[KF][TNW];
+    u32x4_t bX[BL][TNW], bY[BL][TNW], bZ[BL][TNW];
     AV aX, aY, aZ;
     const int last = nchunk - 1;
     auto clampc = [&](int c) { return c < last ? c : last; };
@@ -151,7 +181,7 @@ __global__ __launch_bounds__(NW * 64) void gemv_coop_kernel(
     __syncthreads();
     // step c: prefetch chunk c+2 into (a2, b2), compute chunk c from (LDS c&1, bc), then
     // publish A(c+1) from a1 into LDS.
-    auto step = [&](int c, u32x4_t (&bc)[KF][TNW], u32x4_t (&b2)[KF][TNW], AV& a1, AV& a2) {
+    auto step = [&](int c, u32x4_t (&bc)[BL][TNW], u32x4_t (&b2)[BL][TNW], AV& a1, AV& a2) {
       a2 = load_a(clampc(c + 2));
       load_b(clampc(c + 2), b2);
       __builtin_amdgcn_sched_barrier(0);  // keep the prefetches ahead of this chunk's MFMAs
@@ -269,12 +299,14 @@ __global__ __launch_bounds__(NW * 64) void gemv_coop_kernel(
 
   auto rstd = [&](int mm) -> float { return NORM ? rsqrtf(s_ss[mm] / (float)K + eps) : 1.f; };
   const int ntg0 = g * TG;
+  auto wsc = [&](int col) -> float { return FP8 ? wscale[col] : 1.f; };
   if (EPI == EPI_SWIGLU) {
     for (int e = tid; e < (TG / 2) * MR * 16; e += NTHR) {
       const int tp = e / (MR * 16), mm = (e >> 4) % MR, n = e & 15;
       if (mm >= M) continue;
       const float r = rstd(mm);
-      const float gg = red[((2 * tp) * MR + mm) * 16 + n] * r, uu = red[((2 * tp + 1) * MR + mm) * 16 + n] * r;
+      const float gg = red[((2 * tp) * MR + mm) * 16 + n] * r * wsc((ntg0 + 2 * tp) * 16 + n);
+      const float uu = red[((2 * tp + 1) * MR + mm) * 16 + n] * r * wsc((ntg0 + 2 * tp + 1) * 16 + n);
       ep.out[(size_t)mm * ep.ldo + (ntg0 / 2 + tp) * 16 + n] = f2bf(silu(gg) * uu);
     }
   } else {
@@ -282,14 +314,14 @@ __global__ __launch_bounds__(NW * 64) void gemv_coop_kernel(
       const int t = e / (MR * 16), mm = (e >> 4) % MR, n = e & 15;
       if (mm >= M) continue;
       const float r = rstd(mm);
-      const float v = red[(t * MR + mm) * 16 + n] * r;
       const int col = (ntg0 + t) * 16 + n;
+      const float v = red[(t * MR + mm) * 16 + n] * r * wsc(col);
       if (EPI == EPI_STORE) {
         ep.out[(size_t)mm * ep.ldo + col] = f2bf(v);
       } else if (EPI == EPI_RESID) {
         ep.out[(size_t)mm * ep.ldo + col] = f2bf(bf2f(ep.resid[(size_t)mm * ep.ldr + col]) + v);
       } else if (EPI == EPI_QKV) {
-        epi_qkv_store(ep, mm, col, v, red[(t * MR + mm) * 16 + (n ^ 8)] * r);
+        epi_qkv_store(ep, mm, col, v, red[(t * MR + mm) * 16 + (n ^ 8)] * r * wsc(col ^ 8));
       } else if (EPI == EPI_ARGMAX) {
         atomicMax(&s_key[mm], argmax_key(v, (unsigned)(col + ep.col_offset)));
       }
@@ -301,15 +333,15 @@ __global__ __launch_bounds__(NW * 64) void gemv_coop_kernel(
   }
 }
 
-template <int MB, int TNW, int NW, int KF, int EPI>
+template <int MB, int TNW, int NW, int KF, int EPI, bool FP8>
 int launch(bool norm, const bf16_raw* x, int ldx, const int* a_rows, const bf16_raw* wp, int M, int N, int K, int SK, float eps,
-           const EpiArgs& ep, float* slab, unsigned* cnt, hipStream_t s) {
+           const EpiArgs& ep, float* slab, unsigned* cnt, const float* wscale, hipStream_t s) {
   const int G = N / 16 / (NW * TNW);
   dim3 grid(G * SK), block(NW * 64);
   if (norm)
-    gemv_coop_kernel<MB, TNW, NW, KF, EPI, true><<<grid, block, 0, s>>>(x, ldx, a_rows, wp, M, N, K, SK, eps, ep, slab, cnt);
+    gemv_coop_kernel<MB, TNW, NW, KF, EPI, true, FP8><<<grid, block, 0, s>>>(x, ldx, a_rows, wp, M, N, K, SK, eps, ep, slab, cnt, wscale);
   else
-    gemv_coop_kernel<MB, TNW, NW, KF, EPI, false><<<grid, block, 0, s>>>(x, ldx, a_rows, wp, M, N, K, SK, eps, ep, slab, cnt);
+    gemv_coop_kernel<MB, TNW, NW, KF, EPI, false, FP8><<<grid, block, 0, s>>>(x, ldx, a_rows, wp, M, N, K, SK, eps, ep, slab, cnt, wscale);
   LSA_CHECK_LAUNCH();
   return LSA_OK;
 }
@@ -318,14 +350,52 @@ int launch(bool norm, const bf16_raw* x, int ldx, const int* a_rows, const bf16_
   X(2, 1, 8, 8) X(4, 1, 8, 8) X(2, 1, 8, 4) X(4, 1, 8, 4) X(2, 2, 8, 4) X(4, 2, 8, 4) X(2, 2, 4, 4) X(4, 2, 4, 4) \
   X(8, 1, 8, 4) X(8, 1, 8, 2) X(8, 2, 4, 2) X(2, 1, 4, 4) X(4, 1, 4, 4) X(2, 1, 4, 8) X(8, 1, 4, 2)
 
-template <int EPI>
+// fp8-weight instantiations (subset; KF even so one 16-B load carries two k-fragments)
+#define LSA_COOP_FP8_CONFIGS(X) \
+  X(2, 1, 8, 4) X(4, 1, 8, 4) X(2, 1, 4, 4) X(4, 1, 4, 4) X(8, 1, 8, 4) X(8, 1, 4, 2) X(2, 1, 8, 8) X(4, 1, 8, 8)
+
+template <int EPI, bool FP8>
 int dispatch(int mb, int tnw, int nw, int kf, bool norm, const bf16_raw* x, int ldx, const int* a_rows, const bf16_raw* wp, int M, int N,
-             int K, int SK, float eps, const EpiArgs& ep, float* slab, unsigned* cnt, hipStream_t s) {
+             int K, int SK, float eps, const EpiArgs& ep, float* slab, unsigned* cnt, const float* wscale, hipStream_t s) {
 #define LSA_C(B, T, W, F) \
-  if (mb == B && tnw == T && nw == W && kf == F) return launch<B, T, W, F, EPI>(norm, x, ldx, a_rows, wp, M, N, K, SK, eps, ep, slab, cnt, s);
-  LSA_COOP_CONFIGS(LSA_C)
+  if (mb == B && tnw == T && nw == W && kf == F) return launch<B, T, W, F, EPI, FP8>(norm, x, ldx, a_rows, wp, M, N, K, SK, eps, ep, slab, cnt, wscale, s);
+  if constexpr (FP8) {
+    LSA_COOP_FP8_CONFIGS(LSA_C)
+  } else {
+    LSA_COOP_CONFIGS(LSA_C)
+  }
 #undef LSA_C
   return LSA_UNSUPPORTED;
+}
+
+
+
+// K is split into 32*kf-k chunks, spread over the SK splits as evenly as possible.
+// Workspace: slab >= SK*N*16*MB*4 + SK*(N/16/(nw*tnw))*16*MB*4 bytes (only when SK > 1);
+// counters: N/16/(nw*tnw) zero-initialised uint32 (reset by the kernel itself).
+template <bool FP8>
+int coop_entry(const void* x, int ldx, const int* a_rows, const void* wp, int M, int N, int K, int norm, float eps,
+               int epi, const EpiArgs* ep, int tnw, int nw, int kf, int sk, float* slab, unsigned* counters,
+               const float* wscale, hipStream_t stream) {
+  if (M < 1 || M > 128 || kf < 1 || K % (32 * kf) || ldx < K || sk < 1) return LSA_BAD_SHAPE;
+  if (FP8 && (kf % 2 || !wscale)) return LSA_BAD_SHAPE;
+  const int mb = M <= 32 ? 2 : (M <= 64 ? 4 : 8);
+  const int tg = nw * tnw;
+  if (N % (16 * tg) || sk > K / (32 * kf)) return LSA_BAD_SHAPE;
+  if (sk > 1 && (!slab || !counters)) return LSA_BAD_SHAPE;
+  const bf16_raw* xx = static_cast<const bf16_raw*>(x);
+  const bf16_raw* w = static_cast<const bf16_raw*>(wp);
+  const bool n = norm != 0;
+#define LSA_D(E) dispatch<E, FP8>(mb, tnw, nw, kf, n, xx, ldx, a_rows, w, M, N, K, sk, eps, *ep, slab, counters, wscale, stream)
+  switch (epi) {
+    case EPI_STORE: return LSA_D(EPI_STORE);
+    case EPI_RESID: return LSA_D(EPI_RESID);
+    case EPI_SWIGLU: return LSA_D(EPI_SWIGLU);
+    case EPI_QKV: return LSA_D(EPI_QKV);
+    case EPI_ARGMAX: return LSA_D(EPI_ARGMAX);
+    default: return LSA_UNSUPPORTED;
+  }
+#undef LSA_D
 }
 
 }  // namespace
@@ -336,20 +406,14 @@ int dispatch(int mb, int tnw, int nw, int kf, bool norm, const bf16_raw* x, int 
 extern "C" int lsa_gemv_coop(const void* x, int ldx, const int* a_rows, const void* wp, int M, int N, int K, int norm, float eps,
                              int epi, const EpiArgs* ep, int tnw, int nw, int kf, int sk, float* slab, unsigned* counters,
                              hipStream_t stream) {
-  if (M < 1 || M > 128 || kf < 1 || K % (32 * kf) || ldx < K || sk < 1) return LSA_BAD_SHAPE;
-  const int mb = M <= 32 ? 2 : (M <= 64 ? 4 : 8);
-  const int tg = nw * tnw;
-  if (N % (16 * tg) || sk > K / (32 * kf)) return LSA_BAD_SHAPE;
-  if (sk > 1 && (!slab || !counters)) return LSA_BAD_SHAPE;
-  const bf16_raw* xx = static_cast<const bf16_raw*>(x);
-  const bf16_raw* w = static_cast<const bf16_raw*>(wp);
-  const bool n = norm != 0;
-  switch (epi) {
-    case EPI_STORE: return dispatch<EPI_STORE>(mb, tnw, nw, kf, n, xx, ldx, a_rows, w, M, N, K, sk, eps, *ep, slab, counters, stream);
-    case EPI_RESID: return dispatch<EPI_RESID>(mb, tnw, nw, kf, n, xx, ldx, a_rows, w, M, N, K, sk, eps, *ep, slab, counters, stream);
-    case EPI_SWIGLU: return dispatch<EPI_SWIGLU>(mb, tnw, nw, kf, n, xx, ldx, a_rows, w, M, N, K, sk, eps, *ep, slab, counters, stream);
-    case EPI_QKV: return dispatch<EPI_QKV>(mb, tnw, nw, kf, n, xx, ldx, a_rows, w, M, N, K, sk, eps, *ep, slab, counters, stream);
-    case EPI_ARGMAX: return dispatch<EPI_ARGMAX>(mb, tnw, nw, kf, n, xx, ldx, a_rows, w, M, N, K, sk, eps, *ep, slab, counters, stream);
-    default: return LSA_UNSUPPORTED;
-  }
+  return coop_entry<false>(x, ldx, a_rows, wp, M, N, K, norm, eps, epi, ep, tnw, nw, kf, sk, slab, counters, nullptr,
+                           stream);
+}
+
+// Same with OCP fp8 e4m3 weights packed as in gemv_fp8.hip and fp32 per-row scales.
+extern "C" int lsa_gemv_coop_fp8(const void* x, int ldx, const int* a_rows, const void* wq, const float* wscale, int M,
+                                 int N, int K, int norm, float eps, int epi, const EpiArgs* ep, int tnw, int nw, int kf,
+                                 int sk, float* slab, unsigned* counters, hipStream_t stream) {
+  return coop_entry<true>(x, ldx, a_rows, wq, M, N, K, norm, eps, epi, ep, tnw, nw, kf, sk, slab, counters, wscale,
+                          stream);
 }

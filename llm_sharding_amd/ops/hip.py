@@ -56,6 +56,7 @@ def lib() -> ctypes.CDLL:
     L.lsa_gemv_coop.argtypes = [vp, i, vp, vp, i, i, i, i, f, i, ctypes.POINTER(EpiArgs), i, i, i, i, vp, vp, vp]
     L.lsa_gemv_fp8.argtypes = [vp, i, vp, vp, vp, i, i, i, i, f, i, ctypes.POINTER(EpiArgs), i, i, i, vp]
     L.lsa_dequant_fp8_packed.argtypes = [vp, vp, vp, i, i, vp]
+    L.lsa_gemv_coop_fp8.argtypes = [vp, i, vp, vp, vp, i, i, i, i, f, i, ctypes.POINTER(EpiArgs), i, i, i, i, vp, vp, vp]
     L.lsa_gemm.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(EpiArgs), i, i, vp, vp, vp]
     L.lsa_attn_decode.argtypes = [vp, i, vp, vp, vp, vp, vp, i, i, i, i, i, f, i, i, vp, vp, vp, i, vp]
     L.lsa_attn_prefill.argtypes = [vp, i, vp, vp, vp, i, i, i, i, i, f, i, vp, i, vp]
@@ -63,7 +64,7 @@ def lib() -> ctypes.CDLL:
     L.lsa_rmsnorm.argtypes = [vp, i, vp, i, i, f, vp, i, vp]
     L.lsa_argmax_finalize.argtypes = [vp, i, vp, vp, i, vp, i, i, vp, vp]
     L.lsa_pos_advance.argtypes = [vp, i, i, vp]
-    for name in ("lsa_gemv", "lsa_gemv_coop", "lsa_gemv_fp8", "lsa_dequant_fp8_packed", "lsa_gemm", "lsa_attn_decode", "lsa_attn_prefill", "lsa_embed", "lsa_rmsnorm",
+    for name in ("lsa_gemv", "lsa_gemv_coop", "lsa_gemv_fp8", "lsa_dequant_fp8_packed", "lsa_gemv_coop_fp8", "lsa_gemm", "lsa_attn_decode", "lsa_attn_prefill", "lsa_embed", "lsa_rmsnorm",
                  "lsa_argmax_finalize", "lsa_pos_advance", "lsa_version"):
         getattr(L, name).restype = ctypes.c_int
     _lib = L
@@ -191,6 +192,37 @@ def gemv_fp8(x: torch.Tensor, wq: torch.Tensor, wscale: torch.Tensor, M: int, N:
     rc = lib().lsa_gemv_fp8(_p(x), x.stride(0), _p(a_rows), _p(wq), _p(wscale), M, N, K, int(norm), float(eps), epi,
                             ctypes.byref(ep), tn, nw, u2, _stream())
     _check(rc, "lsa_gemv_fp8")
+
+
+def proj_fp8(x: torch.Tensor, wq: torch.Tensor, wscale: torch.Tensor, M: int, N: int, K: int, epi: int,
+             ep: EpiArgs, norm: bool = False, eps: float = 1e-5, a_rows: Optional[torch.Tensor] = None,
+             ws: Optional[CoopWorkspace] = None, algo: Optional[tuple] = None) -> None:
+    """W8A16 projection for 1..128 rows: plain fp8 GEMV or the cooperative kernel with fp8
+    weights (``packing.fp8_proj_config`` unless ``algo=(name, cfg)`` is given)."""
+    from .packing import coop_fp8_candidates, coop_slab_floats, fp8_proj_config
+    _req(1 <= M <= 128, f"proj_fp8 supports 1..128 rows, got {M}")
+    name, cfg = algo if algo is not None else fp8_proj_config(N // 16, M, need_even=(epi == EPI_SWIGLU), k=K)
+    if name == "fp8":
+        gemv_fp8(x, wq, wscale, M, N, K, epi, ep, norm=norm, eps=eps, a_rows=a_rows, cfg=cfg)
+        return
+    _req(_is_bf16_cuda(x), "proj_fp8: bf16 cuda activations")
+    _req(wq.is_cuda and wq.dtype == torch.uint8 and wq.numel() == N * K, "proj_fp8: packed fp8 weights")
+    _req(wscale.is_cuda and wscale.dtype == torch.float32 and wscale.numel() >= N, "proj_fp8: fp32 scales")
+    _req(x.dim() == 2 and x.shape[1] >= K and x.stride(1) == 1, "proj_fp8: x must be [rows, >=K] row-major")
+    if a_rows is None:
+        _req(x.shape[0] >= M, "proj_fp8: x has fewer rows than M")
+    else:
+        _req(a_rows.dtype == torch.int32 and a_rows.is_cuda and a_rows.numel() >= M, "proj_fp8: a_rows")
+    cfg = tuple(cfg)
+    _req(cfg in coop_fp8_candidates(N // 16, K, M), f"proj_fp8: coop config {cfg} invalid for N={N} K={K} M={M}")
+    tnw, cnw, kf, sk = cfg
+    if ws is None:
+        ws = default_workspace(x.device)
+    _req(ws.slab.numel() >= coop_slab_floats(N, M, tnw, cnw, kf, sk), "proj_fp8: coop workspace too small")
+    _req(ws.counters.numel() >= N // 16 // (tnw * cnw), "proj_fp8: coop workspace counters too small")
+    rc = lib().lsa_gemv_coop_fp8(_p(x), x.stride(0), _p(a_rows), _p(wq), _p(wscale), M, N, K, int(norm), float(eps),
+                                 epi, ctypes.byref(ep), tnw, cnw, kf, sk, _p(ws.slab), _p(ws.counters), _stream())
+    _check(rc, "lsa_gemv_coop_fp8")
 
 
 def dequant_fp8_packed(wq: torch.Tensor, wscale: torch.Tensor, out: torch.Tensor, N: int, K: int) -> torch.Tensor:

@@ -102,23 +102,47 @@ FP8_CONFIGS = [(1, 1, 4, 2), (1, 1, 8, 2), (1, 1, 4, 4), (2, 1, 4, 2), (2, 1, 8,
                (2, 4, 8, 1)]
 
 
-def fp8_config(n_tiles: int, rows: int, need_even: bool = False, k: int = 4096) -> tuple:
-    """(tn, nw, u2) for the fp8 GEMV: the tuning table entry ("fp8" algo) if measured, else the
-    candidate giving >= 256 workgroups with the most weight bytes in flight per wave."""
+def fp8_gemv_candidates(n_tiles: int, k: int, rows: int, need_even: bool = False) -> list:
     mb = row_blocks(rows)
-    t = _tuned().get((n_tiles * 16, k, mb, bool(need_even)) + ("fp8",))
-    cands = [(tn, nw, u2) for (tn, b, nw, u2) in FP8_CONFIGS
-             if b == mb and n_tiles % tn == 0 and (not need_even or tn % 2 == 0) and (k // 32) % (2 * u2) == 0]
-    if t is not None and t in cands:
-        return t
+    return [(tn, nw, u2) for (tn, b, nw, u2) in FP8_CONFIGS
+            if b == mb and n_tiles % tn == 0 and (not need_even or tn % 2 == 0) and (k // 32) % (2 * u2) == 0]
+
+
+def fp8_config(n_tiles: int, rows: int, need_even: bool = False, k: int = 4096) -> tuple:
+    """(tn, nw, u2) for the plain fp8 GEMV (rows <= 64): the candidate giving >= 256 workgroups
+    with the most weight bytes in flight per wave."""
+    cands = fp8_gemv_candidates(n_tiles, k, rows, need_even)
     if not cands:
         raise ValueError(f"no fp8 GEMV config for {n_tiles} tiles, K={k}, rows={rows}")
+
     def cost(c):
         tn, nw, u2 = c
         g = n_tiles // tn
         eff = g / (N_CU * -(-g // N_CU))
         return (1.0 + 0.4 * rows / (16.0 * tn)) / eff - 0.01 * (nw * u2 / 16.0)
     return min(cands, key=cost)
+
+
+def fp8_proj_config(n_tiles: int, rows: int, need_even: bool = False, k: int = 4096) -> tuple:
+    """("fp8", (tn, nw, u2)) [gemv_fp8.hip] or ("coop_fp8", (tnw, nw, kf, sk)) [gemv_coop.hip,
+    fp8 weights] for a W8A16 projection of ``rows`` rows: the measured table if it has the
+    shape, else the plain kernel up to 16 rows and the cooperative one above (it shares the
+    activations through LDS instead of re-reading them per workgroup)."""
+    t = _tuned().get((n_tiles * 16, k, row_blocks(rows), bool(need_even), "fp8"))
+    if t is not None:
+        algo, cfg = t
+        if (algo == "fp8" and rows <= 64 and cfg in fp8_gemv_candidates(n_tiles, k, rows, need_even)) or \
+           (algo == "coop_fp8" and cfg in coop_fp8_candidates(n_tiles, k, rows)):
+            return t
+    if rows > 16:
+        cands = coop_fp8_candidates(n_tiles, k, rows)
+        pref = [c for c in cands if c[:3] == (1, 8, 4)] or [c for c in cands if c[:2] == (1, 8)] or cands
+        for c in pref:
+            if (n_tiles // (c[0] * c[1])) * c[3] >= N_CU:
+                return ("coop_fp8", c)
+        if pref:
+            return ("coop_fp8", pref[-1])
+    return ("fp8", fp8_config(n_tiles, rows, need_even, k))
 
 
 # (tn, mb, nw, u) instantiated in csrc/kernels/gemv.hip (LSA_GEMV_CONFIGS) - keep in sync.
@@ -168,6 +192,25 @@ def coop_candidates(n_tiles: int, k: int, rows: int) -> list:
     return out
 
 
+# (mb, tnw, nw, kf) with fp8 weights (LSA_COOP_FP8_CONFIGS in gemv_coop.hip) - keep in sync.
+COOP_FP8_CONFIGS = [(2, 1, 8, 4), (4, 1, 8, 4), (2, 1, 4, 4), (4, 1, 4, 4), (8, 1, 8, 4), (8, 1, 4, 2), (2, 1, 8, 8),
+                    (4, 1, 8, 8)]
+
+
+def coop_fp8_candidates(n_tiles: int, k: int, rows: int) -> list:
+    if rows <= 16:
+        return []
+    mb = row_blocks(rows)
+    out = []
+    for (b, tnw, nw, kf) in COOP_FP8_CONFIGS:
+        if b != mb or n_tiles % (tnw * nw) or k % (32 * kf):
+            continue
+        for sk in COOP_SPLITS:
+            if k // (32 * kf) >= sk and (n_tiles // (tnw * nw)) * sk <= 4 * N_CU:
+                out.append((tnw, nw, kf, sk))
+    return out
+
+
 def coop_slab_floats(n: int, rows: int, tnw: int, nw: int, kf: int, sk: int) -> int:
     """fp32 workspace a coop launch needs (0 when sk == 1)."""
     if sk == 1:
@@ -199,8 +242,8 @@ def _tuned() -> dict:
         if os.path.exists(TUNING_FILE):
             with open(TUNING_FILE) as f:
                 for e in json.load(f).get("entries", []):
-                    if e.get("algo") == "fp8":
-                        _TUNED[(e["N"], e["K"], e["mb"], bool(e["even"]), "fp8")] = tuple(e["cfg"])
+                    if e.get("algo") in ("fp8", "coop_fp8"):
+                        _TUNED[(e["N"], e["K"], e["mb"], bool(e["even"]), "fp8")] = (e["algo"], tuple(e["cfg"]))
                     else:
                         _TUNED[(e["N"], e["K"], e["mb"], bool(e["even"]))] = (e.get("algo", "gemv"), tuple(e["cfg"]))
     return _TUNED

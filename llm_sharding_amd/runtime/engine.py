@@ -370,7 +370,7 @@ class StageEngine:
         n = idx.numel()
         if keys is None:
             keys = torch.zeros(n, dtype=torch.int64, device=self.device)
-        step = 64 if self.fp8 else self.DECODE_MAX_ROWS
+        step = self.DECODE_MAX_ROWS
         for c0 in range(0, n, step):
             c = min(step, n - c0)
             self.head_gemv(h, c, keys[c0:c0 + c], a_rows=idx[c0:c0 + c])
@@ -382,8 +382,8 @@ class StageEngine:
         ep = hip.make_epi(keys=keys, col_offset=self.head_v0)
         N, H, eps = self.head_v1 - self.head_v0, self.cfg.hidden_size, self.cfg.rms_norm_eps
         if self.lm_head_s is not None:
-            hip.gemv_fp8(h, self.lm_head.view(-1), self.lm_head_s, rows, N, H, hip.EPI_ARGMAX, ep, norm=True, eps=eps,
-                         a_rows=a_rows)
+            hip.proj_fp8(h, self.lm_head.view(-1), self.lm_head_s, rows, N, H, hip.EPI_ARGMAX, ep, norm=True, eps=eps,
+                         a_rows=a_rows, ws=self.coop_ws)
         else:
             hip.gemv(h, self.lm_head, rows, N, H, hip.EPI_ARGMAX, ep, ws=self.coop_ws, norm=True, eps=eps,
                      a_rows=a_rows)
@@ -439,14 +439,14 @@ class StageEngine:
             nsplit = self._attn_nsplit(rows, kv_max)
         q, attn_o, act, xn = self.buf_q[:rows], self.buf_attn[:rows], self.buf_act[:rows], self.buf_xn[:rows]
         ws = self.coop_ws
-        native_fp8 = self.fp8 and rows <= 64
+        native_fp8 = self.fp8 and rows <= packing.GEMV_MAX_ROWS
 
         def wbf(w, s, N, K):  # packed bf16 weights (fp8 -> scratch for the >64-row kernels)
             return w if s is None else hip.dequant_fp8_packed(w.view(-1), s, self.w_scratch, N, K)
 
         def dec(x, w, s, N, K, epi, ep, norm=False):
             if native_fp8:
-                hip.gemv_fp8(x, w.view(-1), s, rows, N, K, epi, ep, norm=norm, eps=eps)
+                hip.proj_fp8(x, w.view(-1), s, rows, N, K, epi, ep, norm=norm, eps=eps, ws=ws)
             else:
                 hip.gemv(x, wbf(w, s, N, K), rows, N, K, epi, ep, norm=norm, eps=eps, ws=ws)
 
@@ -595,9 +595,7 @@ class DecodeGraph:
         h = eng.buf_h[:rows]
         if self.split_head and self.mode == "first":
             self.keys.copy_(self.keys_in)
-            for c0 in range(0, rows, 64 if eng.fp8 else rows):
-                c = min(64 if eng.fp8 else rows, rows - c0)
-                eng.head_gemv(self.h_fin[c0:c0 + c], c, self.keys[c0:c0 + c])
+            eng.head_gemv(self.h_fin, rows, self.keys)
             hip.argmax_finalize(self.keys, rows, self.tokens, None, 1, self.history,
                                 self.step_ctr if self.history is not None else None)
         if self.mode in ("full", "first"):
@@ -607,17 +605,10 @@ class DecodeGraph:
         eng._forward_hip(h, self.slot, self.pos, None, rows, nsplit=eng.decode_nsplit(rows))
         if self.split_head and self.mode == "last":
             self.keys.zero_()
-            for c0 in range(0, rows, 64 if eng.fp8 else rows):
-                c = min(64 if eng.fp8 else rows, rows - c0)
-                eng.head_gemv(h[c0:c0 + c], c, self.keys[c0:c0 + c])
+            eng.head_gemv(h, rows, self.keys)
             hip.pos_advance(self.pos, rows, 1)
         elif self.mode in ("full", "last"):
-            if eng.fp8 and rows > 64:
-                for c0 in range(0, rows, 64):
-                    c = min(64, rows - c0)
-                    eng.head_gemv(h[c0:c0 + c], c, self.keys[c0:c0 + c])
-            else:
-                eng.head_gemv(h, rows, self.keys)
+            eng.head_gemv(h, rows, self.keys)
             hip.argmax_finalize(self.keys, rows, self.tokens, self.pos, 1, self.history,
                                 self.step_ctr if self.history is not None else None)
         else:

@@ -54,7 +54,7 @@ EPIS = {"qkv": hip.EPI_QKV, "o": hip.EPI_RESID, "gate_up": hip.EPI_SWIGLU, "down
         "lm_head": hip.EPI_ARGMAX}
 
 
-def gemv_sweep(out_rows, models, rows_list, tune_entries):
+def gemv_sweep(out_rows, models, rows_list, tune_entries, fp8=False):
     from llm_sharding_amd.models.rope import rope_table
     from llm_sharding_amd.config import llama2_7b
     cos, sin = rope_table(llama2_7b(), 1024, DEV)
@@ -64,6 +64,10 @@ def gemv_sweep(out_rows, models, rows_list, tune_entries):
             epi = EPIS[name]
             nbuf = max(2, (600 << 20) // (N * K * 2) + 1)
             ws = [packing.pack_b(torch.randn(N, K, device=DEV).mul_(0.02).to(torch.bfloat16)) for _ in range(nbuf)]
+            if fp8:
+                nbuf8 = max(2, (600 << 20) // (N * K) + 1)
+                q8, s8 = packing.quantize_fp8_rows(torch.randn(N, K, device=DEV).mul_(0.02))
+                w8 = [packing.pack_b_fp8(q8).view(-1).clone() for _ in range(nbuf8)]
             for M in rows_list:
                 x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
                 out = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
@@ -89,6 +93,23 @@ def gemv_sweep(out_rows, models, rows_list, tune_entries):
                 for cfg in packing.coop_candidates(N // 16, K, M):
                     us = timeit(lambda i: hip.gemv(x, ws[i % nbuf], M, N, K, epi, ep, norm=norm, coop=cfg, ws=cws))
                     res.append((us, "coop", cfg, N * K * 2 / us / 1e6))
+                if fp8:
+                    r8 = []
+                    for cfg in packing.fp8_gemv_candidates(N // 16, K, M, even) if M <= 64 else []:
+                        us = timeit(lambda i: hip.proj_fp8(x, w8[i % nbuf8], s8, M, N, K, epi, ep, norm=norm,
+                                                           algo=("fp8", cfg)))
+                        r8.append((us, "fp8", cfg, N * K / us / 1e6))
+                    for cfg in packing.coop_fp8_candidates(N // 16, K, M):
+                        us = timeit(lambda i: hip.proj_fp8(x, w8[i % nbuf8], s8, M, N, K, epi, ep, norm=norm,
+                                                           algo=("coop_fp8", cfg), ws=cws))
+                        r8.append((us, "coop_fp8", cfg, N * K / us / 1e6))
+                    r8.sort(key=lambda r: r[0])
+                    line8 = {"kernel": "gemv_fp8", "model": model, "shape": name, "N": N, "K": K, "M": M,
+                             "best_us": round(r8[0][0], 2), "best_algo": r8[0][1], "best_cfg": list(r8[0][2]),
+                             "best_TBps": round(r8[0][3], 2), "all": [(round(r[0], 2), r[1]) + tuple(r[2]) for r in r8]}
+                    print(json.dumps(line8), flush=True)
+                    out_rows.append(line8)
+                    tune_entries.setdefault((N, K, packing.row_blocks(M), even, "fp8"), (r8[0][1], list(r8[0][2])))
                 res.sort(key=lambda r: r[0])
                 best = res[0]
                 line = {"kernel": "gemv", "model": model, "shape": name, "N": N, "K": K, "M": M,
@@ -97,7 +118,7 @@ def gemv_sweep(out_rows, models, rows_list, tune_entries):
                         "all": [(round(r[0], 2), r[1]) + tuple(r[2]) for r in res]}
                 print(json.dumps(line), flush=True)
                 out_rows.append(line)
-                tune_entries[(N, K, packing.row_blocks(M), even)] = (best[1], list(best[2]))
+                tune_entries.setdefault((N, K, packing.row_blocks(M), even), (best[1], list(best[2])))  # smallest M of a row block wins (batch-1 latency)
             del ws
             torch.cuda.empty_cache()
 
@@ -153,21 +174,25 @@ def main():
     ap.add_argument("--models", default="llama2-7b")
     ap.add_argument("--rows", default="1,16,32,64")
     ap.add_argument("--tune", action="store_true", help="write llm_sharding_amd/ops/gemv_tuning.json")
+    ap.add_argument("--fp8", action="store_true", help="also sweep the fp8-weight (W8A16) kernels")
     ap.add_argument("--out", default="gpurun_out/bench_kernels.json")
     a = ap.parse_args()
     hip.lib()
     rows = []
     tune = {}
     if "gemv" in a.only:
-        gemv_sweep(rows, a.models.split(","), [int(r) for r in a.rows.split(",")], tune)
+        gemv_sweep(rows, a.models.split(","), [int(r) for r in a.rows.split(",")], tune, fp8=a.fp8)
         if a.tune:
             old = {}
             if os.path.exists(packing.TUNING_FILE):
                 for e in json.load(open(packing.TUNING_FILE)).get("entries", []):
-                    old[(e["N"], e["K"], e["mb"], bool(e["even"]))] = (e.get("algo", "gemv"), e["cfg"])
+                    key = (e["N"], e["K"], e["mb"], bool(e["even"]))
+                    if e.get("algo") in ("fp8", "coop_fp8"):
+                        key = key + ("fp8",)
+                    old[key] = (e.get("algo", "gemv"), e["cfg"])
             old.update(tune)
             ents = [{"N": k[0], "K": k[1], "mb": k[2], "even": k[3], "algo": v[0], "cfg": v[1]}
-                    for k, v in sorted(old.items())]
+                    for k, v in sorted(old.items(), key=lambda kv: tuple(map(str, kv[0])))]
             with open(packing.TUNING_FILE, "w") as f:
                 json.dump({"device": torch.cuda.get_device_name(), "entries": ents}, f, indent=1)
             print(f"wrote {len(ents)} tuning entries to {packing.TUNING_FILE}")

@@ -441,3 +441,29 @@ def test_gemv_fp8_swiglu_argmax_and_dequant():
     scratch = torch.empty(V * H, dtype=torch.bfloat16, device=DEV)
     wp = h.dequant_fp8_packed(packing.pack_b_fp8(ql).view(-1), sl, scratch, V, H)
     assert torch.equal(wp, packing.pack_b(packing.dequantize_fp8_rows(ql, sl).to(torch.bfloat16)))
+
+
+@pytest.mark.parametrize("cfg", packing.COOP_FP8_CONFIGS)
+def test_gemv_coop_fp8_every_config(cfg):
+    """Cooperative split-K GEMV with fp8 weights: every instantiated config x every legal split,
+    fused RMSNorm + residual, against fp32 math on the dequantised weights."""
+    h = hip()
+    mb, tnw, nw, kf = cfg
+    M = {2: 29, 4: 50, 8: 100}[mb]
+    N = 16 * tnw * nw * 3
+    for K in (4096, 64 * kf):
+        x = _rnd(M, K)
+        g = (1 + 0.1 * torch.randn(K, device=DEV)).to(torch.bfloat16)
+        q, sc = packing.quantize_fp8_rows(packing.fold_norm(_rnd(N, K, scale=0.02), g))
+        wd = packing.dequantize_fp8_rows(q, sc)
+        wq = packing.pack_b_fp8(q).view(-1)
+        resid = _rnd(M, N)
+        xn = x.float() * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + 1e-5)
+        ref = resid.float() + xn @ wd.T
+        for c in packing.coop_fp8_candidates(N // 16, K, M):
+            if c[:3] != (tnw, nw, kf):
+                continue
+            out = resid.clone()
+            h.proj_fp8(x, wq, sc, M, N, K, h.EPI_RESID, h.make_epi(out=out, resid=out, ldo=N, ldr=N), norm=True,
+                       algo=("coop_fp8", c))
+            assert rel_err(out, ref) < 8e-3, (cfg, K, c)
