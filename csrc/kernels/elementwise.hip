@@ -2,6 +2,8 @@
 // (cdna_hip_programming.md Guideline 13):
 //   lsa_embed        nn.Embedding row gather (reference node_worker.py:215,302)
 //   lsa_rmsnorm      standalone RMSNorm (prefill path; decode fuses it into the GEMV)
+//   lsa_layernorm    LayerNorm with bias (GPT-2 ln_1 / ln_2 / ln_f), optionally fused with the
+//                    learned absolute position embedding add (x += wpe[pos], written back)
 //   lsa_argmax_finalize  decode the fused-argmax keys -> token ids, reset the keys, append to
 //                    the device-side history and advance the per-row positions. This keeps
 //                    the whole autoregressive step on the device (no .item() host sync per
@@ -49,6 +51,62 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const bf16_raw* __restrict
   }
 }
 
+// Two-pass (mean, then centred variance) over the row held in L2; the optional position add
+// rounds to bf16 first, as HF's ``inputs_embeds + position_embeds`` in the model dtype does.
+__global__ __launch_bounds__(256) void layernorm_kernel(bf16_raw* __restrict__ x, int ldx,
+                                                        const bf16_raw* __restrict__ pe,
+                                                        const int* __restrict__ pos,
+                                                        const bf16_raw* __restrict__ g,
+                                                        const bf16_raw* __restrict__ b, int H,
+                                                        float eps, bf16_raw* __restrict__ out,
+                                                        int ldo) {
+  __shared__ float s_part[2][4];
+  const int row = blockIdx.x, tid = threadIdx.x;
+  bf16_raw* xr = x + (size_t)row * ldx;
+  const bf16_raw* pr = pe ? pe + (size_t)pos[row] * H : nullptr;
+  float s = 0.f;
+  for (int c = tid; c < (H >> 3); c += 256) {
+    float f[8];
+    unpack8(ld16(xr + c * 8), f);
+    if (pr) {
+      float q[8];
+      unpack8(ld16(pr + c * 8), q);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] += q[j];
+      const u32x4_t v = pack8(f);
+      st16(xr + c * 8, v);
+      unpack8(v, f);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += f[j];
+  }
+  s = wave_sum(s);
+  if ((tid & 63) == 0) s_part[0][tid >> 6] = s;
+  __syncthreads();
+  const float mu = (s_part[0][0] + s_part[0][1] + s_part[0][2] + s_part[0][3]) / (float)H;
+  float v2 = 0.f;
+  for (int c = tid; c < (H >> 3); c += 256) {
+    float f[8];
+    unpack8(ld16(xr + c * 8), f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v2 += (f[j] - mu) * (f[j] - mu);
+  }
+  v2 = wave_sum(v2);
+  if ((tid & 63) == 0) s_part[1][tid >> 6] = v2;
+  __syncthreads();
+  const float rs = rsqrtf((s_part[1][0] + s_part[1][1] + s_part[1][2] + s_part[1][3]) / (float)H + eps);
+  bf16_raw* orow = out + (size_t)row * ldo;
+  for (int c = tid; c < (H >> 3); c += 256) {
+    float f[8], gg[8], bb[8];
+    unpack8(ld16(xr + c * 8), f);
+    unpack8(ld16(g + c * 8), gg);
+    unpack8(ld16(b + c * 8), bb);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = (f[j] - mu) * rs * gg[j] + bb[j];
+    st16(orow + c * 8, pack8(f));
+  }
+}
+
 // One workgroup; rows <= 1024.
 __global__ void argmax_finalize_kernel(unsigned long long* __restrict__ keys, int rows,
                                        int* __restrict__ tokens, int* __restrict__ pos,
@@ -86,6 +144,19 @@ extern "C" int lsa_rmsnorm(const void* x, int ldx, const void* w, int rows, int 
   rmsnorm_kernel<<<rows, 256, 0, stream>>>(static_cast<const bf16_raw*>(x), ldx,
                                           static_cast<const bf16_raw*>(w), H, eps,
                                           static_cast<bf16_raw*>(out), ldo);
+  LSA_CHECK_LAUNCH();
+  return LSA_OK;
+}
+
+extern "C" int lsa_layernorm(void* x, int ldx, const void* pe, const int* pos, const void* g,
+                             const void* b, int rows, int H, float eps, void* out, int ldo,
+                             hipStream_t stream) {
+  if (rows < 1 || H % 8 || !g || !b || (pe && !pos)) return LSA_BAD_SHAPE;
+  layernorm_kernel<<<rows, 256, 0, stream>>>(static_cast<bf16_raw*>(x), ldx,
+                                            static_cast<const bf16_raw*>(pe), pos,
+                                            static_cast<const bf16_raw*>(g),
+                                            static_cast<const bf16_raw*>(b), H, eps,
+                                            static_cast<bf16_raw*>(out), ldo);
   LSA_CHECK_LAUNCH();
   return LSA_OK;
 }

@@ -195,12 +195,12 @@ __global__ __launch_bounds__(GTHR) void gemm_packed_kernel(const bf16_raw* __res
           const int col = (ntile0 + tn) * 16 + n;
           if (EPI == EPI_QKV) {
             const float vp = __shfl_xor(v, 8, 64);
-            if (gm < M) epi_qkv_store(ep, gm, col, v, vp);
+            if (gm < M) epi_qkv_store(ep, gm, col, v + epi_bias(ep, col), vp + epi_bias(ep, col ^ 8));
           } else if (gm < M) {
             if (EPI == EPI_STORE)
-              ep.out[(size_t)gm * ep.ldo + col] = f2bf(v);
+              ep.out[(size_t)gm * ep.ldo + col] = f2bf(epi_act(ep, v + epi_bias(ep, col)));
             else if (EPI == EPI_RESID)
-              ep.out[(size_t)gm * ep.ldo + col] = f2bf(bf2f(ep.resid[(size_t)gm * ep.ldr + col]) + v);
+              ep.out[(size_t)gm * ep.ldo + col] = f2bf(bf2f(ep.resid[(size_t)gm * ep.ldr + col]) + v + epi_bias(ep, col));
           }
         }
       }

@@ -173,13 +173,13 @@ __global__ __launch_bounds__(NW * 64) void gemv_packed_kernel(
       const float v = rsum(t, mm, n) * r;
       const int col = (nt0 + t) * 16 + n;
       if (EPI == EPI_STORE) {
-        ep.out[(size_t)mm * ep.ldo + col] = f2bf(v);
+        ep.out[(size_t)mm * ep.ldo + col] = f2bf(epi_act(ep, v + epi_bias(ep, col)));
       } else if (EPI == EPI_RESID) {
-        ep.out[(size_t)mm * ep.ldo + col] = f2bf(bf2f(ep.resid[(size_t)mm * ep.ldr + col]) + v);
+        ep.out[(size_t)mm * ep.ldo + col] = f2bf(bf2f(ep.resid[(size_t)mm * ep.ldr + col]) + v + epi_bias(ep, col));
       } else if (EPI == EPI_QKV) {
-        epi_qkv_store(ep, mm, col, v, rsum(t, mm, n ^ 8) * r);
+        epi_qkv_store(ep, mm, col, v + epi_bias(ep, col), rsum(t, mm, n ^ 8) * r + epi_bias(ep, col ^ 8));
       } else if (EPI == EPI_ARGMAX) {
-        atomicMax(&s_key[mm], argmax_key(v, (unsigned)(col + ep.col_offset)));
+        atomicMax(&s_key[mm], argmax_key(v + epi_bias(ep, col), (unsigned)(col + ep.col_offset)));
       }
     }
     if (EPI == EPI_ARGMAX) {

@@ -10,6 +10,13 @@ presets for the models the reference is configured with:
 * Llama-2-70B (BASELINE.json config 4)
 
 plus tiny configs used by the CPU test-suite.
+
+The same dataclass also describes **GPT-2** (``model_type == "gpt2"``): the reference's
+sharder writes GPT-2 shards (``/root/reference/utils/model_sharder.py:96-132``) but nothing in
+the reference can load or run them. Here GPT-2 is a served family: pre-LN
+LayerNorm with bias, learned absolute positions (no RoPE), Conv1D projections with biases,
+tanh-GELU MLP, tied lm_head. HF GPT-2 ``config.json`` keys (``n_embd``, ``n_layer``,
+``n_head``, ``n_positions``, ``n_inner``, ``layer_norm_epsilon``) are mapped on load.
 """
 from __future__ import annotations
 
@@ -53,6 +60,21 @@ class LlamaConfig:
         return self.q_size + 2 * self.kv_size
 
     @property
+    def is_gpt2(self) -> bool:
+        return self.model_type == "gpt2"
+
+    @property
+    def mlp_in_size(self) -> int:
+        """Output width of the fused MLP input projection (gate|up for SwiGLU, c_fc for GPT-2)."""
+        return self.intermediate_size if self.is_gpt2 else 2 * self.intermediate_size
+
+    @property
+    def head_rows(self) -> int:
+        """lm_head rows as served: the vocabulary padded to the 16-column MFMA tile (GPT-2's
+        50257 -> 50272; padding rows copy row 0, so they can never win the argmax tie-break)."""
+        return -(-self.vocab_size // 16) * 16
+
+    @property
     def gqa_group(self) -> int:
         return self.num_attention_heads // self.num_key_value_heads
 
@@ -65,6 +87,8 @@ class LlamaConfig:
 
     def layer_param_count(self) -> int:
         H, I = self.hidden_size, self.intermediate_size
+        if self.is_gpt2:  # c_attn, c_proj, c_fc, mlp.c_proj (+ biases), ln_1, ln_2 (+ biases)
+            return H * self.qkv_size + self.qkv_size + H * H + H + 2 * H * I + I + H + 4 * H
         return H * self.qkv_size + self.q_size * H + 3 * H * I + 2 * H
 
     def layer_bytes(self, elem_bytes: int = 2) -> int:
@@ -82,6 +106,18 @@ class LlamaConfig:
     # ------------------------------------------------------------------ IO
     @classmethod
     def from_dict(cls, d: dict) -> "LlamaConfig":
+        if d.get("model_type") == "gpt2" and "n_embd" in d:  # HF GPT2Config keys
+            H = int(d["n_embd"])
+            m = {"hidden_size": H, "num_hidden_layers": d.get("n_layer", 12),
+                 "num_attention_heads": d.get("n_head", 12), "num_key_value_heads": d.get("n_head", 12),
+                 "head_dim": H // int(d.get("n_head", 12)),
+                 "intermediate_size": d.get("n_inner") or 4 * H,
+                 "max_position_embeddings": d.get("n_positions", 1024),
+                 "rms_norm_eps": d.get("layer_norm_epsilon", 1e-5), "tie_word_embeddings": True}
+            if d.get("activation_function", "gelu_new") not in ("gelu_new", "gelu_pytorch_tanh"):
+                raise ValueError(f"unsupported GPT-2 activation {d.get('activation_function')!r}")
+            d = {**{k: v for k, v in d.items() if k not in ("n_embd", "n_layer", "n_head", "n_inner",
+                                                              "n_positions", "layer_norm_epsilon")}, **m}
         fields = {f.name for f in dataclasses.fields(cls)}
         kw = {k: v for k, v in d.items() if k in fields}
         if "num_key_value_heads" not in d or d.get("num_key_value_heads") is None:
@@ -107,8 +143,18 @@ class LlamaConfig:
 
     def to_dict(self) -> dict:
         d = dataclasses.asdict(self)
-        d["architectures"] = ["LlamaForCausalLM"]
         d["torch_dtype"] = "bfloat16"
+        if self.is_gpt2:  # HF GPT2Config layout (readable by transformers as well)
+            for k in ("hidden_size", "num_hidden_layers", "num_attention_heads", "num_key_value_heads",
+                      "head_dim", "intermediate_size", "max_position_embeddings", "rms_norm_eps",
+                      "rope_theta", "rope_scaling"):
+                d.pop(k)
+            d.update({"architectures": ["GPT2LMHeadModel"], "n_embd": self.hidden_size,
+                      "n_layer": self.num_hidden_layers, "n_head": self.num_attention_heads,
+                      "n_inner": self.intermediate_size, "n_positions": self.max_position_embeddings,
+                      "layer_norm_epsilon": self.rms_norm_eps, "activation_function": "gelu_new"})
+            return d
+        d["architectures"] = ["LlamaForCausalLM"]
         return d
 
     def save_pretrained(self, path: str) -> None:
@@ -158,12 +204,35 @@ def tiny(layers: int = 4, hidden: int = 256, heads: int = 4, kv_heads: int = 2,
     return cfg
 
 
+def gpt2(size: str = "small") -> LlamaConfig:
+    """GPT-2 124M / medium 355M / large 774M / xl 1.5B (HF ``gpt2*`` configs)."""
+    H, L, nh = {"small": (768, 12, 12), "medium": (1024, 24, 16), "large": (1280, 36, 20),
+                "xl": (1600, 48, 25)}[size]
+    return LlamaConfig(hidden_size=H, intermediate_size=4 * H, num_hidden_layers=L, num_attention_heads=nh,
+                       num_key_value_heads=nh, head_dim=H // nh, vocab_size=50257, max_position_embeddings=1024,
+                       rms_norm_eps=1e-5, tie_word_embeddings=True, bos_token_id=50256, eos_token_id=50256,
+                       model_type="gpt2", name="gpt2" if size == "small" else f"gpt2-{size}")
+
+
+def tiny_gpt2(layers: int = 4, hidden: int = 256, heads: int = 4, vocab: int = 500) -> LlamaConfig:
+    """Small GPT-2 for CPU tests (vocab deliberately not a multiple of 16)."""
+    return LlamaConfig(hidden_size=hidden, intermediate_size=4 * hidden, num_hidden_layers=layers,
+                       num_attention_heads=heads, num_key_value_heads=heads, head_dim=hidden // heads,
+                       vocab_size=vocab, max_position_embeddings=512, tie_word_embeddings=True,
+                       bos_token_id=vocab - 1, eos_token_id=vocab - 1, model_type="gpt2", name="tiny-gpt2")
+
+
 PRESETS = {
     "llama2-7b": llama2_7b,
     "llama2-13b": llama2_13b,
     "llama2-70b": llama2_70b,
     "llama3.2-3b": llama32_3b,
     "tiny": tiny,
+    "gpt2": gpt2,
+    "gpt2-medium": lambda: gpt2("medium"),
+    "gpt2-large": lambda: gpt2("large"),
+    "gpt2-xl": lambda: gpt2("xl"),
+    "tiny-gpt2": tiny_gpt2,
 }
 
 
@@ -195,5 +264,5 @@ def human_bytes(n: float) -> str:
     return f"{n:.2f} TiB"
 
 
-__all__ = ["LlamaConfig", "llama2_7b", "llama2_13b", "llama2_70b", "llama32_3b", "tiny",
+__all__ = ["LlamaConfig", "llama2_7b", "llama2_13b", "llama2_70b", "llama32_3b", "tiny", "gpt2", "tiny_gpt2",
            "get_preset", "dtype_suffix", "ceil_div", "round_up", "human_bytes", "math"]

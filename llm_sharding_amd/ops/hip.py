@@ -29,9 +29,10 @@ class EpiArgs(ctypes.Structure):
         ("out", ctypes.c_void_p), ("resid", ctypes.c_void_p), ("k_cache", ctypes.c_void_p),
         ("v_cache", ctypes.c_void_p), ("slot", ctypes.c_void_p), ("pos", ctypes.c_void_p),
         ("cos_t", ctypes.c_void_p), ("sin_t", ctypes.c_void_p), ("keys", ctypes.c_void_p),
+        ("bias", ctypes.c_void_p),
         ("ldo", ctypes.c_int), ("ldr", ctypes.c_int), ("n_heads", ctypes.c_int),
         ("n_kv", ctypes.c_int), ("head_dim", ctypes.c_int), ("t_max", ctypes.c_int),
-        ("col_offset", ctypes.c_int), ("pad_", ctypes.c_int),
+        ("col_offset", ctypes.c_int), ("act", ctypes.c_int),
     ]
 
 
@@ -62,9 +63,10 @@ def lib() -> ctypes.CDLL:
     L.lsa_attn_prefill.argtypes = [vp, i, vp, vp, vp, i, i, i, i, i, f, i, vp, i, vp]
     L.lsa_embed.argtypes = [vp, i, vp, i, vp, i, vp]
     L.lsa_rmsnorm.argtypes = [vp, i, vp, i, i, f, vp, i, vp]
+    L.lsa_layernorm.argtypes = [vp, i, vp, vp, vp, vp, i, i, f, vp, i, vp]
     L.lsa_argmax_finalize.argtypes = [vp, i, vp, vp, i, vp, i, i, vp, vp]
     L.lsa_pos_advance.argtypes = [vp, i, i, vp]
-    for name in ("lsa_gemv", "lsa_gemv_coop", "lsa_gemv_fp8", "lsa_dequant_fp8_packed", "lsa_gemv_coop_fp8", "lsa_gemm", "lsa_attn_decode", "lsa_attn_prefill", "lsa_embed", "lsa_rmsnorm",
+    for name in ("lsa_gemv", "lsa_gemv_coop", "lsa_gemv_fp8", "lsa_dequant_fp8_packed", "lsa_gemv_coop_fp8", "lsa_gemm", "lsa_attn_decode", "lsa_attn_prefill", "lsa_embed", "lsa_rmsnorm", "lsa_layernorm",
                  "lsa_argmax_finalize", "lsa_pos_advance", "lsa_version"):
         getattr(L, name).restype = ctypes.c_int
     _lib = L
@@ -93,11 +95,18 @@ def _is_bf16_cuda(*ts) -> bool:
     return all(t is None or (t.is_cuda and t.dtype == torch.bfloat16) for t in ts)
 
 
+ACT_NONE, ACT_GELU = 0, 1  # EpiArgs.act (EPI_STORE): identity / tanh-GELU (GPT-2 "gelu_new")
+
+
 def make_epi(out=None, resid=None, k_cache=None, v_cache=None, slot=None, pos=None, cos=None,
              sin=None, keys=None, ldo=0, ldr=0, n_heads=0, n_kv=0, head_dim=0, t_max=0,
-             col_offset=0) -> EpiArgs:
+             col_offset=0, bias=None, act=ACT_NONE) -> EpiArgs:
+    """Epilogue arguments. ``bias``: optional fp32 [N] added to every output column (in packed
+    column order); ``cos=None`` with EPI_QKV: no RoPE, natural q|k|v column order."""
+    if bias is not None:
+        _req(bias.dtype == torch.float32 and bias.is_contiguous(), "epilogue bias: contiguous fp32")
     return EpiArgs(_p(out), _p(resid), _p(k_cache), _p(v_cache), _p(slot), _p(pos), _p(cos), _p(sin),
-                   _p(keys), ldo, ldr, n_heads, n_kv, head_dim, t_max, col_offset, 0)
+                   _p(keys), _p(bias), ldo, ldr, n_heads, n_kv, head_dim, t_max, col_offset, int(act))
 
 
 # ------------------------------------------------------------------------------ projections
@@ -370,6 +379,20 @@ def rmsnorm(x: torch.Tensor, w: Optional[torch.Tensor], out: torch.Tensor, rows:
     _req(_is_bf16_cuda(x, w, out), "rmsnorm: bf16 cuda tensors")
     rc = lib().lsa_rmsnorm(_p(x), x.stride(0), _p(w), rows, H, float(eps), _p(out), out.stride(0), _stream())
     _check(rc, "lsa_rmsnorm")
+
+
+def layernorm(x: torch.Tensor, out: torch.Tensor, w: torch.Tensor, b: torch.Tensor, rows: int, eps: float,
+              pos_emb: Optional[torch.Tensor] = None, pos: Optional[torch.Tensor] = None) -> None:
+    """out = LayerNorm(x) * w + b (GPT-2). With ``pos_emb``: first ``x += pos_emb[pos]`` in
+    place (learned absolute positions, bf16-rounded as HF does)."""
+    H = w.numel()
+    _req(_is_bf16_cuda(x, w, b, out) and b.numel() == H and x.shape[1] >= H, "layernorm: bf16 cuda tensors")
+    if pos_emb is not None:
+        _req(pos is not None and pos.dtype == torch.int32 and pos.numel() >= rows and pos_emb.shape[1] == H,
+             "layernorm: pos_emb needs int32 positions")
+    rc = lib().lsa_layernorm(_p(x), x.stride(0), _p(pos_emb), _p(pos), _p(w), _p(b), rows, H, float(eps),
+                             _p(out), out.stride(0), _stream())
+    _check(rc, "lsa_layernorm")
 
 
 def argmax_finalize(keys: torch.Tensor, rows: int, tokens: torch.Tensor, pos: Optional[torch.Tensor] = None,

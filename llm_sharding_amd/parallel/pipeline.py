@@ -100,7 +100,7 @@ class PipelineStage:
         # first stage [V1, V). The ring back-edge then carries the raw final hidden + partial
         # argmax keys instead of token ids, and the first stage completes the argmax at the
         # start of its next step - the ~0.4-layer lm_head no longer sits on one stage only.
-        V = cfg.vocab_size
+        V = cfg.head_rows
         v1 = (V // 2) // 128 * 128
         self.split = (world > 1 and v1 > 0) if split_head is None else split_head
         head_cols = None

@@ -30,6 +30,7 @@ import torch
 import torch.nn.functional as F
 
 from ..config import LlamaConfig, ceil_div
+from ..models import gpt2 as G2
 from ..models import weights as W
 from ..models.rope import rope_table
 from ..ops import packing
@@ -51,6 +52,14 @@ class WeightSource:
     def lm_head(self, device, dtype) -> torch.Tensor:
         raise NotImplementedError
 
+    def pos_embedding(self, device, dtype) -> Optional[torch.Tensor]:
+        """Learned absolute position table (GPT-2 ``wpe``); None for RoPE models."""
+        return None
+
+    def final_norm_bias(self, device, dtype) -> Optional[torch.Tensor]:
+        """Final LayerNorm bias (GPT-2 ``ln_f.bias``); None for RMSNorm models."""
+        return None
+
 
 class ShardFolderSource(WeightSource):
     """Reference on-disk format (``block_{i}.pth`` ...), read with ``weights_only=True``."""
@@ -60,16 +69,30 @@ class ShardFolderSource(WeightSource):
         self.cfg = cfg or LlamaConfig.from_pretrained(shards_path)
 
     def layer(self, i, device, dtype):
+        if self.cfg.is_gpt2:
+            return G2.load_block(self.path, i, device, dtype)
         return W.load_block(self.path, i, device, dtype)
 
     def embedding(self, device, dtype):
+        if self.cfg.is_gpt2:
+            return G2.load_embedding(self.path, device, dtype)[0]
         return W.load_single(self.path, "embedding.pth", device, dtype)
 
     def final_norm(self, device, dtype):
+        if self.cfg.is_gpt2:
+            return G2.load_ln_f(self.path, device, dtype)[0]
         return W.load_single(self.path, "final_norm.pth", device, dtype)
 
     def lm_head(self, device, dtype):
+        if self.cfg.is_gpt2:
+            return G2.load_lm_head(self.path, device, dtype)
         return W.load_lm_head(self.path, self.cfg, device, dtype)
+
+    def pos_embedding(self, device, dtype):
+        return G2.load_embedding(self.path, device, dtype)[1] if self.cfg.is_gpt2 else None
+
+    def final_norm_bias(self, device, dtype):
+        return G2.load_ln_f(self.path, device, dtype)[1] if self.cfg.is_gpt2 else None
 
 
 class RandomSource(WeightSource):
@@ -79,16 +102,30 @@ class RandomSource(WeightSource):
         self.cfg, self.seed = cfg, seed
 
     def layer(self, i, device, dtype):
+        if self.cfg.is_gpt2:
+            return G2.random_layer(self.cfg, i, dtype, device, self.seed)
         return W.random_layer(self.cfg, i, dtype, device, self.seed)
 
     def embedding(self, device, dtype):
+        if self.cfg.is_gpt2:
+            return G2.random_wte(self.cfg, dtype, device, self.seed)
         return W.random_embedding(self.cfg, dtype, device, self.seed)
 
     def final_norm(self, device, dtype):
+        if self.cfg.is_gpt2:
+            return G2.random_ln_f(self.cfg, dtype, device, self.seed)[0]
         return W.random_final_norm(self.cfg, dtype, device, self.seed)
 
     def lm_head(self, device, dtype):
+        if self.cfg.is_gpt2:  # tied to wte
+            return G2.random_wte(self.cfg, dtype, device, self.seed)
         return W.random_lm_head(self.cfg, dtype, device, self.seed)
+
+    def pos_embedding(self, device, dtype):
+        return G2.random_wpe(self.cfg, dtype, device, self.seed) if self.cfg.is_gpt2 else None
+
+    def final_norm_bias(self, device, dtype):
+        return G2.random_ln_f(self.cfg, dtype, device, self.seed)[1] if self.cfg.is_gpt2 else None
 
 
 @dataclass
@@ -105,6 +142,14 @@ class LayerWeights:
     o_s: Optional[torch.Tensor] = None
     gate_up_s: Optional[torch.Tensor] = None
     down_s: Optional[torch.Tensor] = None
+    # GPT-2: LayerNorm biases (bf16) and projection biases (fp32, packed column order);
+    # gate_up / down hold c_fc / mlp.c_proj
+    ln_in_b: Optional[torch.Tensor] = None
+    ln_post_b: Optional[torch.Tensor] = None
+    qkv_b: Optional[torch.Tensor] = None
+    o_b: Optional[torch.Tensor] = None
+    gate_up_b: Optional[torch.Tensor] = None
+    down_b: Optional[torch.Tensor] = None
 
 
 def _is_gpu(device: torch.device) -> bool:
@@ -155,8 +200,8 @@ class StageEngine:
         self.lm_head_s = None
         # vocab rows [v0, v1) of the lm_head held here (a pipeline may split the head between its
         # last and first stage so that neither carries the whole 0.4-layer lm_head)
-        self.head_v0, self.head_v1 = head_cols if head_cols is not None else (0, cfg.vocab_size)
-        if not (0 <= self.head_v0 < self.head_v1 <= cfg.vocab_size) or (self.head_v1 - self.head_v0) % 16:
+        self.head_v0, self.head_v1 = head_cols if head_cols is not None else (0, cfg.head_rows)
+        if not (0 <= self.head_v0 < self.head_v1 <= cfg.head_rows) or (self.head_v1 - self.head_v0) % 16:
             raise ValueError(f"bad head_cols {head_cols}")
         self.source = source
         self.max_slots = int(max_slots)
@@ -166,6 +211,7 @@ class StageEngine:
         self.verbose = verbose
         self.layers: list = []
         self.embed_w = self.final_norm = self.lm_head = None
+        self.pos_emb = self.final_norm_b = None
         self.k_cache: list = []
         self.v_cache: list = []
         self.seq_len = [0] * self.max_slots  # host-side KV length per slot
@@ -195,23 +241,34 @@ class StageEngine:
         if self.has_embed:
             self._log("[INFO] loading embedding layer...")
             self.embed_w = src.embedding(dev, dt).contiguous()
+        if cfg.is_gpt2 and self.start == 0:  # wpe is added in front of layer 0 (fused into ln_1)
+            self.pos_emb = src.pos_embedding(dev, dt).contiguous()
         if self.has_head:
             self._log("[INFO] loading final norm / lm_head...")
             self.final_norm = src.final_norm(dev, dt).contiguous()
+            fb = src.final_norm_bias(dev, dt)
+            self.final_norm_b = fb.contiguous() if fb is not None else None
             lm = src.lm_head(dev, dt)
-            if (self.head_v0, self.head_v1) != (0, self.cfg.vocab_size):
+            if lm.shape[0] < cfg.head_rows:  # pad to whole 16-row tiles with copies of row 0
+                lm = torch.cat([lm, lm[:1].expand(cfg.head_rows - lm.shape[0], -1)])
+            if (self.head_v0, self.head_v1) != (0, lm.shape[0]):
                 lm = lm[self.head_v0:self.head_v1]
-            # GPU: final RMSNorm weight folded into the packed lm_head (fused norm+GEMV+argmax)
+            # GPU: final RMSNorm weight folded into the packed lm_head (fused norm+GEMV+argmax);
+            # GPT-2's LayerNorm (mean + bias) runs as its own kernel in front of a plain GEMV
+            if self.gpu and not cfg.is_gpt2:
+                lm = packing.fold_norm(lm, self.final_norm)
             if self.fp8:
-                q, self.lm_head_s = packing.quantize_fp8_rows(packing.fold_norm(lm, self.final_norm))
+                q, self.lm_head_s = packing.quantize_fp8_rows(lm)
                 self.lm_head = packing.pack_b_fp8(q)
             else:
-                self.lm_head = packing.pack_b(packing.fold_norm(lm, self.final_norm)) if self.gpu else lm.contiguous()
+                self.lm_head = packing.pack_b(lm) if self.gpu else lm.contiguous()
             del lm
         self._alloc_runtime()
 
     def _prepare_layer(self, lw: dict) -> LayerWeights:
         cfg = self.cfg
+        if cfg.is_gpt2:
+            return self._prepare_layer_gpt2(lw)
         qkv = packing.fuse_qkv(lw["self_attn.q_proj.weight"], lw["self_attn.k_proj.weight"],
                                lw["self_attn.v_proj.weight"], cfg.num_attention_heads,
                                cfg.num_key_value_heads, cfg.head_dim)
@@ -237,13 +294,33 @@ class StageEngine:
         return LayerWeights(None, None, None, None, lw["input_layernorm.weight"],
                             lw["post_attention_layernorm.weight"], raw=lw)
 
+    def _prepare_layer_gpt2(self, lw: dict) -> LayerWeights:
+        t = G2.to_linear(lw)
+        if not self.gpu:
+            return LayerWeights(None, None, None, None, t["ln1_w"], t["ln2_w"], raw=t, ln_in_b=t["ln1_b"],
+                                ln_post_b=t["ln2_b"])
+        mats, scales = [], []
+        for k in ("qkv_w", "o_w", "fc_w", "proj_w"):
+            if self.fp8:
+                q, sc = packing.quantize_fp8_rows(t[k])
+                mats.append(packing.pack_b_fp8(q))
+                scales.append(sc)
+            else:
+                mats.append(packing.pack_b(t[k]))
+                scales.append(None)
+        fb = {k: t[k].float().contiguous() for k in ("qkv_b", "o_b", "fc_b", "proj_b")}
+        return LayerWeights(*mats, t["ln1_w"].contiguous(), t["ln2_w"].contiguous(), qkv_s=scales[0], o_s=scales[1],
+                            gate_up_s=scales[2], down_s=scales[3], ln_in_b=t["ln1_b"].contiguous(),
+                            ln_post_b=t["ln2_b"].contiguous(), qkv_b=fb["qkv_b"], o_b=fb["o_b"],
+                            gate_up_b=fb["fc_b"], down_b=fb["proj_b"])
+
     def _alloc_runtime(self) -> None:
         cfg, dev = self.cfg, self.device
         nkv, hd = cfg.num_key_value_heads, cfg.head_dim
         shape = (self.max_slots, nkv, self.max_seq, hd)
         self.k_cache = [torch.zeros(shape, dtype=self.dtype, device=dev) for _ in range(self.n_layers)]
         self.v_cache = [torch.zeros(shape, dtype=self.dtype, device=dev) for _ in range(self.n_layers)]
-        self.cos, self.sin = rope_table(cfg, self.max_seq, dev)
+        self.cos, self.sin = (None, None) if cfg.is_gpt2 else rope_table(cfg, self.max_seq, dev)
         R = max(self.max_prefill_rows, self.DECODE_MAX_ROWS)
         H, I = cfg.hidden_size, cfg.intermediate_size
         if self.gpu:
@@ -263,10 +340,11 @@ class StageEngine:
             # split-K workspace of the cooperative decode GEMV (gemv_coop.hip), owned by the
             # stage and allocated before any graph capture
             from ..ops import hip
-            shapes = [(cfg.qkv_size, H), (H, cfg.q_size), (2 * I, H), (H, I)]
+            shapes = [(cfg.qkv_size, H), (H, cfg.q_size), (cfg.mlp_in_size, H), (H, I)]
             if self.has_head:
                 shapes.append((self.head_v1 - self.head_v0, H))
-            floats, groups = packing.coop_workspace_need(shapes, self.DECODE_MAX_ROWS, even_n=((2 * I, H),))
+            even = () if cfg.is_gpt2 else ((2 * I, H),)
+            floats, groups = packing.coop_workspace_need(shapes, self.DECODE_MAX_ROWS, even_n=even)
             # the prefill GEMM's split-K slabs (small-M grids only) share it: <= 64 MB
             self.coop_ws = hip.CoopWorkspace(dev, slab_floats=max(floats, 1 << 24), groups=max(groups, 4096))
             self.w_scratch = None
@@ -277,12 +355,12 @@ class StageEngine:
         n = 0
         for lw in self.layers:
             for t in (lw.qkv, lw.o, lw.gate_up, lw.down, lw.ln_in, lw.ln_post, lw.qkv_s, lw.o_s, lw.gate_up_s,
-                      lw.down_s):
+                      lw.down_s, lw.ln_in_b, lw.ln_post_b, lw.qkv_b, lw.o_b, lw.gate_up_b, lw.down_b):
                 if t is not None:
                     n += t.numel() * t.element_size()
             if lw.raw is not None:
                 n += sum(t.numel() * t.element_size() for t in lw.raw.values())
-        for t in (self.embed_w, self.final_norm, self.lm_head):
+        for t in (self.embed_w, self.final_norm, self.lm_head, self.pos_emb, self.final_norm_b, self.lm_head_s):
             if t is not None:
                 n += t.numel() * t.element_size()
         n += sum(t.numel() * t.element_size() for t in self.k_cache + self.v_cache)
@@ -339,7 +417,7 @@ class StageEngine:
             rows_idx = list(range(h.shape[0]))
         if self.gpu:
             from ..ops import hip
-            if (self.head_v0, self.head_v1) != (0, self.cfg.vocab_size):
+            if (self.head_v0, self.head_v1) != (0, self.cfg.head_rows):
                 raise RuntimeError("head(): this stage holds only part of the lm_head (use head_keys)")
             keys = self.head_keys(h, rows_idx)
             n = keys.numel()
@@ -377,10 +455,20 @@ class StageEngine:
         return keys
 
     def head_gemv(self, h: torch.Tensor, rows: int, keys: torch.Tensor, a_rows=None) -> None:
-        """Fused final RMSNorm + lm_head slice + argmax keys (atomicMax into ``keys``)."""
+        """Fused final RMSNorm + lm_head slice + argmax keys (atomicMax into ``keys``).
+        GPT-2: ln_f (LayerNorm kernel, rows gathered first) then the plain GEMV + argmax."""
         from ..ops import hip
         ep = hip.make_epi(keys=keys, col_offset=self.head_v0)
         N, H, eps = self.head_v1 - self.head_v0, self.cfg.hidden_size, self.cfg.rms_norm_eps
+        if self.cfg.is_gpt2:
+            xn = self.buf_xn[:rows]
+            src = h if a_rows is None else h.index_select(0, a_rows.long())
+            hip.layernorm(src, xn, self.final_norm, self.final_norm_b, rows, eps)
+            if self.lm_head_s is not None:
+                hip.proj_fp8(xn, self.lm_head.view(-1), self.lm_head_s, rows, N, H, hip.EPI_ARGMAX, ep, ws=self.coop_ws)
+            else:
+                hip.gemv(xn, self.lm_head, rows, N, H, hip.EPI_ARGMAX, ep, ws=self.coop_ws)
+            return
         if self.lm_head_s is not None:
             hip.proj_fp8(h, self.lm_head.view(-1), self.lm_head_s, rows, N, H, hip.EPI_ARGMAX, ep, norm=True, eps=eps,
                          a_rows=a_rows, ws=self.coop_ws)
@@ -404,7 +492,10 @@ class StageEngine:
 
     def logits_torch(self, hs: torch.Tensor) -> torch.Tensor:
         from ..models.reference import rmsnorm
-        x = rmsnorm(hs, self.final_norm, self.cfg.rms_norm_eps)
+        if self.cfg.is_gpt2:
+            x = G2.layer_norm(hs, self.final_norm, self.final_norm_b, self.cfg.rms_norm_eps)
+        else:
+            x = rmsnorm(hs, self.final_norm, self.cfg.rms_norm_eps)
         return F.linear(x, self.lm_head.float())
 
     # ------------------------------------------------------------------------- HIP path
@@ -440,6 +531,8 @@ class StageEngine:
         q, attn_o, act, xn = self.buf_q[:rows], self.buf_attn[:rows], self.buf_act[:rows], self.buf_xn[:rows]
         ws = self.coop_ws
         native_fp8 = self.fp8 and rows <= packing.GEMV_MAX_ROWS
+        if cfg.is_gpt2:
+            return self._forward_hip_gpt2(hbuf, slot, pos, kv_len, rows, nsplit, tiles, decode, native_fp8)
 
         def wbf(w, s, N, K):  # packed bf16 weights (fp8 -> scratch for the >64-row kernels)
             return w if s is None else hip.dequant_fp8_packed(w.view(-1), s, self.w_scratch, N, K)
@@ -480,12 +573,98 @@ class StageEngine:
                 pre(act, lw.down, lw.down_s, H, I, hip.EPI_RESID, ep_o)
         return hbuf
 
+    def _forward_hip_gpt2(self, hbuf, slot, pos, kv_len, rows, nsplit, tiles, decode, native_fp8) -> torch.Tensor:
+        """GPT-2 layer on the HIP path: LayerNorm kernel (ln_1, with the wpe add fused in front
+        of layer 0) -> QKV projection + bias + KV-cache append (no RoPE) -> attention ->
+        c_proj + bias + residual -> LayerNorm (ln_2) -> c_fc + bias + GELU -> mlp.c_proj + bias
+        + residual. Decode rows use the GEMV / coop / fp8 kernels, prefill rows the MFMA GEMM."""
+        from ..ops import hip
+        cfg = self.cfg
+        H, I, eps = cfg.hidden_size, cfg.intermediate_size, cfg.rms_norm_eps
+        nh, nkv, hd = cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim
+        q, attn_o, act, xn = self.buf_q[:rows], self.buf_attn[:rows], self.buf_act[:rows], self.buf_xn[:rows]
+        ws = self.coop_ws
+
+        def proj(x, w, s, N, K, epi, ep):
+            if decode and native_fp8:
+                hip.proj_fp8(x, w.view(-1), s, rows, N, K, epi, ep, ws=ws)
+                return
+            wb = w if s is None else hip.dequant_fp8_packed(w.view(-1), s, self.w_scratch, N, K)
+            if decode:
+                hip.gemv(x, wb, rows, N, K, epi, ep, ws=ws)
+            else:
+                hip.gemm(x, wb, rows, N, K, epi, ep, ws=ws)
+
+        for li, lw in enumerate(self.layers):
+            kc, vc = self.k_cache[li], self.v_cache[li]
+            pe = self.pos_emb if (li == 0 and self.start == 0) else None
+            hip.layernorm(hbuf, xn, lw.ln_in, lw.ln_in_b, rows, eps, pos_emb=pe, pos=pos)
+            ep_qkv = hip.make_epi(out=q, k_cache=kc, v_cache=vc, slot=slot, pos=pos, ldo=q.stride(0), n_heads=nh,
+                                  n_kv=nkv, head_dim=hd, t_max=self.max_seq, bias=lw.qkv_b)
+            proj(xn, lw.qkv, lw.qkv_s, cfg.qkv_size, H, hip.EPI_QKV, ep_qkv)
+            if tiles is not None:
+                hip.attn_prefill(q, kc, vc, tiles[1], nh, nkv, hd, attn_o, causal=kv_len is None, tiles_host=tiles[0])
+            else:
+                hip.attn(q, kc, vc, slot, pos, rows, nh, nkv, hd, nsplit, self.part_o, self.part_lse, attn_o,
+                         kv_len=kv_len)
+            proj(attn_o, lw.o, lw.o_s, H, cfg.q_size, hip.EPI_RESID,
+                 hip.make_epi(out=hbuf, resid=hbuf, ldo=hbuf.stride(0), ldr=hbuf.stride(0), bias=lw.o_b))
+            hip.layernorm(hbuf, xn, lw.ln_post, lw.ln_post_b, rows, eps)
+            proj(xn, lw.gate_up, lw.gate_up_s, I, H, hip.EPI_STORE,
+                 hip.make_epi(out=act, ldo=act.stride(0), bias=lw.gate_up_b, act=hip.ACT_GELU))
+            proj(act, lw.down, lw.down_s, H, I, hip.EPI_RESID,
+                 hip.make_epi(out=hbuf, resid=hbuf, ldo=hbuf.stride(0), ldr=hbuf.stride(0), bias=lw.down_b))
+        return hbuf
+
     # ------------------------------------------------------------------------- torch path (CPU)
-    def _forward_torch(self, h, slot, pos, kv_len) -> torch.Tensor:
-        from ..models.reference import rmsnorm
+    def _attend_torch(self, q, kc, vc, slot, T) -> torch.Tensor:
+        """Per-slot causal attention over the cache (fp32). q [rows, nh, hd] -> [rows, nh*hd]."""
         cfg = self.cfg
         nh, nkv, hd = cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim
         g = nh // nkv
+        rows = q.shape[0]
+        o = torch.empty((rows, nh, hd), dtype=torch.float32, device=self.device)
+        for s_ in torch.unique(slot).tolist():
+            sel = (slot == s_).nonzero().flatten()
+            tmax = int(T[sel].max())
+            K = kc[s_, :, :tmax].float().repeat_interleave(g, dim=0)  # [nh, t, hd]
+            V = vc[s_, :, :tmax].float().repeat_interleave(g, dim=0)
+            qs = q[sel].float().transpose(0, 1)  # [nh, n, hd]
+            sc = torch.matmul(qs, K.transpose(1, 2)) * (hd ** -0.5)  # [nh, n, t]
+            mask = torch.arange(tmax, device=self.device)[None, :] >= T[sel][:, None]
+            sc = sc.masked_fill(mask[None], float("-inf"))
+            o[sel] = torch.matmul(torch.softmax(sc, dim=-1), V).transpose(0, 1)
+        return o.reshape(rows, nh * hd)
+
+    def _forward_torch_gpt2(self, h, slot, pos, kv_len) -> torch.Tensor:
+        cfg = self.cfg
+        nh, hd, eps, dt = cfg.num_attention_heads, cfg.head_dim, cfg.rms_norm_eps, self.dtype
+        rows = h.shape[0]
+        h = h.to(self.device, dt)
+        if self.start == 0:
+            h = (h.float() + self.pos_emb[pos].float()).to(dt)
+        T = (pos + 1) if kv_len is None else kv_len
+        for li, lw in enumerate(self.layers):
+            w = lw.raw
+            x = G2.layer_norm(h, w["ln1_w"], w["ln1_b"], eps).to(dt).float()
+            qkv = F.linear(x, w["qkv_w"].float(), w["qkv_b"].float())
+            q, k, v = (t.reshape(rows, nh, hd) for t in qkv.split(cfg.hidden_size, dim=-1))
+            kc, vc = self.k_cache[li], self.v_cache[li]
+            kc[slot, :, pos] = k.to(dt)
+            vc[slot, :, pos] = v.to(dt)
+            o = self._attend_torch(q.to(dt), kc, vc, slot, T).to(dt)
+            h = (h.float() + F.linear(o.float(), w["o_w"].float(), w["o_b"].float())).to(dt)
+            x = G2.layer_norm(h, w["ln2_w"], w["ln2_b"], eps).to(dt).float()
+            a = G2.gelu_new(F.linear(x, w["fc_w"].float(), w["fc_b"].float())).to(dt)
+            h = (h.float() + F.linear(a.float(), w["proj_w"].float(), w["proj_b"].float())).to(dt)
+        return h
+
+    def _forward_torch(self, h, slot, pos, kv_len) -> torch.Tensor:
+        from ..models.reference import rmsnorm
+        cfg = self.cfg
+        if cfg.is_gpt2:
+            return self._forward_torch_gpt2(h, slot, pos, kv_len)
+        nh, nkv, hd = cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim
         dt = self.dtype
         rows = h.shape[0]
         h = h.to(self.device, dt)
@@ -509,19 +688,7 @@ class StageEngine:
             kc, vc = self.k_cache[li], self.v_cache[li]
             kc[slot, :, pos] = k
             vc[slot, :, pos] = v.to(dt)
-            o = torch.empty((rows, nh, hd), dtype=torch.float32, device=self.device)
-            for s_ in torch.unique(slot).tolist():
-                sel = (slot == s_).nonzero().flatten()
-                tmax = int(T[sel].max())
-                K = kc[s_, :, :tmax].float().repeat_interleave(g, dim=0)  # [nh, t, hd]
-                V = vc[s_, :, :tmax].float().repeat_interleave(g, dim=0)
-                qs = q[sel].float().transpose(0, 1)  # [nh, n, hd]
-                sc = torch.matmul(qs, K.transpose(1, 2)) * (hd ** -0.5)  # [nh, n, t]
-                mask = torch.arange(tmax, device=self.device)[None, :] >= T[sel][:, None]
-                sc = sc.masked_fill(mask[None], float("-inf"))
-                p = torch.softmax(sc, dim=-1)
-                o[sel] = torch.matmul(p, V).transpose(0, 1)
-            o = o.reshape(rows, nh * hd).to(dt)
+            o = self._attend_torch(q, kc, vc, slot, T).to(dt)
             h = (h.float() + F.linear(o.float(), w["self_attn.o_proj.weight"].float())).to(dt)
             x = rmsnorm(h, lw.ln_post, cfg.rms_norm_eps).to(dt).float()
             a = (F.silu(F.linear(x, w["mlp.gate_proj.weight"].float())) *

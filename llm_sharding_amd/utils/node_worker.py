@@ -196,7 +196,10 @@ class NodeWorker:
         if self.end == self.layer_num:
             return eng.head(h, [b * S + S - 1 for b in range(B)]).to("cpu", torch.long)
         position_ids = torch.arange(past, past + S, dtype=torch.long)[None].expand(B, S)
-        cos, sin = full_cos_sin(eng.cos.cpu(), eng.sin.cpu(), position_ids, dtype=eng.dtype)
+        if eng.cos is None:  # GPT-2 (learned positions): keep the message schema, empty tables
+            cos = sin = torch.empty((B, S, 0), dtype=eng.dtype)
+        else:
+            cos, sin = full_cos_sin(eng.cos.cpu(), eng.sin.cpu(), position_ids, dtype=eng.dtype)
         return {"hidden_states": h.reshape(B, S, H).clone(), "cos": cos, "sin": sin}
 
     # ------------------------------------------------------------------ autoregression

@@ -310,3 +310,89 @@ def test_fp8_weights_engine():
         dg.replay()
     torch.cuda.synchronize()
     assert bool(((dg.history >= 0) & (dg.history < cfg.vocab_size)).all())
+
+
+class _CpuGenAny(RandomSource):
+    """Any family's random weights drawn on the CPU in bf16, then moved/cast (GPU and CPU
+    engines see identical values)."""
+
+    def layer(self, i, device, dtype):
+        return {k: v.to(device, dtype) for k, v in super().layer(i, "cpu", torch.bfloat16).items()}
+
+    def embedding(self, device, dtype):
+        return super().embedding("cpu", torch.bfloat16).to(device, dtype)
+
+    def final_norm(self, device, dtype):
+        return super().final_norm("cpu", torch.bfloat16).to(device, dtype)
+
+    def lm_head(self, device, dtype):
+        return super().lm_head("cpu", torch.bfloat16).to(device, dtype)
+
+    def pos_embedding(self, device, dtype):
+        t = super().pos_embedding("cpu", torch.bfloat16)
+        return None if t is None else t.to(device, dtype)
+
+    def final_norm_bias(self, device, dtype):
+        t = super().final_norm_bias("cpu", torch.bfloat16)
+        return None if t is None else t.to(device, dtype)
+
+
+@pytest.mark.parametrize("S", [6, 150])
+def test_gpt2_engine_vs_cpu_engine(S):
+    """GPT-2 small shapes (2 layers, full 50257 vocab): HIP engine (LayerNorm kernel, biased
+    GEMV/coop/GEMM epilogues, no-RoPE KV append, hd=64 attention, padded lm_head) against the
+    fp32 CPU engine on identical weights: prefill (S=150 takes the GEMM + flash path), then
+    decode steps feeding the CPU engine's tokens."""
+    from llm_sharding_amd.config import gpt2
+    cfg = gpt2()
+    cfg.num_hidden_layers = 2
+    src = _CpuGenAny(cfg, 5)
+    kw = dict(has_embed=True, has_head=True, source=src, max_slots=48, max_seq=256, max_prefill_rows=256)
+    eg = StageEngine(cfg, 0, 2, DEV, torch.bfloat16, **kw)
+    ec = StageEngine(cfg, 0, 2, "cpu", torch.float32, **kw)
+    g = torch.Generator().manual_seed(S)
+    ids = torch.randint(0, cfg.vocab_size, (S,), generator=g)
+    hs = []
+    for e, d in ((eg, DEV), (ec, "cpu")):
+        sl, po = e.prefill_rows([0], [S])
+        hs.append(e.forward(e.embed(ids.to(d)), sl, po))
+        e.advance([0], [S])
+    assert rel_err(hs[0].cpu(), hs[1]) < 3e-2
+    tok = int(ec.head(hs[1], [S - 1])[0])
+    for _ in range(4):
+        outs = []
+        for e, d in ((eg, DEV), (ec, "cpu")):
+            sl, po = e.prefill_rows([0], [1])
+            outs.append(e.forward(e.embed(torch.tensor([tok], device=d)), sl, po))
+            e.advance([0], [1])
+        assert rel_err(outs[0].cpu(), outs[1]) < 3e-2
+        lg = ec.logits_torch(outs[1])[0]
+        top2 = lg.topk(2).values
+        got, tok = int(eg.head(outs[0], [0])[0]), int(lg.argmax())
+        if (top2[0] - top2[1]).item() > 0.05 * lg.abs().max().item():
+            assert got == tok
+    assert tok < cfg.vocab_size
+    # 40-row decode batch (coop kernels) + hipGraph replay with valid (unpadded) token ids
+    for s_ in range(1, 40):
+        eg.seq_len[s_] = 3
+    dg = DecodeGraph(eg, 40, "full", slots=list(range(40)), history_len=3).capture()
+    for _ in range(3):
+        dg.replay()
+    torch.cuda.synchronize()
+    assert bool(((dg.history >= 0) & (dg.history < cfg.vocab_size)).all())
+
+
+def test_gpt2_fp8_engine():
+    from llm_sharding_amd.config import gpt2
+    cfg = gpt2()
+    cfg.num_hidden_layers = 2
+    src = _CpuGenAny(cfg, 9)
+    kw = dict(has_embed=True, has_head=True, source=src, max_slots=8, max_seq=128, max_prefill_rows=256)
+    e16 = StageEngine(cfg, 0, 2, DEV, torch.bfloat16, **kw)
+    e8 = StageEngine(cfg, 0, 2, DEV, torch.bfloat16, weight_dtype="fp8", **kw)
+    ids = torch.randint(0, cfg.vocab_size, (20,), generator=torch.Generator().manual_seed(0))
+    hs = []
+    for e in (e16, e8):
+        sl, po = e.prefill_rows([0], [20])
+        hs.append(e.forward(e.embed(ids.to(DEV)), sl, po).clone())
+    assert rel_err(hs[1], hs[0]) < 0.15

@@ -467,3 +467,86 @@ def test_gemv_coop_fp8_every_config(cfg):
             h.proj_fp8(x, wq, sc, M, N, K, h.EPI_RESID, h.make_epi(out=out, resid=out, ldo=N, ldr=N), norm=True,
                        algo=("coop_fp8", c))
             assert rel_err(out, ref) < 8e-3, (cfg, K, c)
+
+
+# ----------------------------------------------------------------------------- GPT-2 paths
+@pytest.mark.parametrize("rows,H", [(1, 768), (7, 768), (130, 1024), (3, 1600)])
+@pytest.mark.parametrize("with_pos", [False, True])
+def test_layernorm(rows, H, with_pos):
+    """lsa_layernorm (+ fused learned-position add) vs torch fp32 LayerNorm."""
+    h = hip()
+    x = _rnd(rows, H, scale=3.0) + 0.5
+    w, b = _rnd(H, scale=0.2) + 1.0, _rnd(H, scale=0.2)
+    pe = _rnd(64, H, scale=0.3) if with_pos else None
+    pos = torch.randint(0, 64, (rows,), device=DEV, dtype=torch.int32)
+    xin = x.clone()
+    out = torch.empty(rows, H, dtype=torch.bfloat16, device=DEV)
+    h.layernorm(x, out, w, b, rows, 1e-5, pos_emb=pe, pos=pos if with_pos else None)
+    xr = (xin.float() + pe[pos.long()].float()).to(torch.bfloat16) if with_pos else xin
+    assert torch.equal(x, xr)  # position add written back (bf16-rounded)
+    ref = F.layer_norm(xr.float(), (H,), w.float(), b.float(), 1e-5)
+    assert rel_err(out, ref) < 8e-3
+
+
+def _proj(h, x, w_bf, wq, sc, rows, N, K, epi, ep, fp8, ws):
+    """The engine's dispatch: decode rows -> gemv/coop (fp8: native kernels), else GEMM."""
+    if rows <= 128:
+        if fp8:
+            h.proj_fp8(x, wq, sc, rows, N, K, epi, ep, ws=ws)
+        else:
+            h.gemv(x, w_bf, rows, N, K, epi, ep, ws=ws)
+    else:
+        h.gemm(x, w_bf, rows, N, K, epi, ep, ws=ws)
+
+
+@pytest.mark.parametrize("rows", [1, 9, 40, 100, 200])
+@pytest.mark.parametrize("fp8", [False, True])
+def test_bias_gelu_and_norope_qkv_epilogues(rows, fp8):
+    """GPT-2 epilogues on every projection kernel: bias + tanh-GELU store, bias + residual, and
+    QKV with bias and no RoPE (natural q|k|v order) into the static KV cache."""
+    h = hip()
+    ws = h.CoopWorkspace(DEV, slab_floats=1 << 24, groups=1 << 14)
+    H, I, nh, hd, T = 768, 3072, 12, 64, 256
+    x = _rnd(rows, H)
+
+    def weights(N, K):
+        w = _rnd(N, K, scale=K ** -0.5)
+        if fp8:
+            q, sc = packing.quantize_fp8_rows(w)
+            wd = packing.dequantize_fp8_rows(q, sc)
+            return wd, packing.pack_b(wd.to(torch.bfloat16)), packing.pack_b_fp8(q).view(-1), sc
+        return w, packing.pack_b(w), None, None
+
+    # c_fc + bias + GELU
+    wf, wfb, wfq, sf = weights(I, H)
+    bias = torch.randn(I, device=DEV) * 0.5
+    act = torch.zeros(rows, I, dtype=torch.bfloat16, device=DEV)
+    _proj(h, x, wfb, wfq, sf, rows, I, H, h.EPI_STORE,
+          h.make_epi(out=act, ldo=I, bias=bias, act=h.ACT_GELU), fp8, ws)
+    z = x.float() @ wf.float().T + bias
+    ref = 0.5 * z * (1 + torch.tanh(0.7978845608028654 * (z + 0.044715 * z ** 3)))
+    assert rel_err(act, ref) < 1e-2
+    # mlp.c_proj + bias + residual
+    wp, wpb, wpq, sp = weights(H, I)
+    bias2 = torch.randn(H, device=DEV) * 0.5
+    res = _rnd(rows, H)
+    out = res.clone()
+    _proj(h, act, wpb, wpq, sp, rows, H, I, h.EPI_RESID,
+          h.make_epi(out=out, resid=out, ldo=H, ldr=H, bias=bias2), fp8, ws)
+    assert rel_err(out, res.float() + act.float() @ wp.float().T + bias2) < 1e-2
+    # c_attn + bias, no RoPE
+    wq_, wqb, wqq, sq = weights(3 * H, H)
+    bq = torch.randn(3 * H, device=DEV) * 0.5
+    kc = torch.zeros(rows, nh, T, hd, dtype=torch.bfloat16, device=DEV)
+    vc = torch.zeros_like(kc)
+    q = torch.zeros(rows, H, dtype=torch.bfloat16, device=DEV)
+    slot = torch.arange(rows, dtype=torch.int32, device=DEV)
+    pos = torch.randint(0, T, (rows,), dtype=torch.int32, device=DEV)
+    _proj(h, x, wqb, wqq, sq, rows, 3 * H, H, h.EPI_QKV,
+          h.make_epi(out=q, k_cache=kc, v_cache=vc, slot=slot, pos=pos, ldo=H, n_heads=nh, n_kv=nh,
+                     head_dim=hd, t_max=T, bias=bq), fp8, ws)
+    z = x.float() @ wq_.float().T + bq
+    assert rel_err(q, z[:, :H]) < 1e-2
+    r = torch.arange(rows, device=DEV)
+    assert rel_err(kc[r, :, pos.long()], z[:, H:2 * H].view(rows, nh, hd)) < 1e-2
+    assert rel_err(vc[r, :, pos.long()], z[:, 2 * H:].view(rows, nh, hd)) < 1e-2
