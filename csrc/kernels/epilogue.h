@@ -55,14 +55,14 @@ LSA_DEVICE float epi_act(const EpiArgs& ep, float v) { return ep.act == 1 ? gelu
 //   tile tt (16 columns): columns 0..7 -> dims 8tt..8tt+7, columns 8..15 -> dims hd/2+8tt..
 // so a rotate_half partner pair always lives in one 16-wide tile (see ops/packing.py).
 LSA_DEVICE void epi_qkv_store(const EpiArgs& ep, int m, int n, float v, float vp) {
-  const int hd = ep.head_dim;
-  const int qs = ep.n_heads * hd, ks = ep.n_kv * hd;
+  const int hd = ep.head_dim, sh = __builtin_ctz((unsigned)hd);  // power of two (host-checked)
+  const int qs = ep.n_heads << sh, ks = ep.n_kv << sh;
   const int p = ep.pos[m];
   if (p < 0 || p >= ep.t_max) return;  // never write outside the static cache
   if (ep.cos_t == nullptr) {  // no RoPE: natural column order [q | k | v]
     const int isk = n >= qs, isv = n >= qs + ks;
     const int c0 = n - (isv ? qs + ks : (isk ? qs : 0));
-    const int head = c0 / hd, dim = c0 - head * hd;
+    const int head = c0 >> sh, dim = c0 & (hd - 1);
     if (!isk) {
       ep.out[(size_t)m * ep.ldo + c0] = f2bf(v);
     } else {
@@ -74,7 +74,7 @@ LSA_DEVICE void epi_qkv_store(const EpiArgs& ep, int m, int n, float v, float vp
   if (n < qs + ks) {
     const bool isq = n < qs;
     const int c0 = isq ? n : n - qs;
-    const int head = c0 / hd, c = c0 - head * hd;
+    const int head = c0 >> sh, c = c0 & (hd - 1);
     const int tt = c >> 4, cc = c & 15;
     const int half = hd >> 1;
     const int fi = 8 * tt + (cc & 7);
@@ -90,8 +90,98 @@ LSA_DEVICE void epi_qkv_store(const EpiArgs& ep, int m, int n, float v, float vp
     }
   } else {
     const int c0 = n - qs - ks;
-    const int head = c0 / hd, dim = c0 - head * hd;
+    const int head = c0 >> sh, dim = c0 & (hd - 1);
     const size_t base = ((size_t)ep.slot[m] * ep.n_kv + head) * ep.t_max + p;
     ep.v_cache[base * hd + dim] = f2bf(v);
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Vectorised epilogue of one finished 16-column tile row: v[j] = C[m][c0 + j], c0 % 16 == 0
+// (packed column order). One thread per (tile, row) instead of one per element: 16-B stores,
+// 16-B residual / bias / cos / sin loads, the index math (shifts: head_dim is a power of two)
+// done once per 16 outputs. EPI_SWIGLU and EPI_ARGMAX are handled by the callers.
+LSA_DEVICE void epi_qkv_row16(const EpiArgs& ep, int m, int c0, const float* v) {
+  const int hd = ep.head_dim, sh = __builtin_ctz((unsigned)hd);
+  const int qs = ep.n_heads << sh, ks = ep.n_kv << sh;
+  const int p = ep.pos[m];
+  if (p < 0 || p >= ep.t_max) return;  // never write outside the static cache
+  const int sec = c0 < qs ? 0 : (c0 < qs + ks ? 1 : 2);
+  const int cs0 = c0 - (sec == 0 ? 0 : (sec == 1 ? qs : qs + ks));
+  const int head = cs0 >> sh, c = cs0 & (hd - 1);
+  bf16_raw* dst = sec == 0 ? ep.out + (size_t)m * ep.ldo + ((size_t)head << sh)
+                           : (sec == 1 ? ep.k_cache : ep.v_cache) +
+                                 ((((size_t)ep.slot[m] * ep.n_kv + head) * ep.t_max + p) << sh);
+  if (ep.cos_t == nullptr || sec == 2) {  // v (or no RoPE): natural order, 16 contiguous dims
+    st16(dst + c, pack8(v));
+    st16(dst + c + 8, pack8(v + 8));
+    return;
+  }
+  // rotate_half pairs live in this tile: columns 0..7 -> dims 8tt+j, 8..15 -> hd/2 + 8tt + j
+  const int half = hd >> 1, fi0 = (c >> 4) * 8;
+  const float* ct = ep.cos_t + (size_t)p * half + fi0;
+  const float* stb = ep.sin_t + (size_t)p * half + fi0;
+  float cs[8], sn[8], lo[8], hi[8];
+  *reinterpret_cast<f32x4_t*>(cs) = *reinterpret_cast<const f32x4_t*>(ct);
+  *reinterpret_cast<f32x4_t*>(cs + 4) = *reinterpret_cast<const f32x4_t*>(ct + 4);
+  *reinterpret_cast<f32x4_t*>(sn) = *reinterpret_cast<const f32x4_t*>(stb);
+  *reinterpret_cast<f32x4_t*>(sn + 4) = *reinterpret_cast<const f32x4_t*>(stb + 4);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    lo[j] = v[j] * cs[j] - v[j + 8] * sn[j];
+    hi[j] = v[j + 8] * cs[j] + v[j] * sn[j];
+  }
+  st16(dst + fi0, pack8(lo));
+  st16(dst + half + fi0, pack8(hi));
+}
+
+// Adds the bias (if any) to v in place.
+LSA_DEVICE void epi_bias16(const EpiArgs& ep, int c0, float* v) {
+  if (!ep.bias) return;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const f32x4_t b = *reinterpret_cast<const f32x4_t*>(ep.bias + c0 + 4 * q);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[4 * q + j] += b[j];
+  }
+}
+
+template <int EPI>
+LSA_DEVICE void epi_row16(const EpiArgs& ep, int m, int c0, float* v) {
+  epi_bias16(ep, c0, v);
+  if (EPI == EPI_QKV) {
+    epi_qkv_row16(ep, m, c0, v);
+  } else if (EPI == EPI_STORE) {
+    if (ep.act == 1) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v[j] = gelu_tanh(v[j]);
+    }
+    bf16_raw* o = ep.out + (size_t)m * ep.ldo + c0;
+    st16(o, pack8(v));
+    st16(o + 8, pack8(v + 8));
+  } else if (EPI == EPI_RESID) {
+    const bf16_raw* rr = ep.resid + (size_t)m * ep.ldr + c0;
+    float a[8], b[8];
+    unpack8(ld16(rr), a);
+    unpack8(ld16(rr + 8), b);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      a[j] += v[j];
+      b[j] += v[j + 8];
+    }
+    bf16_raw* o = ep.out + (size_t)m * ep.ldo + c0;
+    st16(o, pack8(a));
+    st16(o + 8, pack8(b));
+  }
+}
+
+// Largest argmax key of a 16-column tile row (bias added by epi_bias16 first).
+LSA_DEVICE unsigned long long argmax_key16(const float* v, unsigned idx0) {
+  unsigned long long k = 0ull;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const unsigned long long kj = argmax_key(v[j], idx0 + j);
+    k = kj > k ? kj : k;
+  }
+  return k;
 }

@@ -299,31 +299,55 @@ __global__ __launch_bounds__(NW * 64) void gemv_coop_kernel(
 
   auto rstd = [&](int mm) -> float { return NORM ? rsqrtf(s_ss[mm] / (float)K + eps) : 1.f; };
   const int ntg0 = g * TG;
-  auto wsc = [&](int col) -> float { return FP8 ? wscale[col] : 1.f; };
+  auto load16 = [&](int t, int mm, float r, float* v) {  // row-rotated quads (LDS banks)
+    const float* rp = red + (t * MR + mm) * 16;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int qq = (q + mm) & 3;
+      const f32x4_t x4 = *reinterpret_cast<const f32x4_t*>(rp + 4 * qq);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[4 * qq + j] = x4[j] * r;
+    }
+    if (FP8) {
+      const float* sp = wscale + (ntg0 + t) * 16;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4_t s4 = *reinterpret_cast<const f32x4_t*>(sp + 4 * q);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[4 * q + j] *= s4[j];
+      }
+    }
+  };
   if (EPI == EPI_SWIGLU) {
-    for (int e = tid; e < (TG / 2) * MR * 16; e += NTHR) {
-      const int tp = e / (MR * 16), mm = (e >> 4) % MR, n = e & 15;
+    // gate tile 2tp / up tile 2tp+1 -> 16 outputs per thread, two 16-B stores
+    for (int e = tid; e < (TG / 2) * MR; e += NTHR) {
+      const int tp = e / MR, mm = e % MR;
       if (mm >= M) continue;
       const float r = rstd(mm);
-      const float gg = red[((2 * tp) * MR + mm) * 16 + n] * r * wsc((ntg0 + 2 * tp) * 16 + n);
-      const float uu = red[((2 * tp + 1) * MR + mm) * 16 + n] * r * wsc((ntg0 + 2 * tp + 1) * 16 + n);
-      ep.out[(size_t)mm * ep.ldo + (ntg0 / 2 + tp) * 16 + n] = f2bf(silu(gg) * uu);
+      float gg[16], uu[16];
+      load16(2 * tp, mm, r, gg);
+      load16(2 * tp + 1, mm, r, uu);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) gg[j] = silu(gg[j]) * uu[j];
+      bf16_raw* o = ep.out + (size_t)mm * ep.ldo + (ntg0 / 2 + tp) * 16;
+      st16(o, pack8(gg));
+      st16(o + 8, pack8(gg + 8));
     }
   } else {
-    for (int e = tid; e < TG * MR * 16; e += NTHR) {
-      const int t = e / (MR * 16), mm = (e >> 4) % MR, n = e & 15;
+    // one thread per finished 16-column tile row (epilogue.h epi_row16); the 4 quad reads
+    // start at a row-rotated quad so neighbouring lanes hit different LDS banks
+    for (int e = tid; e < TG * MR; e += NTHR) {
+      const int t = e / MR, mm = e % MR;
       if (mm >= M) continue;
       const float r = rstd(mm);
-      const int col = (ntg0 + t) * 16 + n;
-      const float v = red[(t * MR + mm) * 16 + n] * r * wsc(col);
-      if (EPI == EPI_STORE) {
-        ep.out[(size_t)mm * ep.ldo + col] = f2bf(epi_act(ep, v + epi_bias(ep, col)));
-      } else if (EPI == EPI_RESID) {
-        ep.out[(size_t)mm * ep.ldo + col] = f2bf(bf2f(ep.resid[(size_t)mm * ep.ldr + col]) + v + epi_bias(ep, col));
-      } else if (EPI == EPI_QKV) {
-        epi_qkv_store(ep, mm, col, v + epi_bias(ep, col), red[(t * MR + mm) * 16 + (n ^ 8)] * r * wsc(col ^ 8) + epi_bias(ep, col ^ 8));
-      } else if (EPI == EPI_ARGMAX) {
-        atomicMax(&s_key[mm], argmax_key(v + epi_bias(ep, col), (unsigned)(col + ep.col_offset)));
+      const int c0 = (ntg0 + t) * 16;
+      float v[16];
+      load16(t, mm, r, v);
+      if (EPI == EPI_ARGMAX) {
+        epi_bias16(ep, c0, v);
+        atomicMax(&s_key[mm], argmax_key16(v, (unsigned)(c0 + ep.col_offset)));
+      } else {
+        epi_row16<EPI>(ep, mm, c0, v);
       }
     }
     if (EPI == EPI_ARGMAX) {

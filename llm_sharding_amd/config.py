@@ -70,9 +70,10 @@ class LlamaConfig:
 
     @property
     def head_rows(self) -> int:
-        """lm_head rows as served: the vocabulary padded to the 16-column MFMA tile (GPT-2's
-        50257 -> 50272; padding rows copy row 0, so they can never win the argmax tie-break)."""
-        return -(-self.vocab_size // 16) * 16
+        """lm_head rows as served: the vocabulary padded to whole 128-column groups (8 MFMA
+        tiles, so every GEMV / coop tiling applies; GPT-2's 50257 -> 50304; Llama vocabularies
+        are already multiples). Padding rows copy row 0, so they never win the argmax tie-break."""
+        return -(-self.vocab_size // 128) * 128
 
     @property
     def gqa_group(self) -> int:
@@ -100,8 +101,8 @@ class LlamaConfig:
     def validate(self) -> None:
         if self.num_attention_heads % self.num_key_value_heads:
             raise ValueError("num_attention_heads must be a multiple of num_key_value_heads")
-        if self.head_dim % 16:
-            raise ValueError("head_dim must be a multiple of 16")
+        if self.head_dim % 16 or self.head_dim & (self.head_dim - 1):
+            raise ValueError("head_dim must be a power of two >= 16")
 
     # ------------------------------------------------------------------ IO
     @classmethod

@@ -105,6 +105,11 @@ def make_epi(out=None, resid=None, k_cache=None, v_cache=None, slot=None, pos=No
     column order); ``cos=None`` with EPI_QKV: no RoPE, natural q|k|v column order."""
     if bias is not None:
         _req(bias.dtype == torch.float32 and bias.is_contiguous(), "epilogue bias: contiguous fp32")
+    # vectorised epilogues store 16-B runs: rows must start 16-B aligned
+    _req(ldo % 8 == 0 and ldr % 8 == 0, f"epilogue: ldo/ldr ({ldo}, {ldr}) must be multiples of 8")
+    for t in (out, resid, bias):
+        _req(t is None or t.data_ptr() % 16 == 0, "epilogue: out/resid/bias must be 16-byte aligned")
+    _req(head_dim == 0 or (head_dim & (head_dim - 1)) == 0, f"epilogue: head_dim {head_dim} not a power of two")
     return EpiArgs(_p(out), _p(resid), _p(k_cache), _p(v_cache), _p(slot), _p(pos), _p(cos), _p(sin),
                    _p(keys), _p(bias), ldo, ldr, n_heads, n_kv, head_dim, t_max, col_offset, int(act))
 

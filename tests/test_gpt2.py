@@ -79,7 +79,7 @@ def test_config_maps_hf_keys(hf):
     _, shards = hf
     cfg = LlamaConfig.from_pretrained(shards)
     assert cfg.is_gpt2 and cfg.hidden_size == 128 and cfg.num_hidden_layers == 3 and cfg.head_dim == 32
-    assert cfg.intermediate_size == 512 and cfg.vocab_size == 300 and cfg.head_rows == 304
+    assert cfg.intermediate_size == 512 and cfg.vocab_size == 300 and cfg.head_rows == 384
 
 
 def test_shard_format_matches_reference_layout(hf):

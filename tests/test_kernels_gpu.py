@@ -232,7 +232,9 @@ def test_gemv_argmax_with_rows(M):
     # logit to be within tolerance of the max and most picks to be exact.
     chosen = logits.gather(1, tok.long()[:, None])[:, 0]
     assert torch.all(logits.max(-1).values - chosen < 2e-2 * logits.abs().max())
-    assert (tok.long() == want).float().mean() >= 0.9
+    top2 = logits.topk(2, dim=-1).values
+    clear = (top2[:, 0] - top2[:, 1]) > 2e-2 * logits.abs().max()
+    assert torch.all((tok.long() == want)[clear])  # exact wherever the top-2 margin is clear
     assert torch.all(keys == 0)  # finalize resets the keys
 
 
