@@ -31,15 +31,37 @@ from .scheduler import plan_stages
 
 
 class DistP2P:
-    """Point-to-point over torch.distributed (RCCL on GPUs, gloo on CPU)."""
+    """Point-to-point over torch.distributed (RCCL on GPUs, gloo on CPU), with one process group
+    - i.e. one RCCL communicator and one communication stream - per directed ring edge
+    ``r -> r+1`` (the back-edge ``N-1 -> 0`` included).
+
+    Why: RCCL executes the p2p ops of a communicator in issue order on one stream, and an
+    ``ncclSend`` may wait for its matching ``ncclRecv`` to be running. On a single shared
+    communicator stage 0's stream holds ``send(mb1 -> 1)`` ahead of ``recv(back-edge mb0)``
+    while the last stage's holds ``send(back-edge mb0)`` ahead of ``recv(mb1)``: a cycle that
+    only the transport's eager buffering breaks (small messages), not the API contract. With a
+    communicator per edge each stream carries one direction in FIFO order, so the pipeline's
+    dataflow order alone guarantees progress, and sends / receives on different edges overlap.
+    Must be constructed on every rank at the same point (``new_group`` is collective)."""
+
+    def __init__(self):
+        import torch.distributed as dist
+        self.groups = {}
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            n = dist.get_world_size()
+            for r in range(n):
+                self.groups[(r, (r + 1) % n)] = dist.new_group([r, (r + 1) % n])
+
+    def _group(self, src: int, dst: int):
+        return self.groups.get((src, dst))  # non-ring edges (none in the pipeline): default group
 
     def isend(self, t: torch.Tensor, dst: int):
         import torch.distributed as dist
-        return dist.isend(t, dst)
+        return dist.isend(t, dst, group=self._group(dist.get_rank(), dst))
 
     def recv(self, t: torch.Tensor, src: int) -> None:
         import torch.distributed as dist
-        dist.irecv(t, src).wait()
+        dist.irecv(t, src, group=self._group(src, dist.get_rank())).wait()
 
 
 class LocalP2P:
