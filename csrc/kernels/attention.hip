@@ -13,7 +13,12 @@
 //                     kv_len array is given (the reference's unmasked prefill, Q1).
 //                     The split count is fixed per launch (graph-capturable); the chunk is
 //                     derived on-device from the current length, so empty splits exit.
-//  attn_combine_kernel merges the per-split (o, lse) partials -> bf16 [rows][n_heads*HD].
+//                     With nsplit > 1 every split publishes its (o, lse) partials with
+//                     write-through (sc1) stores and takes an agent-scope arrival ticket per
+//                     (row, kv-head); the last-arriving split merges all partials in split
+//                     order (deterministic) and writes bf16 [rows][n_heads*HD] - no separate
+//                     combine launch (cdna_hip_programming.md §5 'In-launch split-K reduction',
+//                     sc1 form). The last arriver resets its counter: graph-replay safe.
 #include "common.h"
 
 namespace {
@@ -21,6 +26,7 @@ namespace {
 constexpr int ATT_WAVES = 4;
 constexpr int ATT_THR = ATT_WAVES * LSA_WAVE;
 constexpr float NEG_BIG = -1e30f;
+constexpr int ATT_MAX_SPLIT = 16;  // split-KV factor limit (the merge keeps one lse per split in VGPRs)
 
 template <int HD, int G>
 __global__ __launch_bounds__(ATT_THR) void attn_split_kernel(
@@ -28,7 +34,7 @@ __global__ __launch_bounds__(ATT_THR) void attn_split_kernel(
     const bf16_raw* __restrict__ vc, const int* __restrict__ slot, const int* __restrict__ pos,
     const int* __restrict__ kv_len, int n_heads, int n_kv, int t_max, float scale_log2,
     int nsplit, int min_chunk, float* __restrict__ part_o, float* __restrict__ part_lse,
-    bf16_raw* __restrict__ out, int ldo) {
+    bf16_raw* __restrict__ out, int ldo, unsigned* __restrict__ counters) {
   constexpr int LPK = HD / 8;          // lanes per key row (8 bf16 = 16 B per lane)
   constexpr int KPW = LSA_WAVE / LPK;  // keys per wave-instruction
   constexpr int KPI = KPW * ATT_WAVES; // keys per workgroup iteration
@@ -37,6 +43,7 @@ __global__ __launch_bounds__(ATT_THR) void attn_split_kernel(
   __shared__ float s_m[ATT_WAVES][G];
   __shared__ float s_l[ATT_WAVES][G];
   __shared__ float s_o[ATT_WAVES][G][HD];
+  __shared__ int s_last;
 
   const int split = blockIdx.x, kvh = blockIdx.y, row = blockIdx.z;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -49,11 +56,53 @@ __global__ __launch_bounds__(ATT_THR) void attn_split_kernel(
   chunk = (chunk + KPI - 1) / KPI * KPI;
   const int k0 = split * chunk;
   const int k1 = min(T, k0 + chunk);
+  // every split derives the same number of non-empty splits from T: empty ones exit at once
+  // (no ticket), and a lone active split writes the final output itself (no merge)
+  const int nact = (T + chunk - 1) / chunk;
+  if (k0 >= k1) return;
   const size_t pbase = ((size_t)row * n_heads + (size_t)kvh * G) * nsplit + split;
-  if (k0 >= k1) {
-    if (tid < G) part_lse[pbase + (size_t)tid * nsplit] = -INFINITY;
-    return;
-  }
+  const __amdgpu_buffer_rsrc_t por = __builtin_amdgcn_make_buffer_rsrc(part_o, (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t plr = __builtin_amdgcn_make_buffer_rsrc(part_lse, (short)0, 0x7fffffff, 0x00020000);
+  const size_t pbase0 = pbase - split;  // split 0 of head 0 of this group
+  // last-arriver merge of the nsplit partials of this (row, kv-head) group (sc1 loads)
+  auto combine = [&]() {
+    for (int e = tid; e < G * HD; e += ATT_THR) {
+      const int r = e / HD, d = e - r * HD;
+      const int hb = (int)(pbase0 + (size_t)r * nsplit);  // index of split 0 of head r
+      float lse[ATT_MAX_SPLIT];
+      float mm = -INFINITY;
+#pragma unroll
+      for (int sp = 0; sp < ATT_MAX_SPLIT; ++sp) {
+        lse[sp] = sp < nact ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(plr, (hb + sp) * 4, 0, 16))
+                            : -INFINITY;
+        mm = fmaxf(mm, lse[sp]);
+      }
+      float ws = 0.f, acc = 0.f;
+#pragma unroll
+      for (int sp = 0; sp < ATT_MAX_SPLIT; ++sp) {
+        if (sp < nact) {
+          const float wgt = exp2f(lse[sp] - mm);
+          ws += wgt;
+          acc += wgt * __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(por, ((hb + sp) * HD + d) * 4, 0, 16));
+        }
+      }
+      out[(size_t)row * ldo + (size_t)(kvh * G + r) * HD + d] = f2bf(acc / ws);
+    }
+  };
+  // publish (every storing wave drained), take the ticket, merge if last
+  auto arrive = [&]() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    unsigned* cnt = counters + (size_t)row * n_kv + kvh;
+    if (tid == 0) {
+      const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = old == (unsigned)(nact - 1);
+    }
+    __syncthreads();
+    if (!s_last) return;
+    combine();
+    if (tid == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
 
   float qf[G][8];
 #pragma unroll
@@ -165,44 +214,25 @@ __global__ __launch_bounds__(ATT_THR) void attn_split_kernel(
       ls += s_l[i][r] * a;
       os += s_o[i][r][d] * a;
     }
-    if (nsplit == 1) {  // single split: final output directly, no combine launch
+    if (nact == 1) {  // lone active split: final output directly, no merge
       out[(size_t)row * ldo + (size_t)(kvh * G + r) * HD + d] = f2bf(os / ls);
     } else {
-      const size_t pi = pbase + (size_t)r * nsplit;
-      part_o[pi * HD + d] = os / ls;
-      if (d == 0) part_lse[pi] = mm + log2f(ls);
+      const int pi = (int)(pbase + (size_t)r * nsplit);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(os / ls), por, (pi * HD + d) * 4, 0, 16 /* sc1 */);
+      if (d == 0) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(mm + log2f(ls)), plr, pi * 4, 0, 16);
     }
   }
-}
-
-template <int HD>
-__global__ __launch_bounds__(HD) void attn_combine_kernel(const float* __restrict__ part_o,
-                                                          const float* __restrict__ part_lse,
-                                                          int n_heads, int nsplit,
-                                                          bf16_raw* __restrict__ out, int ldo) {
-  const int h = blockIdx.x, row = blockIdx.y, d = threadIdx.x;
-  const size_t pb = ((size_t)row * n_heads + h) * nsplit;
-  float mm = -INFINITY;
-  for (int s = 0; s < nsplit; ++s) mm = fmaxf(mm, part_lse[pb + s]);
-  float ws = 0.f, acc = 0.f;
-  for (int s = 0; s < nsplit; ++s) {
-    const float lse = part_lse[pb + s];
-    if (lse == -INFINITY) continue;
-    const float wgt = exp2f(lse - mm);
-    ws += wgt;
-    acc += wgt * part_o[(pb + s) * HD + d];
-  }
-  out[(size_t)row * ldo + (size_t)h * HD + d] = f2bf(acc / ws);
+  if (nact > 1) arrive();
 }
 
 template <int HD, int G>
 int launch_split(const bf16_raw* q, int ldq, const bf16_raw* kc, const bf16_raw* vc, const int* slot,
                  const int* pos, const int* kv_len, int rows, int n_heads, int n_kv, int t_max,
                  float scale_log2, int nsplit, int min_chunk, float* po, float* pl, bf16_raw* out,
-                 int ldo, hipStream_t s) {
+                 int ldo, unsigned* cnt, hipStream_t s) {
   dim3 grid(nsplit, n_kv, rows);
   attn_split_kernel<HD, G><<<grid, ATT_THR, 0, s>>>(q, ldq, kc, vc, slot, pos, kv_len, n_heads, n_kv,
-                                                     t_max, scale_log2, nsplit, min_chunk, po, pl, out, ldo);
+                                                     t_max, scale_log2, nsplit, min_chunk, po, pl, out, ldo, cnt);
   LSA_CHECK_LAUNCH();
   return LSA_OK;
 }
@@ -211,9 +241,9 @@ template <int HD>
 int dispatch_g(int g, const bf16_raw* q, int ldq, const bf16_raw* kc, const bf16_raw* vc,
                const int* slot, const int* pos, const int* kv_len, int rows, int n_heads, int n_kv,
                int t_max, float sl2, int nsplit, int min_chunk, float* po, float* pl, bf16_raw* out,
-               int ldo, hipStream_t s) {
+               int ldo, unsigned* cnt, hipStream_t s) {
 #define LSA_G(GG) \
-  case GG: return launch_split<HD, GG>(q, ldq, kc, vc, slot, pos, kv_len, rows, n_heads, n_kv, t_max, sl2, nsplit, min_chunk, po, pl, out, ldo, s);
+  case GG: return launch_split<HD, GG>(q, ldq, kc, vc, slot, pos, kv_len, rows, n_heads, n_kv, t_max, sl2, nsplit, min_chunk, po, pl, out, ldo, cnt, s);
   switch (g) {
     LSA_G(1) LSA_G(2) LSA_G(3) LSA_G(4) LSA_G(6) LSA_G(8)
     default: return LSA_UNSUPPORTED;
@@ -227,8 +257,10 @@ extern "C" int lsa_attn_decode(const void* q, int ldq, const void* k_cache, cons
                                const int* slot, const int* pos, const int* kv_len, int rows,
                                int n_heads, int n_kv, int head_dim, int t_max, float scale,
                                int nsplit, int min_chunk, float* part_o, float* part_lse,
-                               void* out, int ldo, hipStream_t stream) {
-  if (rows < 1 || n_heads % n_kv || nsplit < 1 || min_chunk < 1) return LSA_BAD_SHAPE;
+                               void* out, int ldo, unsigned* counters, hipStream_t stream) {
+  // counters: rows * n_kv zero-initialised uint32 (only read when nsplit > 1; left zeroed)
+  if (rows < 1 || n_heads % n_kv || nsplit < 1 || nsplit > ATT_MAX_SPLIT || min_chunk < 1) return LSA_BAD_SHAPE;
+  if (nsplit > 1 && !counters) return LSA_BAD_SHAPE;
   const int g = n_heads / n_kv;
   const float sl2 = scale * 1.4426950408889634f;
   const bf16_raw* qq = static_cast<const bf16_raw*>(q);
@@ -237,17 +269,10 @@ extern "C" int lsa_attn_decode(const void* q, int ldq, const void* k_cache, cons
   bf16_raw* o = static_cast<bf16_raw*>(out);
   int rc;
   if (head_dim == 128)
-    rc = dispatch_g<128>(g, qq, ldq, kc, vc, slot, pos, kv_len, rows, n_heads, n_kv, t_max, sl2, nsplit, min_chunk, part_o, part_lse, o, ldo, stream);
+    rc = dispatch_g<128>(g, qq, ldq, kc, vc, slot, pos, kv_len, rows, n_heads, n_kv, t_max, sl2, nsplit, min_chunk, part_o, part_lse, o, ldo, counters, stream);
   else if (head_dim == 64)
-    rc = dispatch_g<64>(g, qq, ldq, kc, vc, slot, pos, kv_len, rows, n_heads, n_kv, t_max, sl2, nsplit, min_chunk, part_o, part_lse, o, ldo, stream);
+    rc = dispatch_g<64>(g, qq, ldq, kc, vc, slot, pos, kv_len, rows, n_heads, n_kv, t_max, sl2, nsplit, min_chunk, part_o, part_lse, o, ldo, counters, stream);
   else
     return LSA_UNSUPPORTED;
-  if (rc != LSA_OK || nsplit == 1) return rc;
-  dim3 grid(n_heads, rows);
-  if (head_dim == 128)
-    attn_combine_kernel<128><<<grid, 128, 0, stream>>>(part_o, part_lse, n_heads, nsplit, static_cast<bf16_raw*>(out), ldo);
-  else
-    attn_combine_kernel<64><<<grid, 64, 0, stream>>>(part_o, part_lse, n_heads, nsplit, static_cast<bf16_raw*>(out), ldo);
-  LSA_CHECK_LAUNCH();
-  return LSA_OK;
+  return rc;
 }

@@ -40,37 +40,48 @@ LSA_DEVICE u32x4_t fp8x8_to_bf16(unsigned lo, unsigned hi) {
   return r;
 }
 
-template <int MB, int TNW, int NW, int KF, int EPI, bool NORM, bool FP8>
-__global__ __launch_bounds__(NW * 64) void gemv_coop_kernel(
+// KW > 1: the workgroup holds KW groups of NW waves; group kg streams the kg-th contiguous
+// part of the split's K chunks for the SAME NW*TNW tiles (A chunks of every group staged
+// side by side in LDS), and the groups' fp32 partials are summed through LDS before the
+// epilogue. More waves (bytes in flight) per workgroup at the same column grouping: the
+// decode projections have too few 16-column tiles to give every CU a workgroup of 8+ waves.
+template <int MB, int TNW, int NW, int KF, int KW, int EPI, bool NORM, bool FP8>
+__global__ __launch_bounds__(NW * KW * 64) void gemv_coop_kernel(
     const bf16_raw* __restrict__ x, int ldx, const int* __restrict__ a_rows, const bf16_raw* __restrict__ wp,
     int M, int N, int K, int SK, float eps, EpiArgs ep, float* __restrict__ slab, unsigned* __restrict__ counters,
     const float* __restrict__ wscale) {
-  constexpr int NTHR = NW * 64;
+  constexpr int NTHR = NW * KW * 64;
   constexpr int KC = 32 * KF;                   // k per chunk (KF MFMA k-fragments)
   constexpr int C16 = KC / 8;                   // 16-B pieces per A row
   constexpr int MR = 16 * MB;
   constexpr int TG = NW * TNW;                  // 16-col tiles per workgroup
-  constexpr int ABUF = MR * KC * 2;             // bytes per A buffer
+  constexpr int ABUF = MR * KC * 2;             // bytes per A chunk of one k-group
+  constexpr int ABUFT = KW * ABUF;              // bytes per A buffer (all k-groups)
   constexpr int RED = TG * MR * 16 * 4;         // fp32 reduction tile
-  constexpr int SMEM = (2 * ABUF > RED ? 2 * ABUF : RED);
+  constexpr int XRED = (KW - 1) * TG * MB * 64 * 16;  // k-group partials, fragment-native
+  constexpr int SMEM0 = (2 * ABUFT > RED ? 2 * ABUFT : RED);
+  constexpr int SMEM = (SMEM0 > XRED ? SMEM0 : XRED);
   __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
   __shared__ float s_ss[MR];
   __shared__ int s_last;
   __shared__ unsigned long long s_key[MR];
 
   const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wt = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int w = wt % NW, kg = wt / NW;          // tile wave within the k-group, k-group
   const int KT = K >> 5;
   const int G = N / 16 / TG;                    // column groups
   const int g = blockIdx.x % G, s = blockIdx.x / G;
   const int nt0 = g * TG + w * TNW;             // this wave's first tile
   const int nch_all = KT / KF;                  // KC-k chunks; split s owns [c_lo, c_hi)
   const int c_lo = s * nch_all / SK, c_hi = (s + 1) * nch_all / SK;
-  const int kt0 = c_lo * KF, nchunk = c_hi - c_lo;
+  // k-group q owns chunks [q*nchunk, (q+1)*nchunk) of the split (host: divisible by KW)
+  const int kt0 = c_lo * KF, nchunk = (c_hi - c_lo) / KW;
 
-  // ---- A staging: thread -> (row + i*RSTEP, 16-B chunk) fixed for all chunks
-  constexpr int LPT = MR * C16 / NTHR;         // A loads per thread per chunk (exact: no
-  static_assert(LPT * NTHR == MR * C16, "A tile must split evenly");  // guarded loads/stores)
+  // ---- A staging: thread -> (row + i*RSTEP, 16-B chunk) fixed for all chunks, one load per
+  // k-group per i
+  constexpr int LPT = MR * C16 / NTHR;         // A loads per thread per chunk and k-group (exact:
+  static_assert(LPT >= 1 && LPT * NTHR == MR * C16, "A tile must split evenly");  // no guards)
   constexpr int RSTEP = NTHR / C16;
   const int arow = tid / C16, ac16 = tid % C16;
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, 0x7fffffff, 0x00020000);
@@ -89,31 +100,33 @@ __global__ __launch_bounds__(NW * 64) void gemv_coop_kernel(
 #pragma unroll
   for (int i = 0; i < LPT; ++i) ss[i] = 0.f;
 
-  struct AV { u32x4_t v[LPT]; };
+  struct AV { u32x4_t v[KW][LPT]; };
   auto load_a = [&](int c) -> AV {
     AV a;
 #pragma unroll
-    for (int i = 0; i < LPT; ++i) {
-      a.v[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, a_voff[i], (kt0 * 32 + c * KC) * 2, 0);
-    }
+    for (int q = 0; q < KW; ++q)
+#pragma unroll
+      for (int i = 0; i < LPT; ++i)
+        a.v[q][i] = __builtin_amdgcn_raw_buffer_load_b128(xr, a_voff[i], (kt0 * 32 + (q * nchunk + c) * KC) * 2, 0);
     return a;
   };
   auto store_a = [&](int buf, const AV& a_in, float count) {  // count: 0 for clamped duplicates
-    AV a;  // rows >= M were loaded from row 0 (valid memory): zero them here, after the MFMAs
 #pragma unroll
-    for (int i = 0; i < LPT; ++i) a.v[i] = a_valid[i] ? a_in.v[i] : zero;
+    for (int q = 0; q < KW; ++q)
 #pragma unroll
-    for (int i = 0; i < LPT; ++i) {
-      if (NORM) {
-        float f[8];
-        unpack8(a.v[i], f);
-        float t = 0.f;
+      for (int i = 0; i < LPT; ++i) {
+        // rows >= M were loaded from row 0 (valid memory): zero them here
+        const u32x4_t av = a_valid[i] ? a_in.v[q][i] : zero;
+        if (NORM) {
+          float f[8];
+          unpack8(av, f);
+          float t = 0.f;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) t += f[j] * f[j];
-        ss[i] += count * t;
+          for (int j = 0; j < 8; ++j) t += f[j] * f[j];
+          ss[i] += count * t;
+        }
+        *reinterpret_cast<u32x4_t*>(smem + buf * ABUFT + q * ABUF + a_off<KC>(arow + i * RSTEP, ac16)) = av;
       }
-      *reinterpret_cast<u32x4_t*>(smem + buf * ABUF + a_off<KC>(arow + i * RSTEP, ac16)) = a.v[i];
-    }
   };
   // B fragments: bf16 -> one 16-B load per k-fragment; FP8 (W8A16, packed as in gemv_fp8.hip)
   // -> one 16-B load per PAIR of k-fragments, converted to bf16 in registers right before the
@@ -126,10 +139,10 @@ __global__ __launch_bounds__(NW * 64) void gemv_coop_kernel(
       for (int t = 0; t < TNW; ++t) {
         if constexpr (FP8)
           b[p][t] = __builtin_amdgcn_raw_buffer_load_b128(
-              wr, lane16, ((nt0 + t) * (KT >> 1) + ((kt0 + c * KF) >> 1) + p) * 1024, 2);
+              wr, lane16, ((nt0 + t) * (KT >> 1) + ((kt0 + (kg * nchunk + c) * KF) >> 1) + p) * 1024, 2);
         else
           b[p][t] = __builtin_amdgcn_raw_buffer_load_b128(
-              wr, lane16, (((nt0 + t) * KT + kt0 + c * KF + p) * 512) * 2, 2);
+              wr, lane16, (((nt0 + t) * KT + kt0 + (kg * nchunk + c) * KF + p) * 512) * 2, 2);
       }
   };
 
@@ -140,7 +153,7 @@ __global__ __launch_bounds__(NW * 64) void gemv_coop_kernel(
     for (int t = 0; t < TNW; ++t) acc[rb][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   auto compute = [&](int buf, u32x4_t (&b)[BL][TNW]) {
-    const unsigned char* base = smem + buf * ABUF;
+    const unsigned char* base = smem + buf * ABUFT + kg * ABUF;
 #pragma unroll
     for (int kf = 0; kf < KF; ++kf) {
       u32x4_t bk[TNW];
@@ -209,8 +222,29 @@ __global__ __launch_bounds__(NW * 64) void gemv_coop_kernel(
     }
   }
   __syncthreads();  // all waves done with the A buffers: smem becomes the reduction tile
+  if constexpr (KW > 1) {
+    // k-groups 1..KW-1 hand their partial tiles to group 0 (fragment-native, 16 B per lane)
+    f32x4_t* xp = reinterpret_cast<f32x4_t*>(smem);  // [KW-1][TG][MB][64]
+    if (kg > 0) {
+#pragma unroll
+      for (int rb = 0; rb < MB; ++rb)
+#pragma unroll
+        for (int t = 0; t < TNW; ++t) xp[(((kg - 1) * TG + w * TNW + t) * MB + rb) * 64 + lane] = acc[rb][t];
+    }
+    __syncthreads();
+    if (kg == 0) {
+#pragma unroll
+      for (int q = 1; q < KW; ++q)
+#pragma unroll
+        for (int rb = 0; rb < MB; ++rb)
+#pragma unroll
+          for (int t = 0; t < TNW; ++t) acc[rb][t] += xp[(((q - 1) * TG + w * TNW + t) * MB + rb) * 64 + lane];
+    }
+    __syncthreads();
+  }
   float* red = reinterpret_cast<float*>(smem);  // [TG][MR][16]
   if (SK == 1) {
+    if (kg == 0)
 #pragma unroll
     for (int rb = 0; rb < MB; ++rb)
 #pragma unroll
@@ -232,6 +266,7 @@ __global__ __launch_bounds__(NW * 64) void gemv_coop_kernel(
     //   [SK][N/16 tiles][MB][64 lanes][4]  fp32, then [SK][G][MR] partial sum(x^2).
     const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc((void*)slab, (short)0, 0x7fffffff, 0x00020000);
     const int split_stride = (N / 16) * MR * 16;  // floats
+    if (kg == 0)
 #pragma unroll
     for (int rb = 0; rb < MB; ++rb)
 #pragma unroll
@@ -357,32 +392,37 @@ __global__ __launch_bounds__(NW * 64) void gemv_coop_kernel(
   }
 }
 
-template <int MB, int TNW, int NW, int KF, int EPI, bool FP8>
+template <int MB, int TNW, int NW, int KF, int KW, int EPI, bool FP8>
 int launch(bool norm, const bf16_raw* x, int ldx, const int* a_rows, const bf16_raw* wp, int M, int N, int K, int SK, float eps,
            const EpiArgs& ep, float* slab, unsigned* cnt, const float* wscale, hipStream_t s) {
   const int G = N / 16 / (NW * TNW);
-  dim3 grid(G * SK), block(NW * 64);
+  dim3 grid(G * SK), block(NW * KW * 64);
   if (norm)
-    gemv_coop_kernel<MB, TNW, NW, KF, EPI, true, FP8><<<grid, block, 0, s>>>(x, ldx, a_rows, wp, M, N, K, SK, eps, ep, slab, cnt, wscale);
+    gemv_coop_kernel<MB, TNW, NW, KF, KW, EPI, true, FP8><<<grid, block, 0, s>>>(x, ldx, a_rows, wp, M, N, K, SK, eps, ep, slab, cnt, wscale);
   else
-    gemv_coop_kernel<MB, TNW, NW, KF, EPI, false, FP8><<<grid, block, 0, s>>>(x, ldx, a_rows, wp, M, N, K, SK, eps, ep, slab, cnt, wscale);
+    gemv_coop_kernel<MB, TNW, NW, KF, KW, EPI, false, FP8><<<grid, block, 0, s>>>(x, ldx, a_rows, wp, M, N, K, SK, eps, ep, slab, cnt, wscale);
   LSA_CHECK_LAUNCH();
   return LSA_OK;
 }
 
+// (mb, tnw, nw, kf, kw); kw > 1 needs mb*16*kf/8 a multiple of nw*kw*64 (exact A staging)
 #define LSA_COOP_CONFIGS(X) \
-  X(2, 1, 8, 8) X(4, 1, 8, 8) X(2, 1, 8, 4) X(4, 1, 8, 4) X(2, 2, 8, 4) X(4, 2, 8, 4) X(2, 2, 4, 4) X(4, 2, 4, 4) \
-  X(8, 1, 8, 4) X(8, 1, 8, 2) X(8, 2, 4, 2) X(2, 1, 4, 4) X(4, 1, 4, 4) X(2, 1, 4, 8) X(8, 1, 4, 2)
+  X(2, 1, 8, 8, 1) X(4, 1, 8, 8, 1) X(2, 1, 8, 4, 1) X(4, 1, 8, 4, 1) X(2, 2, 8, 4, 1) X(4, 2, 8, 4, 1) X(2, 2, 4, 4, 1) \
+  X(4, 2, 4, 4, 1) X(8, 1, 8, 4, 1) X(8, 1, 8, 2, 1) X(8, 2, 4, 2, 1) X(2, 1, 4, 4, 1) X(4, 1, 4, 4, 1) X(2, 1, 4, 8, 1) \
+  X(8, 1, 4, 2, 1) \
+  X(2, 1, 4, 8, 2) X(4, 1, 4, 4, 2) X(4, 1, 4, 8, 2) X(4, 1, 8, 4, 2) X(4, 2, 4, 4, 2) X(8, 1, 4, 2, 2) X(8, 1, 4, 4, 2) \
+  X(4, 1, 4, 4, 4)
 
 // fp8-weight instantiations (subset; KF even so one 16-B load carries two k-fragments)
 #define LSA_COOP_FP8_CONFIGS(X) \
-  X(2, 1, 8, 4) X(4, 1, 8, 4) X(2, 1, 4, 4) X(4, 1, 4, 4) X(8, 1, 8, 4) X(8, 1, 4, 2) X(2, 1, 8, 8) X(4, 1, 8, 8)
+  X(2, 1, 8, 4, 1) X(4, 1, 8, 4, 1) X(2, 1, 4, 4, 1) X(4, 1, 4, 4, 1) X(8, 1, 8, 4, 1) X(8, 1, 4, 2, 1) X(2, 1, 8, 8, 1) \
+  X(4, 1, 8, 8, 1)
 
 template <int EPI, bool FP8>
-int dispatch(int mb, int tnw, int nw, int kf, bool norm, const bf16_raw* x, int ldx, const int* a_rows, const bf16_raw* wp, int M, int N,
+int dispatch(int mb, int tnw, int nw, int kf, int kw, bool norm, const bf16_raw* x, int ldx, const int* a_rows, const bf16_raw* wp, int M, int N,
              int K, int SK, float eps, const EpiArgs& ep, float* slab, unsigned* cnt, const float* wscale, hipStream_t s) {
-#define LSA_C(B, T, W, F) \
-  if (mb == B && tnw == T && nw == W && kf == F) return launch<B, T, W, F, EPI, FP8>(norm, x, ldx, a_rows, wp, M, N, K, SK, eps, ep, slab, cnt, wscale, s);
+#define LSA_C(B, T, W, F, Q) \
+  if (mb == B && tnw == T && nw == W && kf == F && kw == Q) return launch<B, T, W, F, Q, EPI, FP8>(norm, x, ldx, a_rows, wp, M, N, K, SK, eps, ep, slab, cnt, wscale, s);
   if constexpr (FP8) {
     LSA_COOP_FP8_CONFIGS(LSA_C)
   } else {
@@ -399,9 +439,10 @@ int dispatch(int mb, int tnw, int nw, int kf, bool norm, const bf16_raw* x, int 
 // counters: N/16/(nw*tnw) zero-initialised uint32 (reset by the kernel itself).
 template <bool FP8>
 int coop_entry(const void* x, int ldx, const int* a_rows, const void* wp, int M, int N, int K, int norm, float eps,
-               int epi, const EpiArgs* ep, int tnw, int nw, int kf, int sk, float* slab, unsigned* counters,
+               int epi, const EpiArgs* ep, int tnw, int nw, int kf, int sk, int kw, float* slab, unsigned* counters,
                const float* wscale, hipStream_t stream) {
-  if (M < 1 || M > 128 || kf < 1 || K % (32 * kf) || ldx < K || sk < 1) return LSA_BAD_SHAPE;
+  if (M < 1 || M > 128 || kf < 1 || K % (32 * kf) || ldx < K || sk < 1 || kw < 1) return LSA_BAD_SHAPE;
+  if (kw > 1 && (K / (32 * kf)) % (sk * kw)) return LSA_BAD_SHAPE;  // every k-group: same chunk count
   if (FP8 && (kf % 2 || !wscale)) return LSA_BAD_SHAPE;
   const int mb = M <= 32 ? 2 : (M <= 64 ? 4 : 8);
   const int tg = nw * tnw;
@@ -410,7 +451,7 @@ int coop_entry(const void* x, int ldx, const int* a_rows, const void* wp, int M,
   const bf16_raw* xx = static_cast<const bf16_raw*>(x);
   const bf16_raw* w = static_cast<const bf16_raw*>(wp);
   const bool n = norm != 0;
-#define LSA_D(E) dispatch<E, FP8>(mb, tnw, nw, kf, n, xx, ldx, a_rows, w, M, N, K, sk, eps, *ep, slab, counters, wscale, stream)
+#define LSA_D(E) dispatch<E, FP8>(mb, tnw, nw, kf, kw, n, xx, ldx, a_rows, w, M, N, K, sk, eps, *ep, slab, counters, wscale, stream)
   switch (epi) {
     case EPI_STORE: return LSA_D(EPI_STORE);
     case EPI_RESID: return LSA_D(EPI_RESID);
@@ -424,13 +465,14 @@ int coop_entry(const void* x, int ldx, const int* a_rows, const void* wp, int M,
 
 }  // namespace
 
-// K is split into 32*kf-k chunks, spread over the SK splits as evenly as possible.
+// K is split into 32*kf-k chunks, spread over the SK splits as evenly as possible; each split
+// over kw k-groups of nw waves (kw > 1: (K/(32*kf)) % (sk*kw) == 0).
 // Workspace: slab >= SK*N*16*MB*4 + SK*(N/16/(nw*tnw))*16*MB*4 bytes (only when SK > 1);
 // counters: N/16/(nw*tnw) zero-initialised uint32 (reset by the kernel itself).
 extern "C" int lsa_gemv_coop(const void* x, int ldx, const int* a_rows, const void* wp, int M, int N, int K, int norm, float eps,
-                             int epi, const EpiArgs* ep, int tnw, int nw, int kf, int sk, float* slab, unsigned* counters,
-                             hipStream_t stream) {
-  return coop_entry<false>(x, ldx, a_rows, wp, M, N, K, norm, eps, epi, ep, tnw, nw, kf, sk, slab, counters, nullptr,
+                             int epi, const EpiArgs* ep, int tnw, int nw, int kf, int sk, int kw, float* slab,
+                             unsigned* counters, hipStream_t stream) {
+  return coop_entry<false>(x, ldx, a_rows, wp, M, N, K, norm, eps, epi, ep, tnw, nw, kf, sk, kw, slab, counters, nullptr,
                            stream);
 }
 
@@ -438,6 +480,6 @@ extern "C" int lsa_gemv_coop(const void* x, int ldx, const int* a_rows, const vo
 extern "C" int lsa_gemv_coop_fp8(const void* x, int ldx, const int* a_rows, const void* wq, const float* wscale, int M,
                                  int N, int K, int norm, float eps, int epi, const EpiArgs* ep, int tnw, int nw, int kf,
                                  int sk, float* slab, unsigned* counters, hipStream_t stream) {
-  return coop_entry<true>(x, ldx, a_rows, wq, M, N, K, norm, eps, epi, ep, tnw, nw, kf, sk, slab, counters, wscale,
+  return coop_entry<true>(x, ldx, a_rows, wq, M, N, K, norm, eps, epi, ep, tnw, nw, kf, sk, 1, slab, counters, wscale,
                           stream);
 }

@@ -54,12 +54,12 @@ def lib() -> ctypes.CDLL:
     L = ctypes.CDLL(KERNELS_SO, mode=ctypes.RTLD_GLOBAL)
     vp, i, f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
     L.lsa_gemv.argtypes = [vp, i, vp, vp, i, i, i, i, f, i, ctypes.POINTER(EpiArgs), i, i, i, vp]
-    L.lsa_gemv_coop.argtypes = [vp, i, vp, vp, i, i, i, i, f, i, ctypes.POINTER(EpiArgs), i, i, i, i, vp, vp, vp]
+    L.lsa_gemv_coop.argtypes = [vp, i, vp, vp, i, i, i, i, f, i, ctypes.POINTER(EpiArgs), i, i, i, i, i, vp, vp, vp]
     L.lsa_gemv_fp8.argtypes = [vp, i, vp, vp, vp, i, i, i, i, f, i, ctypes.POINTER(EpiArgs), i, i, i, vp]
     L.lsa_dequant_fp8_packed.argtypes = [vp, vp, vp, i, i, vp]
     L.lsa_gemv_coop_fp8.argtypes = [vp, i, vp, vp, vp, i, i, i, i, f, i, ctypes.POINTER(EpiArgs), i, i, i, i, vp, vp, vp]
     L.lsa_gemm.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(EpiArgs), i, i, vp, vp, vp]
-    L.lsa_attn_decode.argtypes = [vp, i, vp, vp, vp, vp, vp, i, i, i, i, i, f, i, i, vp, vp, vp, i, vp]
+    L.lsa_attn_decode.argtypes = [vp, i, vp, vp, vp, vp, vp, i, i, i, i, i, f, i, i, vp, vp, vp, i, vp, vp]
     L.lsa_attn_prefill.argtypes = [vp, i, vp, vp, vp, i, i, i, i, i, f, i, vp, i, vp]
     L.lsa_embed.argtypes = [vp, i, vp, i, vp, i, vp]
     L.lsa_rmsnorm.argtypes = [vp, i, vp, i, i, f, vp, i, vp]
@@ -147,7 +147,7 @@ def gemv(x: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep
     when ``norm``: RMSNorm of the A rows is then applied in-kernel), W: [N, K].
 
     Kernel choice: explicit ``tn/nw/u`` -> streaming GEMV (gemv.hip); explicit
-    ``coop=(tnw, nw, kf, sk)`` -> cooperative split-K (gemv_coop.hip); neither -> the tuned
+    ``coop=(tnw, nw, kf, sk[, kw])`` -> cooperative split-K (gemv_coop.hip); neither -> the tuned
     choice of :func:`packing.proj_config`."""
     from .packing import GEMV_CONFIGS, coop_candidates, coop_slab_floats, proj_config, row_blocks
     _req(1 <= M <= 128, f"gemv supports 1..128 rows, got {M}")
@@ -165,8 +165,8 @@ def gemv(x: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep
         else:
             tn, nw, u = cfg
     if coop is not None:
-        coop = tuple(coop)
-        tnw, cnw, kf, sk = coop
+        coop = tuple(coop) if len(coop) == 5 else tuple(coop) + (1,)
+        tnw, cnw, kf, sk, kw = coop
         _req(coop in coop_candidates(N // 16, K, M), f"gemv: coop config {coop} invalid for N={N} K={K} M={M}")
         if ws is None:
             ws = default_workspace(x.device)
@@ -174,7 +174,7 @@ def gemv(x: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep
         _req(ws.slab.numel() >= need, f"gemv: coop workspace too small ({ws.slab.numel()} < {need} floats)")
         _req(ws.counters.numel() >= N // 16 // (tnw * cnw), "gemv: coop workspace counters too small")
         rc = lib().lsa_gemv_coop(_p(x), x.stride(0), _p(a_rows), _p(wp), M, N, K, int(norm), float(eps), epi,
-                                 ctypes.byref(ep), tnw, cnw, kf, sk, _p(ws.slab), _p(ws.counters), _stream())
+                                 ctypes.byref(ep), tnw, cnw, kf, sk, kw, _p(ws.slab), _p(ws.counters), _stream())
         _check(rc, "lsa_gemv_coop")
         return
     mb = row_blocks(M)
@@ -296,8 +296,10 @@ def attn(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, slot: to
          pos: torch.Tensor, rows: int, n_heads: int, n_kv: int, head_dim: int, nsplit: int,
          part_o: torch.Tensor, part_lse: torch.Tensor, out: torch.Tensor,
          kv_len: Optional[torch.Tensor] = None, min_chunk: int = 64,
-         scale: Optional[float] = None) -> None:
-    """Split-KV attention of ``rows`` query rows against the static cache + combine."""
+         scale: Optional[float] = None, counters: Optional[torch.Tensor] = None) -> None:
+    """Split-KV attention of ``rows`` query rows against the static cache; with nsplit > 1 the
+    last-arriving split of each (row, kv-head) merges the partials in-kernel. ``counters``:
+    >= rows * n_kv zeroed int32 (left zeroed; default: the stream's coop workspace)."""
     _req(_is_bf16_cuda(q, k_cache, v_cache, out), "attn: bf16 cuda tensors")
     _req(k_cache.dim() == 4 and k_cache.shape == v_cache.shape, "attn: cache [slots, n_kv, T, hd]")
     _req(k_cache.shape[1] == n_kv and k_cache.shape[3] == head_dim, "attn: cache dims")
@@ -308,9 +310,14 @@ def attn(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, slot: to
     _req(slot.dtype == torch.int32 and pos.dtype == torch.int32, "attn: int32 slot/pos")
     t_max = k_cache.shape[2]
     sc = head_dim ** -0.5 if scale is None else scale
+    if nsplit > 1 and counters is None:
+        counters = default_workspace(q.device).counters
+    _req(nsplit == 1 or (counters.dtype == torch.int32 and counters.numel() >= rows * n_kv),
+         "attn: counters too small")
     rc = lib().lsa_attn_decode(_p(q), q.stride(0), _p(k_cache), _p(v_cache), _p(slot), _p(pos), _p(kv_len),
                                rows, n_heads, n_kv, head_dim, t_max, float(sc), nsplit, min_chunk,
-                               _p(part_o), _p(part_lse), _p(out), out.stride(0), _stream())
+                               _p(part_o), _p(part_lse), _p(out), out.stride(0),
+                               _p(counters) if nsplit > 1 else None, _stream())
     _check(rc, "lsa_attn_decode")
 
 

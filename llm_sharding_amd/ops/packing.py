@@ -168,27 +168,34 @@ def gemv_candidates(n_tiles: int, k: int, rows: int, need_even: bool = False) ->
             if b == mb and n_tiles % tn == 0 and (not need_even or tn % 2 == 0) and (k // 32) % u == 0]
 
 
-# (mb, tnw, nw, kf) instantiated in csrc/kernels/gemv_coop.hip (LSA_COOP_CONFIGS) - keep in sync.
-COOP_CONFIGS = [(2, 1, 8, 8), (4, 1, 8, 8), (2, 1, 8, 4), (4, 1, 8, 4), (2, 2, 8, 4), (4, 2, 8, 4),
-                (2, 2, 4, 4), (4, 2, 4, 4), (8, 1, 8, 4), (8, 1, 8, 2), (8, 2, 4, 2), (2, 1, 4, 4), (4, 1, 4, 4),
-                (2, 1, 4, 8), (8, 1, 4, 2)]
+# (mb, tnw, nw, kf, kw) instantiated in csrc/kernels/gemv_coop.hip (LSA_COOP_CONFIGS) - keep in sync.
+# kw = k-groups of nw waves per workgroup (kw * nw waves stream the same nw * tnw tiles).
+COOP_CONFIGS = [(2, 1, 8, 8, 1), (4, 1, 8, 8, 1), (2, 1, 8, 4, 1), (4, 1, 8, 4, 1), (2, 2, 8, 4, 1),
+                (4, 2, 8, 4, 1), (2, 2, 4, 4, 1), (4, 2, 4, 4, 1), (8, 1, 8, 4, 1), (8, 1, 8, 2, 1), (8, 2, 4, 2, 1),
+                (2, 1, 4, 4, 1), (4, 1, 4, 4, 1), (2, 1, 4, 8, 1), (8, 1, 4, 2, 1),
+                (2, 1, 4, 8, 2), (4, 1, 4, 4, 2), (4, 1, 4, 8, 2), (4, 1, 8, 4, 2), (4, 2, 4, 4, 2), (8, 1, 4, 2, 2),
+                (8, 1, 4, 4, 2), (4, 1, 4, 4, 4)]
 GEMV_MAX_ROWS = 128  # rows 65..128 are served by the coop kernel only
 COOP_SPLITS = (1, 2, 4, 8, 16)
 
 
 def coop_candidates(n_tiles: int, k: int, rows: int) -> list:
-    """(tnw, nw, kf, sk) for the cooperative split-K GEMV (rows 17..128): every split keeps at
-    least two K chunks of 32*kf so the register prefetch overlaps."""
+    """(tnw, nw, kf, sk, kw) for the cooperative split-K GEMV (rows 17..128): every split
+    (and every k-group of a split) keeps at least one K chunk of 32*kf, and kw > 1 needs the
+    chunks to divide evenly over sk*kw."""
     if rows <= 16:
         return []
     mb = row_blocks(rows)
     out = []
-    for (b, tnw, nw, kf) in COOP_CONFIGS:
+    for (b, tnw, nw, kf, kw) in COOP_CONFIGS:
         if b != mb or n_tiles % (tnw * nw) or k % (32 * kf):
             continue
+        nch = k // (32 * kf)
         for sk in COOP_SPLITS:
-            if k // (32 * kf) >= sk and (n_tiles // (tnw * nw)) * sk <= 4 * N_CU:
-                out.append((tnw, nw, kf, sk))
+            if nch < sk * kw or (kw > 1 and nch % (sk * kw)):
+                continue
+            if (n_tiles // (tnw * nw)) * sk <= 4 * N_CU:
+                out.append((tnw, nw, kf, sk, kw))
     return out
 
 
@@ -211,7 +218,7 @@ def coop_fp8_candidates(n_tiles: int, k: int, rows: int) -> list:
     return out
 
 
-def coop_slab_floats(n: int, rows: int, tnw: int, nw: int, kf: int, sk: int) -> int:
+def coop_slab_floats(n: int, rows: int, tnw: int, nw: int, kf: int, sk: int, kw: int = 1) -> int:
     """fp32 workspace a coop launch needs (0 when sk == 1)."""
     if sk == 1:
         return 0
@@ -229,7 +236,7 @@ def coop_workspace_need(shapes, max_rows: int = 64, even_n=()) -> tuple:
                 continue
             algo, cfg = proj_config(n // 16, rows, need_even=(n, k) in even_n, k=k)
             if algo == "coop":
-                tnw, nw, kf, sk = cfg
+                tnw, nw, kf, sk = cfg[:4]
                 floats = max(floats, coop_slab_floats(n, rows, tnw, nw, kf, sk))
                 groups = max(groups, n // 16 // (tnw * nw))
     return floats, groups
@@ -245,12 +252,15 @@ def _tuned() -> dict:
                     if e.get("algo") in ("fp8", "coop_fp8"):
                         _TUNED[(e["N"], e["K"], e["mb"], bool(e["even"]), "fp8")] = (e["algo"], tuple(e["cfg"]))
                     else:
-                        _TUNED[(e["N"], e["K"], e["mb"], bool(e["even"]))] = (e.get("algo", "gemv"), tuple(e["cfg"]))
+                        cfg = tuple(e["cfg"])
+                        if e.get("algo") == "coop" and len(cfg) == 4:
+                            cfg = cfg + (1,)  # tables written before k-groups existed
+                        _TUNED[(e["N"], e["K"], e["mb"], bool(e["even"]))] = (e.get("algo", "gemv"), cfg)
     return _TUNED
 
 
 def proj_config(n_tiles: int, rows: int, need_even: bool = False, k: int = 4096) -> tuple:
-    """("gemv", (tn, nw, u)) or ("coop", (tnw, nw, kf, sk)) for a decode projection of ``rows``
+    """("gemv", (tn, nw, u)) or ("coop", (tnw, nw, kf, sk, kw)) for a decode projection of ``rows``
     rows. The tuning table (measured on MI355X) wins; otherwise rows <= 16 use the
     weight-streaming GEMV and larger row counts the cooperative split-K kernel with the
     smallest split that fills the 256 CUs."""
@@ -264,7 +274,7 @@ def proj_config(n_tiles: int, rows: int, need_even: bool = False, k: int = 4096)
         allc = coop_candidates(n_tiles, k, rows)
         cands = []
         for pref in ((1, 8, 8), (1, 8, 4), (1, 8, 2)):
-            cands = [c for c in allc if c[:3] == pref]
+            cands = [c for c in allc if c[:3] == pref and c[4] == 1]
             if cands:
                 break
         cands = cands or allc

@@ -415,7 +415,9 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
     cfg = get_preset(model)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per visible GPU; modulo the device count so a 1-GPU box can rehearse the
+    # multi-rank RCCL path (identity on an 8-GPU node)
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     if n_gpus != world:
         raise ValueError(f"n_gpus={n_gpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local)

@@ -174,6 +174,9 @@ def keys_max_torch(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
 
 class StageEngine:
     DECODE_MAX_ROWS = packing.GEMV_MAX_ROWS  # rows handled by the weight-streaming GEMV paths (128)
+    # split-KV chunks never shorter than this many keys: below ~256 keys per split the merge
+    # costs more than the extra parallelism buys (profiles/r1_bench_kernels_sweep.jsonl, attn)
+    ATTN_MIN_CHUNK = 256
 
     def __init__(self, cfg: LlamaConfig, start: int, end: int, device="cpu",
                  dtype=torch.bfloat16, *, has_embed: bool = False, has_head: bool = False,
@@ -211,6 +214,7 @@ class StageEngine:
         self.verbose = verbose
         self.layers: list = []
         self.embed_w = self.final_norm = self.lm_head = None
+        self.head_bias = None  # fp32 [head_v1 - head_v0]: -huge on vocab padding columns
         self.pos_emb = self.final_norm_b = None
         self.k_cache: list = []
         self.v_cache: list = []
@@ -263,6 +267,13 @@ class StageEngine:
             else:
                 self.lm_head = packing.pack_b(lm) if self.gpu else lm.contiguous()
             del lm
+            # padding columns (copies of row 0) tie with token 0 up to rounding: a -huge bias
+            # keeps them out of the fused argmax
+            n_pad = self.head_v1 - max(self.head_v0, cfg.vocab_size)
+            if n_pad > 0:
+                hb = torch.zeros(self.head_v1 - self.head_v0, dtype=torch.float32, device=dev)
+                hb[hb.numel() - n_pad:] = -3.0e38
+                self.head_bias = hb
         self._alloc_runtime()
 
     def _prepare_layer(self, lw: dict) -> LayerWeights:
@@ -334,6 +345,8 @@ class StageEngine:
             ws_rows = max(self.DECODE_MAX_ROWS * self.max_decode_nsplit, R * 4)
             self.part_o = torch.zeros(ws_rows * cfg.num_attention_heads * hd, dtype=torch.float32, device=dev)
             self.part_lse = torch.zeros(ws_rows * cfg.num_attention_heads, dtype=torch.float32, device=dev)
+            # per-(row, kv-head) arrival tickets of the in-kernel split-KV merge (self-resetting)
+            self.attn_cnt = torch.zeros(ws_rows * cfg.num_key_value_heads, dtype=torch.int32, device=dev)
             self.ws_rows = ws_rows
             self.keys = torch.zeros(R, dtype=torch.int64, device=dev)
             self.tokens = torch.zeros(R, dtype=torch.int32, device=dev)
@@ -458,7 +471,7 @@ class StageEngine:
         """Fused final RMSNorm + lm_head slice + argmax keys (atomicMax into ``keys``).
         GPT-2: ln_f (LayerNorm kernel, rows gathered first) then the plain GEMV + argmax."""
         from ..ops import hip
-        ep = hip.make_epi(keys=keys, col_offset=self.head_v0)
+        ep = hip.make_epi(keys=keys, col_offset=self.head_v0, bias=self.head_bias)
         N, H, eps = self.head_v1 - self.head_v0, self.cfg.hidden_size, self.cfg.rms_norm_eps
         if self.cfg.is_gpt2:
             xn = self.buf_xn[:rows]
@@ -496,7 +509,10 @@ class StageEngine:
             x = G2.layer_norm(hs, self.final_norm, self.final_norm_b, self.cfg.rms_norm_eps)
         else:
             x = rmsnorm(hs, self.final_norm, self.cfg.rms_norm_eps)
-        return F.linear(x, self.lm_head.float())
+        lg = F.linear(x, self.lm_head.float())
+        if self.head_bias is not None:
+            lg = lg + self.head_bias.to(lg.device)
+        return lg
 
     # ------------------------------------------------------------------------- HIP path
     def decode_nsplit(self, rows: int) -> int:
@@ -559,7 +575,7 @@ class StageEngine:
                 hip.attn_prefill(q, kc, vc, tiles[1], nh, nkv, hd, attn_o, causal=kv_len is None, tiles_host=tiles[0])
             else:
                 hip.attn(q, kc, vc, slot, pos, rows, nh, nkv, hd, nsplit, self.part_o, self.part_lse, attn_o,
-                         kv_len=kv_len)
+                         kv_len=kv_len, counters=self.attn_cnt, min_chunk=self.ATTN_MIN_CHUNK)
             ep_o = hip.make_epi(out=hbuf, resid=hbuf, ldo=hbuf.stride(0), ldr=hbuf.stride(0))
             ep_gu = hip.make_epi(out=act, ldo=act.stride(0))
             if decode:
@@ -606,7 +622,7 @@ class StageEngine:
                 hip.attn_prefill(q, kc, vc, tiles[1], nh, nkv, hd, attn_o, causal=kv_len is None, tiles_host=tiles[0])
             else:
                 hip.attn(q, kc, vc, slot, pos, rows, nh, nkv, hd, nsplit, self.part_o, self.part_lse, attn_o,
-                         kv_len=kv_len)
+                         kv_len=kv_len, counters=self.attn_cnt, min_chunk=self.ATTN_MIN_CHUNK)
             proj(attn_o, lw.o, lw.o_s, H, cfg.q_size, hip.EPI_RESID,
                  hip.make_epi(out=hbuf, resid=hbuf, ldo=hbuf.stride(0), ldr=hbuf.stride(0), bias=lw.o_b))
             hip.layernorm(hbuf, xn, lw.ln_post, lw.ln_post_b, rows, eps)

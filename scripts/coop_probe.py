@@ -23,7 +23,7 @@ for N, M, cfg in ((4096, 64, (1, 8, 4)), (4096, 32, (1, 8, 4)), (12288, 64, (1, 
         ep = hip.make_epi(out=out, resid=out, ldo=N, ldr=N)
         row = {"N": N, "M": M, "K": K}
         for sk in (1, 2, 4, 8):
-            c = cfg + (sk,)
+            c = cfg + (sk, 1)
             if c not in packing.coop_candidates(N // 16, K, M):
                 continue
             row[f"coop_sk{sk}"] = round(timeit(lambda i: hip.gemv(x, ws[i % nbuf], M, N, K, hip.EPI_RESID, ep,

@@ -93,14 +93,15 @@ def test_gemv_every_config(cfg):
 
 @pytest.mark.parametrize("cfg", packing.COOP_CONFIGS)
 def test_gemv_coop_every_config(cfg):
-    """Cooperative split-K GEMV: every instantiated (mb, tnw, nw) x every legal split, with
-    the fused RMSNorm + residual epilogue (partial sum(x^2) combined across splits) and
-    uneven chunk splits (K = 11008 -> 43 or 86 chunks)."""
+    """Cooperative split-K GEMV: every instantiated (mb, tnw, nw, kf, kw) x every legal split,
+    with the fused RMSNorm + residual epilogue (partial sum(x^2) combined across splits and
+    k-groups) and uneven chunk splits (K = 11008 -> 43 or 86 chunks)."""
     h = hip()
-    mb, tnw, nw, kf = cfg
+    mb, tnw, nw, kf, kw = cfg
     M = {2: 29, 4: 50, 8: 100}[mb]
     N = 16 * tnw * nw * 3
-    for K in (11008, 512):
+    tested = 0
+    for K in (11008, 4096, 512):
         x = _rnd(M, K)
         g = (1 + 0.1 * torch.randn(K, device=DEV)).to(torch.bfloat16)
         w = _rnd(N, K, scale=0.02)
@@ -108,12 +109,14 @@ def test_gemv_coop_every_config(cfg):
         resid = _rnd(M, N)
         ref = resid.float() + _rmsnorm(x, g, 1e-5) @ w.float().T
         for c in packing.coop_candidates(N // 16, K, M):
-            if c[:3] != (tnw, nw, kf):
+            if c[:3] != (tnw, nw, kf) or c[4] != kw:
                 continue
+            tested += 1
             out = resid.clone()
             h.gemv(x, wp, M, N, K, h.EPI_RESID, h.make_epi(out=out, resid=out, ldo=N, ldr=N), norm=True,
                    coop=c)
             assert rel_err(out, ref) < 8e-3, (cfg, K, c)
+    assert tested > 0, cfg
 
 
 @pytest.mark.parametrize("M", [20, 64])
