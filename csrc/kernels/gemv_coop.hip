@@ -411,7 +411,7 @@ int launch(bool norm, const bf16_raw* x, int ldx, const int* a_rows, const bf16_
   X(4, 2, 4, 4, 1) X(8, 1, 8, 4, 1) X(8, 1, 8, 2, 1) X(8, 2, 4, 2, 1) X(2, 1, 4, 4, 1) X(4, 1, 4, 4, 1) X(2, 1, 4, 8, 1) \
   X(8, 1, 4, 2, 1) \
   X(2, 1, 4, 8, 2) X(4, 1, 4, 4, 2) X(4, 1, 4, 8, 2) X(4, 1, 8, 4, 2) X(4, 2, 4, 4, 2) X(8, 1, 4, 2, 2) X(8, 1, 4, 4, 2) \
-  X(4, 1, 4, 4, 4)
+  X(4, 1, 4, 4, 4) X(4, 1, 2, 4, 2) X(4, 1, 2, 4, 1) X(2, 1, 2, 4, 2) X(8, 1, 2, 2, 2)
 
 // fp8-weight instantiations (subset; KF even so one 16-B load carries two k-fragments)
 #define LSA_COOP_FP8_CONFIGS(X) \

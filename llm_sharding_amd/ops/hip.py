@@ -139,6 +139,16 @@ def default_workspace(device=None) -> CoopWorkspace:
     return _WS[key]
 
 
+def _check_epi(epi: int, ep: EpiArgs, N: int) -> None:
+    """Host-side guard for the in-kernel stores: a QKV epilogue writes q + k/v columns into
+    caches of n_kv heads, so its column count must match the head geometry exactly."""
+    if epi == EPI_QKV:
+        _req(N == (ep.n_heads + 2 * ep.n_kv) * ep.head_dim,
+             f"QKV epilogue: N={N} != (n_heads {ep.n_heads} + 2 n_kv {ep.n_kv}) x head_dim {ep.head_dim}")
+    elif epi == EPI_ARGMAX:
+        _req(bool(ep.keys), "ARGMAX epilogue needs keys")
+
+
 def gemv(x: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep: EpiArgs,
          norm: bool = False, eps: float = 1e-5, a_rows: Optional[torch.Tensor] = None,
          tn: int = 0, nw: int = 0, u: int = 0, coop: Optional[tuple] = None,
@@ -151,6 +161,7 @@ def gemv(x: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep
     choice of :func:`packing.proj_config`."""
     from .packing import GEMV_CONFIGS, coop_candidates, coop_slab_floats, proj_config, row_blocks
     _req(1 <= M <= 128, f"gemv supports 1..128 rows, got {M}")
+    _check_epi(epi, ep, N)
     _req(_is_bf16_cuda(x, wp), "gemv: bf16 cuda tensors required")
     _req(wp.numel() == N * K and N % 16 == 0 and K % 32 == 0, "gemv: packed weight shape")
     _req(x.dim() == 2 and x.shape[1] >= K and x.stride(1) == 1, "gemv: x must be [rows, >=K] row-major")
@@ -192,6 +203,7 @@ def gemv_fp8(x: torch.Tensor, wq: torch.Tensor, wscale: torch.Tensor, M: int, N:
     ``wscale`` fp32 [N] per-row scale (the RMSNorm weight folded in before quantisation)."""
     from .packing import FP8_CONFIGS, fp8_config, row_blocks
     _req(1 <= M <= 64, f"gemv_fp8 supports 1..64 rows, got {M}")
+    _check_epi(epi, ep, N)
     _req(_is_bf16_cuda(x), "gemv_fp8: bf16 cuda activations")
     _req(wq.is_cuda and wq.dtype == torch.uint8 and wq.numel() == N * K, "gemv_fp8: packed fp8 weights [N*K] uint8")
     _req(wscale.is_cuda and wscale.dtype == torch.float32 and wscale.numel() >= N, "gemv_fp8: fp32 scales [N]")
@@ -215,6 +227,7 @@ def proj_fp8(x: torch.Tensor, wq: torch.Tensor, wscale: torch.Tensor, M: int, N:
     weights (``packing.fp8_proj_config`` unless ``algo=(name, cfg)`` is given)."""
     from .packing import coop_fp8_candidates, coop_slab_floats, fp8_proj_config
     _req(1 <= M <= 128, f"proj_fp8 supports 1..128 rows, got {M}")
+    _check_epi(epi, ep, N)
     name, cfg = algo if algo is not None else fp8_proj_config(N // 16, M, need_even=(epi == EPI_SWIGLU), k=K)
     if name == "fp8":
         gemv_fp8(x, wq, wscale, M, N, K, epi, ep, norm=norm, eps=eps, a_rows=a_rows, cfg=cfg)
@@ -269,6 +282,7 @@ def gemm(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep
     _req(_is_bf16_cuda(a, wp), "gemm: bf16 cuda tensors required")
     _req(wp.numel() == N * K and K % 64 == 0, "gemm: packed weight shape")
     _req(a.dim() == 2 and a.shape[0] >= M and a.shape[1] >= K and a.stride(1) == 1, "gemm: A shape")
+    _check_epi(epi, ep, N)
     if N % (64 * tn):
         tn = 1
     _req(N % (64 * tn) == 0, f"gemm: N={N} not a multiple of {64 * tn}")

@@ -174,7 +174,8 @@ COOP_CONFIGS = [(2, 1, 8, 8, 1), (4, 1, 8, 8, 1), (2, 1, 8, 4, 1), (4, 1, 8, 4, 
                 (4, 2, 8, 4, 1), (2, 2, 4, 4, 1), (4, 2, 4, 4, 1), (8, 1, 8, 4, 1), (8, 1, 8, 2, 1), (8, 2, 4, 2, 1),
                 (2, 1, 4, 4, 1), (4, 1, 4, 4, 1), (2, 1, 4, 8, 1), (8, 1, 4, 2, 1),
                 (2, 1, 4, 8, 2), (4, 1, 4, 4, 2), (4, 1, 4, 8, 2), (4, 1, 8, 4, 2), (4, 2, 4, 4, 2), (8, 1, 4, 2, 2),
-                (8, 1, 4, 4, 2), (4, 1, 4, 4, 4)]
+                (8, 1, 4, 4, 2), (4, 1, 4, 4, 4), (4, 1, 2, 4, 2), (4, 1, 2, 4, 1), (2, 1, 2, 4, 2),
+                (8, 1, 2, 2, 2)]
 GEMV_MAX_ROWS = 128  # rows 65..128 are served by the coop kernel only
 COOP_SPLITS = (1, 2, 4, 8, 16)
 

@@ -50,6 +50,8 @@ MODEL_SHAPES = {
     "llama3.2-3b": {"qkv": (5120, 3072), "o": (3072, 3072), "gate_up": (16384, 3072), "down": (3072, 8192),
                     "lm_head": (128256, 3072)},
 }
+# (n_heads, n_kv) of each model: the QKV epilogue writes k/v into a cache of n_kv heads
+MODEL_HEADS = {"llama2-7b": (32, 32), "llama2-70b": (64, 8), "llama3.2-3b": (24, 8)}
 EPIS = {"qkv": hip.EPI_QKV, "o": hip.EPI_RESID, "gate_up": hip.EPI_SWIGLU, "down": hip.EPI_RESID,
         "lm_head": hip.EPI_ARGMAX}
 
@@ -71,15 +73,16 @@ def gemv_sweep(out_rows, models, rows_list, tune_entries, fp8=False):
             for M in rows_list:
                 x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
                 out = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
-                nh = (N // 128) // 3 if epi == hip.EPI_QKV else 1
+                nh, nkv = MODEL_HEADS[model] if epi == hip.EPI_QKV else (1, 1)
+                assert epi != hip.EPI_QKV or N == (nh + 2 * nkv) * 128, (model, N)
                 q = torch.zeros(M, max(N, 128), dtype=torch.bfloat16, device=DEV)
-                kc = torch.zeros(M, max(nh, 1), 1024, 128, dtype=torch.bfloat16, device=DEV)
+                kc = torch.zeros(M, nkv, 1024, 128, dtype=torch.bfloat16, device=DEV)
                 slot = torch.arange(M, dtype=torch.int32, device=DEV)
                 pos = torch.full((M,), 100, dtype=torch.int32, device=DEV)
                 keys = torch.zeros(M, dtype=torch.int64, device=DEV)
                 if epi == hip.EPI_QKV:
                     ep = hip.make_epi(out=q, k_cache=kc, v_cache=kc, slot=slot, pos=pos, cos=cos, sin=sin,
-                                      ldo=q.shape[1], n_heads=nh, n_kv=nh, head_dim=128, t_max=1024)
+                                      ldo=q.shape[1], n_heads=nh, n_kv=nkv, head_dim=128, t_max=1024)
                 elif epi == hip.EPI_ARGMAX:
                     ep = hip.make_epi(keys=keys)
                 else:
@@ -173,7 +176,9 @@ def main():
     ap.add_argument("--only", default="gemv,attn,gemm")
     ap.add_argument("--models", default="llama2-7b")
     ap.add_argument("--rows", default="1,16,32,64")
-    ap.add_argument("--tune", action="store_true", help="write llm_sharding_amd/ops/gemv_tuning.json")
+    ap.add_argument("--tune", action="store_true", help="merge the winners into the tuning table")
+    ap.add_argument("--tune-file", default=packing.TUNING_FILE,
+                    help="table to write (on a gpurun box: a path under gpurun_out/, then copy it back)")
     ap.add_argument("--fp8", action="store_true", help="also sweep the fp8-weight (W8A16) kernels")
     ap.add_argument("--out", default="gpurun_out/bench_kernels.json")
     a = ap.parse_args()
@@ -193,9 +198,9 @@ def main():
             old.update(tune)
             ents = [{"N": k[0], "K": k[1], "mb": k[2], "even": k[3], "algo": v[0], "cfg": v[1]}
                     for k, v in sorted(old.items(), key=lambda kv: tuple(map(str, kv[0])))]
-            with open(packing.TUNING_FILE, "w") as f:
+            with open(a.tune_file, "w") as f:
                 json.dump({"device": torch.cuda.get_device_name(), "entries": ents}, f, indent=1)
-            print(f"wrote {len(ents)} tuning entries to {packing.TUNING_FILE}")
+            print(f"wrote {len(ents)} tuning entries to {a.tune_file}")
     if "attn" in a.only:
         attn_sweep(rows)
     if "gemm" in a.only:
