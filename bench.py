@@ -38,7 +38,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=64)
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--model", default="llama2-7b")
-    ap.add_argument("--batch", type=int, default=64, help="sequences per micro-batch (per GPU)")
+    ap.add_argument("--batch", type=int, default=128,
+                    help="sequences per micro-batch (per GPU); 128 = the largest hipGraph decode batch")
     ap.add_argument("--prompt-len", type=int, default=128)
     ap.add_argument("--max-seq", type=int, default=1024)
     ap.add_argument("--microbatches", type=int, default=0, help="0 = one per pipeline stage")
@@ -79,7 +80,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": (round(res["tok_s"] / BASELINE_TOK_S, 3) if BASELINE_TOK_S else None),
         "dtype": "bf16" if a.weight_dtype == "bf16" else "bf16 activations, fp8-e4m3 weights (W8A16)",
-        "data": "synthetic prompts, random-init weights (Llama-2-7B architecture)",
+        "data": f"synthetic prompts, random-init weights ({res['model_name']} architecture)",
         "config": {"model": res["model_name"], "global_batch": res["global_batch"],
                    "seq_len": a.prompt_len + a.warmup + a.steps,
                    "parallelism": f"pp{a.gpus}", "microbatches": res["microbatches"],
