@@ -152,25 +152,39 @@ __global__ __launch_bounds__(NW * KW * 64) void gemv_coop_kernel(
 #pragma unroll
     for (int t = 0; t < TNW; ++t) acc[rb][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
+  // The A fragments of a group of GK k-fragments (GK*MB <= 16 ds_read_b128) are all issued
+  // before the group's MFMAs (sched_barrier): with one wave per SIMD nothing else hides LDS
+  // latency, and the default schedule waited lgkmcnt on a fresh read before every MFMA.
+  constexpr int GK = (16 / MB) < KF ? (16 / MB > 0 ? 16 / MB : 1) : KF;
+  static_assert(KF % GK == 0, "k-fragment groups must tile the chunk");
   auto compute = [&](int buf, u32x4_t (&b)[BL][TNW]) {
     const unsigned char* base = smem + buf * ABUFT + kg * ABUF;
 #pragma unroll
-    for (int kf = 0; kf < KF; ++kf) {
-      u32x4_t bk[TNW];
+    for (int k0 = 0; k0 < KF; k0 += GK) {
+      u32x4_t af[GK][MB];
 #pragma unroll
-      for (int t = 0; t < TNW; ++t) {
-        if constexpr (FP8)
-          bk[t] = (kf & 1) ? fp8x8_to_bf16(b[kf >> 1][t][2], b[kf >> 1][t][3])
-                           : fp8x8_to_bf16(b[kf >> 1][t][0], b[kf >> 1][t][1]);
-        else
-          bk[t] = b[kf][t];
-      }
+      for (int j = 0; j < GK; ++j)
 #pragma unroll
-      for (int rb = 0; rb < MB; ++rb) {
-        const int row = rb * 16 + (lane & 15);
-        const u32x4_t a = *reinterpret_cast<const u32x4_t*>(base + a_off<KC>(row, kf * 4 + (lane >> 4)));
+        for (int rb = 0; rb < MB; ++rb)
+          af[j][rb] = *reinterpret_cast<const u32x4_t*>(
+              base + a_off<KC>(rb * 16 + (lane & 15), (k0 + j) * 4 + (lane >> 4)));
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int t = 0; t < TNW; ++t) acc[rb][t] = mfma16(a, bk[t], acc[rb][t]);
+      for (int j = 0; j < GK; ++j) {
+        const int kf = k0 + j;
+        u32x4_t bk[TNW];
+#pragma unroll
+        for (int t = 0; t < TNW; ++t) {
+          if constexpr (FP8)
+            bk[t] = (kf & 1) ? fp8x8_to_bf16(b[kf >> 1][t][2], b[kf >> 1][t][3])
+                             : fp8x8_to_bf16(b[kf >> 1][t][0], b[kf >> 1][t][1]);
+          else
+            bk[t] = b[kf][t];
+        }
+#pragma unroll
+        for (int rb = 0; rb < MB; ++rb)
+#pragma unroll
+          for (int t = 0; t < TNW; ++t) acc[rb][t] = mfma16(af[j][rb], bk[t], acc[rb][t]);
       }
     }
   };
