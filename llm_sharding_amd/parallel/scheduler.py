@@ -152,6 +152,21 @@ def plan_stages(cfg: LlamaConfig, devices: Sequence[DeviceSpec] | int, *,
     return plan
 
 
+def kv_slots_for_memory(cfg: LlamaConfig, n_layers: int, max_seq: int, mem_bytes: float,
+                        weight_bytes: float, reserve_bytes: float = 8e9, elem_bytes: int = 2,
+                        microbatches: int = 1, max_per_microbatch: int = 128) -> int:
+    """KV slots (sequences of ``max_seq`` tokens) per micro-batch that fit a stage of
+    ``n_layers`` layers next to its weights: the static KV cache is sized from the device's
+    HBM (288 GB on MI355X) instead of a fixed guess. Capped at
+    ``max_per_microbatch`` (the largest hipGraph decode batch)."""
+    per_slot = float(cfg.kv_bytes_per_token_per_layer(elem_bytes)) * n_layers * max_seq
+    free = mem_bytes - reserve_bytes - weight_bytes
+    if per_slot <= 0 or free < per_slot * microbatches:
+        raise ValueError(f"no room for a KV cache of {max_seq} tokens x {n_layers} layers "
+                         f"({free / 1e9:.1f} GB free after weights)")
+    return int(min(max_per_microbatch, free // (per_slot * microbatches)))
+
+
 def even_split(n_layers: int, n_stages: int) -> list:
     base, extra = divmod(n_layers, n_stages)
     out, s = [], 0

@@ -22,7 +22,7 @@ class RuntimeConfig:
     device: str = ""              # "" = cuda:<LOCAL_RANK> if a GPU is visible, else cpu
     dtype: str = "bfloat16"
     backend: str = "rccl"         # stage hand-off: rccl (torch.distributed/RCCL), tcp, local
-    batch: int = 32               # KV slots per micro-batch
+    batch: int = 32               # KV slots per micro-batch (0 = as many as HBM holds, <= 128)
     microbatches: int = 0         # 0 = max(2, pipeline stages)
     max_seq: int = 2048
     prefill_budget: int = 2048    # prompt tokens per prefill command (longer prompts are chunked)
@@ -37,8 +37,8 @@ class RuntimeConfig:
     def __post_init__(self):
         if self.backend not in BACKENDS:
             raise ValueError(f"backend must be one of {BACKENDS}, got {self.backend!r}")
-        if self.batch < 1 or self.max_seq < 2 or self.prefill_budget < 1:
-            raise ValueError("batch, max_seq and prefill_budget must be positive")
+        if self.batch < 0 or self.max_seq < 2 or self.prefill_budget < 1:
+            raise ValueError("batch must be >= 0 (0 = auto), max_seq and prefill_budget positive")
 
     # ------------------------------------------------------------------ CLI
     @classmethod

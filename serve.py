@@ -120,6 +120,13 @@ def main():
         ctrl = dist.new_group(backend="gloo")
     cfg, source = rc.model_and_source()
     M = rc.microbatches or max(2, world)
+    if rc.batch == 0:  # size the KV cache from this GPU's HBM (bottleneck stage of a weights-only plan)
+        from llm_sharding_amd.parallel.scheduler import kv_slots_for_memory
+        wplan = plan_stages(cfg, world, head_split=world > 1)
+        mem = torch.cuda.get_device_properties(dev).total_memory if gpu else 64e9
+        rc.batch = min(kv_slots_for_memory(cfg, s.n_layers, rc.max_seq, mem, s.weight_bytes, microbatches=M)
+                       for s in wplan.stages)
+        log.info(f"KV cache sized from {mem / 1e9:.0f} GB HBM: {rc.batch} slots x {M} micro-batches")
     plan = plan_stages(cfg, world, kv_tokens=rc.max_seq * rc.batch * M)
     st = plan.stages[rank]
     if rank == 0:
