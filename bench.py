@@ -10,8 +10,10 @@ Workload (synthetic prompts, random-init bf16 weights of the exact Llama-2-7B ar
 generated on each device - no checkpoints are available offline):
   * rank r owns a contiguous layer range chosen by the master scheduler (rank 0 also holds
     the embedding, rank N-1 the final norm + lm_head), one process per GPU;
-  * M = N micro-batches of B sequences each are in flight in the pipeline (B per GPU is
-    fixed -> weak scaling); every sequence was prefilled with a P-token prompt first;
+  * M = S x N micro-batches of B sequences each are in flight (S x B sequences per GPU,
+    fixed -> weak scaling); every sequence was prefilled with a P-token prompt first. On one
+    GPU the S micro-batches replay their decode graphs concurrently on S HIP streams (a 7B
+    decode graph alone leaves CUs idle); pipelines keep one compute stream per stage;
   * one timed "step" = every in-flight sequence produces one new token (greedy, fused
     lm_head+argmax on device); hidden states move stage->stage with RCCL send/recv over
     xGMI, token ids return last->first the same way.
@@ -41,8 +43,11 @@ def parse():
     ap.add_argument("--batch", type=int, default=128,
                     help="sequences per micro-batch (per GPU); 128 = the largest hipGraph decode batch")
     ap.add_argument("--prompt-len", type=int, default=128)
-    ap.add_argument("--max-seq", type=int, default=1024)
-    ap.add_argument("--microbatches", type=int, default=0, help="0 = one per pipeline stage")
+    ap.add_argument("--max-seq", type=int, default=0, help="0 = prompt + warmup + steps, rounded up to 64")
+    ap.add_argument("--streams", type=int, default=3,
+                    help="micro-batches resident per GPU; on one GPU they replay concurrently on this many "
+                         "HIP streams")
+    ap.add_argument("--microbatches", type=int, default=0, help="0 = streams x pipeline stages")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--json-out", default="")
@@ -65,7 +70,7 @@ def main():
     res = run_decode_benchmark(model=a.model, n_gpus=a.gpus, steps=a.steps, warmup=a.warmup,
                                batch=a.batch, prompt_len=a.prompt_len, max_seq=a.max_seq,
                                microbatches=a.microbatches, seed=a.seed, use_graph=not a.no_graph,
-                               weight_dtype=a.weight_dtype)
+                               weight_dtype=a.weight_dtype, streams=a.streams)
     if res is None:  # non-zero ranks
         return
     line = {
@@ -84,7 +89,8 @@ def main():
         "config": {"model": res["model_name"], "global_batch": res["global_batch"],
                    "seq_len": a.prompt_len + a.warmup + a.steps,
                    "parallelism": f"pp{a.gpus}", "microbatches": res["microbatches"],
-                   "batch_per_microbatch": a.batch, "prompt_len": a.prompt_len},
+                   "batch_per_microbatch": a.batch, "prompt_len": a.prompt_len,
+                   "concurrent_streams": res["streams"], "max_seq": res["max_seq"]},
         "p50_tpot_ms": round(res["p50_tpot_ms"], 4),
         "p90_tpot_ms": round(res["p90_tpot_ms"], 4),
         "ttft_ms": round(res["ttft_ms"], 3),

@@ -109,7 +109,7 @@ class PipelineStage:
     def __init__(self, cfg, rank: int, world: int, start: int, end: int, device, batch: int,
                  microbatches: int, max_seq: int, source, use_graph: bool = True,
                  max_prefill_rows: int = 2048, dtype=torch.bfloat16, p2p=None,
-                 split_head: Optional[bool] = None, weight_dtype: str = "bf16"):
+                 split_head: Optional[bool] = None, weight_dtype: str = "bf16", streams: int = 1):
         self.cfg, self.rank, self.world = cfg, rank, world
         self.p2p = p2p if p2p is not None else DistP2P()
         self.first, self.last = rank == 0, rank == world - 1
@@ -146,6 +146,15 @@ class PipelineStage:
         self.send_works: dict = {}
         self.tokens_ready = [True] * microbatches  # stage 0: next-step token ids are in place
         self.tl = tracing.from_env(rank, self.device if self.gpu else "cpu")  # LSA_TRACE=dir
+        # Concurrent micro-batches (single-stage GPU pipelines only): micro-batch mb replays on
+        # stream mb % S with its own scratch set, so up to S decode graphs share the GPU at once.
+        # A Llama-2-7B decode graph alone leaves CUs idle (its projections have too few tiles to
+        # fill 256 CUs), and S graphs side by side raise throughput (scripts/concurrency_probe.py).
+        # Multi-stage pipelines keep one compute stream: their RCCL p2p kernels wait on peers,
+        # and more streams than the process's hardware queues would multiplex a blocked p2p
+        # kernel in front of compute it depends on.
+        self.S = max(1, min(streams, microbatches)) if (self.gpu and world == 1 and self.use_graph) else 1
+        self.streams = [torch.cuda.Stream(self.device) for _ in range(self.S)] if self.S > 1 else []
 
     # ---------------------------------------------------------------- p2p helpers
     def _send(self, t: torch.Tensor, dst: int, key):
@@ -247,8 +256,12 @@ class PipelineStage:
                     g.h_fin.copy_(self.seed[mb][0])
                     g.keys_in.copy_(self.seed[mb][1])
             else:
-                cls = DecodeGraph if self.gpu else EagerDecode
-                g = cls(self.eng, self.B, mode, slots=self.slots(mb), history_len=history_len if self.last else 0)
+                if self.gpu:
+                    g = DecodeGraph(self.eng, self.B, mode, slots=self.slots(mb),
+                                    history_len=history_len if self.last else 0, scratch=mb % self.S)
+                else:
+                    g = EagerDecode(self.eng, self.B, mode, slots=self.slots(mb),
+                                    history_len=history_len if self.last else 0)
                 if first_tokens is not None and mode in ("full", "first"):
                     g.tokens.copy_(first_tokens[mb])
             if self.use_graph:
@@ -263,8 +276,23 @@ class PipelineStage:
 
     def step(self, s: int, events: Optional[list] = None) -> None:
         """One decode step for every micro-batch (the host never blocks on the GPU here)."""
+        if self.S > 1:
+            cur = torch.cuda.current_stream(self.device)
+            for mb in range(self.M):
+                st = self.streams[mb % self.S]
+                if mb < self.S:
+                    st.wait_stream(cur)  # ordered after whatever the caller enqueued before
+                with torch.cuda.stream(st):
+                    self.step_mb(s, mb, events)
+            return
         for mb in range(self.M):
             self.step_mb(s, mb, events)
+
+    def join_streams(self) -> None:
+        """Make the current stream wait for the concurrent micro-batch streams."""
+        cur = torch.cuda.current_stream(self.device) if self.gpu else None
+        for st in self.streams:
+            cur.wait_stream(st)
 
     def step_mb(self, s: int, mb: int, events: Optional[list] = None) -> None:
         g = self.graphs[mb]
@@ -324,6 +352,7 @@ class PipelineStage:
                     self.tokens_ready[mb] = True
         for k in list(self.send_works):
             self._wait_send(k)
+        self.join_streams()
 
 
 def run_pipeline_generate(cfg, source, prompts: Optional[torch.Tensor], n_new: int, rank: int, world: int,
@@ -409,9 +438,11 @@ def drive_local_pipeline(cfg, source, prompts: torch.Tensor, n_new: int, n_stage
 
 
 def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int = 64, warmup: int = 8,
-                         batch: int = 16, prompt_len: int = 128, max_seq: int = 1024,
+                         batch: int = 16, prompt_len: int = 128, max_seq: int = 0,
                          microbatches: int = 0, seed: int = 0, use_graph: bool = True,
-                         verbose: bool = True, weight_dtype: str = "bf16") -> Optional[dict]:
+                         verbose: bool = True, weight_dtype: str = "bf16", streams: int = 1) -> Optional[dict]:
+    """``microbatches`` 0 = ``streams`` x stages (every GPU holds ``streams`` micro-batches of
+    ``batch`` sequences: weak scaling); ``max_seq`` 0 = what the run needs, rounded up to 64."""
     cfg = get_preset(model)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -426,10 +457,11 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
-    M = microbatches or world
+    M = microbatches or streams * world
+    need = prompt_len + warmup + steps + 1
+    max_seq = max_seq or -(-need // 64) * 64
     plan = plan_stages(cfg, world, kv_tokens=max_seq * batch * M, head_split=world > 1)
     st = plan.stages[rank]
-    need = prompt_len + warmup + steps + 1
     if need > max_seq:
         raise ValueError(f"prompt+warmup+steps ({need}) exceeds max_seq {max_seq}")
     if verbose and rank == 0:
@@ -437,7 +469,7 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
     t0 = time.perf_counter()
     stage = PipelineStage(cfg, rank, world, st.start, st.end, dev, batch, M, max_seq,
                           RandomSource(cfg, seed), use_graph=use_graph,
-                          max_prefill_rows=batch * prompt_len, weight_dtype=weight_dtype)
+                          max_prefill_rows=batch * prompt_len, weight_dtype=weight_dtype, streams=streams)
     torch.cuda.synchronize()
     load_s = time.perf_counter() - t0
     if dist:
@@ -507,6 +539,8 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
         "ttft_ms": ttft_ms,
         "global_batch": M * batch,
         "microbatches": M,
+        "streams": stage.S,
+        "max_seq": max_seq,
         "model_name": "Llama-2-7B" if model == "llama2-7b" else cfg.name,
         "load_s": load_s,
         "plan": plan.ranges(),

@@ -23,6 +23,7 @@ from __future__ import annotations
 
 import math
 import os
+from contextlib import contextmanager
 from dataclasses import dataclass
 from typing import Callable, Optional
 
@@ -220,6 +221,7 @@ class StageEngine:
         self.v_cache: list = []
         self.seq_len = [0] * self.max_slots  # host-side KV length per slot
         self._graphs: dict = {}
+        self._scratch: dict = {}  # decode scratch sets of concurrent graphs (decode_scratch)
         if self.gpu:
             from ..ops import hip as _hip  # noqa: F401  (fail loudly if the .so is missing)
             _hip.lib()
@@ -363,6 +365,49 @@ class StageEngine:
             self.w_scratch = None
             if self.fp8:  # one projection's bf16 weights, for the >64-row paths
                 self.w_scratch = torch.empty(max(n * k for n, k in shapes), dtype=torch.bfloat16, device=dev)
+
+    # buffers a forward pass writes besides the KV cache: one set per concurrently running graph
+    SCRATCH_ATTRS = ("buf_h", "buf_xn", "buf_q", "buf_attn", "buf_act", "part_o", "part_lse", "attn_cnt",
+                     "coop_ws", "w_scratch")
+
+    def decode_scratch(self, k: int) -> dict:
+        """Scratch set ``k`` for decode graphs that run CONCURRENTLY on different streams (a
+        hipGraph bakes in its buffer addresses, so two graphs replayed at once must not share
+        activations, attention partials or split-K tickets). Set 0 is the engine's own; sets
+        k >= 1 are allocated on first use, sized for DECODE_MAX_ROWS rows."""
+        if k == 0:
+            return {a: getattr(self, a) for a in self.SCRATCH_ATTRS}
+        if k not in self._scratch:
+            from ..ops import hip
+            cfg, dev, bf, R = self.cfg, self.device, torch.bfloat16, self.DECODE_MAX_ROWS
+            H, I, nh, hd = cfg.hidden_size, cfg.intermediate_size, cfg.num_attention_heads, cfg.head_dim
+            ws_rows = R * self.max_decode_nsplit
+            self._scratch[k] = {
+                "buf_h": torch.zeros((R, H), dtype=bf, device=dev),
+                "buf_xn": torch.zeros((R, H), dtype=bf, device=dev),
+                "buf_q": torch.zeros((R, cfg.q_size), dtype=bf, device=dev),
+                "buf_attn": torch.zeros((R, cfg.q_size), dtype=bf, device=dev),
+                "buf_act": torch.zeros((R, I), dtype=bf, device=dev),
+                "part_o": torch.zeros(ws_rows * nh * hd, dtype=torch.float32, device=dev),
+                "part_lse": torch.zeros(ws_rows * nh, dtype=torch.float32, device=dev),
+                "attn_cnt": torch.zeros(ws_rows * cfg.num_key_value_heads, dtype=torch.int32, device=dev),
+                "coop_ws": hip.CoopWorkspace(dev, slab_floats=self.coop_ws.slab.numel(),
+                                             groups=self.coop_ws.counters.numel()),
+                "w_scratch": None if self.w_scratch is None else torch.empty_like(self.w_scratch),
+            }
+        return self._scratch[k]
+
+    @contextmanager
+    def use_scratch(self, k: int):
+        """Run (capture) forward passes against scratch set ``k``."""
+        saved = {a: getattr(self, a) for a in self.SCRATCH_ATTRS}
+        for a, v in self.decode_scratch(k).items():
+            setattr(self, a, v)
+        try:
+            yield
+        finally:
+            for a, v in saved.items():
+                setattr(self, a, v)
 
     def memory_bytes(self) -> int:
         n = 0
@@ -745,7 +790,7 @@ class DecodeGraph:
     """
 
     def __init__(self, eng: StageEngine, rows: int, mode: str, slots: Optional[list] = None,
-                 history_len: int = 0, split_head: bool = False):
+                 history_len: int = 0, split_head: bool = False, scratch: int = 0):
         from ..ops import hip
         if not eng.gpu:
             raise RuntimeError("DecodeGraph needs a GPU stage")
@@ -753,6 +798,9 @@ class DecodeGraph:
             raise ValueError(f"decode graph supports <= {eng.DECODE_MAX_ROWS} rows")
         self.eng, self.rows, self.mode = eng, rows, mode
         dev = eng.device
+        # scratch set (StageEngine.decode_scratch): graphs replayed concurrently need distinct sets
+        self.scratch = scratch
+        self._out = eng.decode_scratch(scratch)["buf_h"][:rows]
         self.slots = list(range(rows)) if slots is None else list(slots)
         self.slot = torch.tensor(self.slots, dtype=torch.int32, device=dev)
         self.pos = torch.tensor([eng.seq_len[s] for s in self.slots], dtype=torch.int32, device=dev)
@@ -774,6 +822,10 @@ class DecodeGraph:
             self.keys_in = torch.zeros(rows, dtype=torch.int64, device=dev)
 
     def _body(self) -> None:
+        with self.eng.use_scratch(self.scratch):
+            self._step()
+
+    def _step(self) -> None:
         hip, eng, rows = self._hip, self.eng, self.rows
         h = eng.buf_h[:rows]
         if self.split_head and self.mode == "first":
@@ -799,7 +851,7 @@ class DecodeGraph:
 
     @property
     def out_hidden(self) -> torch.Tensor:
-        return self.eng.buf_h[:self.rows]
+        return self._out
 
     def capture(self, warmup: bool = True) -> "DecodeGraph":
         """Capture the step. The warm-up replay (if any) is undone (positions restored)."""
