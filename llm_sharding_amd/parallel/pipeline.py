@@ -18,6 +18,7 @@ steps. Hidden states go rank r -> r+1 over xGMI, token ids go last -> 0 (the rin
 """
 from __future__ import annotations
 
+import contextlib
 import os
 import time
 from typing import Optional
@@ -84,14 +85,22 @@ class LocalP2P:
             self.hub, self.rank = hub, rank
 
         def isend(self, t, dst):
-            self.hub.boxes.setdefault((self.rank, dst), []).append(t.clone())
+            # snapshot on the sender's current stream; the receiver's stream waits on its event
+            ev = None
+            if t.is_cuda:
+                ev = torch.cuda.Event()
+                ev.record()
+            self.hub.boxes.setdefault((self.rank, dst), []).append((t.clone(), ev))
             return LocalP2P._Done()
 
         def recv(self, t, src):
             box = self.hub.boxes.get((src, self.rank))
             if not box:
                 raise RuntimeError(f"local p2p: no message from stage {src} to {self.rank} (drive order?)")
-            t.copy_(box.pop(0))
+            snap, ev = box.pop(0)
+            if ev is not None:
+                torch.cuda.current_stream(t.device).wait_event(ev)
+            t.copy_(snap)
 
 
 def _percentile(xs, q):
@@ -109,7 +118,8 @@ class PipelineStage:
     def __init__(self, cfg, rank: int, world: int, start: int, end: int, device, batch: int,
                  microbatches: int, max_seq: int, source, use_graph: bool = True,
                  max_prefill_rows: int = 2048, dtype=torch.bfloat16, p2p=None,
-                 split_head: Optional[bool] = None, weight_dtype: str = "bf16", streams: int = 1):
+                 split_head: Optional[bool] = None, weight_dtype: str = "bf16", streams: int = 1,
+                 pp_streams: Optional[bool] = None):
         self.cfg, self.rank, self.world = cfg, rank, world
         self.p2p = p2p if p2p is not None else DistP2P()
         self.first, self.last = rank == 0, rank == world - 1
@@ -150,10 +160,16 @@ class PipelineStage:
         # stream mb % S with its own scratch set, so up to S decode graphs share the GPU at once.
         # A Llama-2-7B decode graph alone leaves CUs idle (its projections have too few tiles to
         # fill 256 CUs), and S graphs side by side raise throughput (scripts/concurrency_probe.py).
-        # Multi-stage pipelines keep one compute stream: their RCCL p2p kernels wait on peers,
-        # and more streams than the process's hardware queues would multiplex a blocked p2p
-        # kernel in front of compute it depends on.
-        self.S = max(1, min(streams, microbatches)) if (self.gpu and world == 1 and self.use_graph) else 1
+        # Multi-stage pipelines do the same (``pp_streams``; LSA_PP_STREAMS=0 keeps one compute
+        # stream per stage): every GPU enqueues its p2p and compute work in one global (step,
+        # micro-batch) order on every stream, and each op waits only on ops of an equal or
+        # earlier (step, micro-batch) on any GPU, so the waits-for relation stays acyclic however
+        # streams share hardware queues. Exercised in-process (LocalP2P + stream events, GPU tests)
+        # and over gloo; RCCL between GPUs adds per-edge FIFO ordering, which the same order meets.
+        if pp_streams is None:
+            pp_streams = os.environ.get("LSA_PP_STREAMS", "1") == "1"
+        multi = world == 1 or pp_streams
+        self.S = max(1, min(streams, microbatches)) if (self.gpu and self.use_graph and multi) else 1
         self.streams = [torch.cuda.Stream(self.device) for _ in range(self.S)] if self.S > 1 else []
 
     # ---------------------------------------------------------------- p2p helpers
@@ -276,17 +292,18 @@ class PipelineStage:
 
     def step(self, s: int, events: Optional[list] = None) -> None:
         """One decode step for every micro-batch (the host never blocks on the GPU here)."""
-        if self.S > 1:
-            cur = torch.cuda.current_stream(self.device)
-            for mb in range(self.M):
-                st = self.streams[mb % self.S]
-                if mb < self.S:
-                    st.wait_stream(cur)  # ordered after whatever the caller enqueued before
-                with torch.cuda.stream(st):
-                    self.step_mb(s, mb, events)
-            return
         for mb in range(self.M):
             self.step_mb(s, mb, events)
+
+    def _mb_stream(self, mb: int):
+        """Stream context of micro-batch ``mb`` (concurrent mode), ordered after whatever the
+        caller enqueued on its current stream before."""
+        if self.S == 1:
+            return contextlib.nullcontext()
+        st = self.streams[mb % self.S]
+        if mb < self.S:
+            st.wait_stream(torch.cuda.current_stream(self.device))
+        return torch.cuda.stream(st)
 
     def join_streams(self) -> None:
         """Make the current stream wait for the concurrent micro-batch streams."""
@@ -295,6 +312,10 @@ class PipelineStage:
             cur.wait_stream(st)
 
     def step_mb(self, s: int, mb: int, events: Optional[list] = None) -> None:
+        with self._mb_stream(mb):
+            self._step_mb(s, mb, events)
+
+    def _step_mb(self, s: int, mb: int, events: Optional[list] = None) -> None:
         g = self.graphs[mb]
         tl = self.tl
         if self.world > 1:
@@ -341,23 +362,28 @@ class PipelineStage:
         if self.world > 1 and self.first:
             for mb, g in enumerate(self.graphs):
                 if not self.tokens_ready[mb]:
-                    if self.split:
-                        # the last step's keys: complete them eagerly; the inputs stay in
-                        # place, so a later replay re-derives the same token first
-                        self._recv(g.h_fin, self.world - 1)
-                        self._recv(g.keys_in, self.world - 1)
-                        self.final_tokens[mb] = self._complete(g.h_fin, g.keys_in)
-                    else:
-                        self._recv(g.tokens, self.world - 1)
-                    self.tokens_ready[mb] = True
+                    with self._mb_stream(mb), (self.eng.use_scratch(mb % self.S) if self.S > 1
+                                               else contextlib.nullcontext()):
+                        self._drain_mb(mb, g)
         for k in list(self.send_works):
             self._wait_send(k)
         self.join_streams()
 
+    def _drain_mb(self, mb: int, g) -> None:
+        if self.split:
+            # the last step's keys: complete them eagerly; the inputs stay in place, so a later
+            # replay re-derives the same token first
+            self._recv(g.h_fin, self.world - 1)
+            self._recv(g.keys_in, self.world - 1)
+            self.final_tokens[mb] = self._complete(g.h_fin, g.keys_in)
+        else:
+            self._recv(g.tokens, self.world - 1)
+        self.tokens_ready[mb] = True
+
 
 def run_pipeline_generate(cfg, source, prompts: Optional[torch.Tensor], n_new: int, rank: int, world: int,
                           device="cpu", batch: int = 1, microbatches: int = 1, max_seq: int = 256,
-                          plan=None, dtype=torch.float32) -> Optional[torch.Tensor]:
+                          plan=None, dtype=torch.float32, streams: int = 1) -> Optional[torch.Tensor]:
     """Greedy generation through the micro-batched pipeline (torch.distributed already
     initialised; gloo on CPU or nccl/RCCL on GPUs). ``prompts`` [M, B, P] on rank 0.
     Returns [n_new, M, B] generated ids on rank 0 (gathered from the last stage)."""
@@ -370,7 +396,7 @@ def run_pipeline_generate(cfg, source, prompts: Optional[torch.Tensor], n_new: i
         dist.broadcast(pl, 0)
         P = int(pl[0])
     stage = PipelineStage(cfg, rank, world, st.start, st.end, device, batch, microbatches, max_seq, source,
-                          use_graph=True, max_prefill_rows=batch * P, dtype=dtype)
+                          use_graph=True, max_prefill_rows=batch * P, dtype=dtype, streams=streams)
     firsts = stage.prefill(prompts, P)
     stage.build_graphs(firsts, history_len=n_new - 1)
     for s in range(n_new - 1):
@@ -402,7 +428,7 @@ def run_pipeline_generate(cfg, source, prompts: Optional[torch.Tensor], n_new: i
 
 def drive_local_pipeline(cfg, source, prompts: torch.Tensor, n_new: int, n_stages: int, device,
                          batch: int = 1, microbatches: int = 1, max_seq: int = 256, plan=None,
-                         dtype=torch.bfloat16, use_graph: bool = True) -> torch.Tensor:
+                         dtype=torch.bfloat16, use_graph: bool = True, streams: int = 1) -> torch.Tensor:
     """All stages of a pipeline in ONE process (one device), connected by :class:`LocalP2P`
     and driven in pipeline order. Same PipelineStage code as the multi-process RCCL path."""
     if n_stages < 2:
@@ -411,7 +437,8 @@ def drive_local_pipeline(cfg, source, prompts: torch.Tensor, n_new: int, n_stage
     hub = LocalP2P()
     P = int(prompts.shape[-1])
     stages = [PipelineStage(cfg, r, n_stages, st.start, st.end, device, batch, microbatches, max_seq, source,
-                            use_graph=use_graph, max_prefill_rows=batch * P, dtype=dtype, p2p=hub.bind(r))
+                            use_graph=use_graph, max_prefill_rows=batch * P, dtype=dtype, p2p=hub.bind(r),
+                            streams=streams, pp_streams=streams > 1)
               for r, st in enumerate(plan.stages)]
     firsts = []
     for mb in range(microbatches):

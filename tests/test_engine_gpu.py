@@ -131,10 +131,11 @@ def test_decode_graph_matches_eager():
     assert e2.seq_len == e1.seq_len
 
 
-@pytest.mark.parametrize("n_stages", [2, 4])
-def test_multistage_on_one_gpu_graphs(n_stages):
+@pytest.mark.parametrize("n_stages,streams", [(2, 1), (4, 1), (2, 2), (4, 3)])
+def test_multistage_on_one_gpu_graphs(n_stages, streams):
     """The pipelined micro-batch decode (hipGraph per stage/micro-batch, local device-copy
-    hand-off) generates exactly what the single-stage graph loop generates."""
+    hand-off with stream events; optionally micro-batches on concurrent streams in every stage)
+    generates exactly what the single-stage graph loop generates."""
     from llm_sharding_amd.parallel.pipeline import drive_local_pipeline, run_pipeline_generate
     cfg = tiny(layers=8)
     src = RandomSource(cfg, seed=21)
@@ -142,8 +143,24 @@ def test_multistage_on_one_gpu_graphs(n_stages):
     prompts = torch.randint(3, cfg.vocab_size, (3, 4, 9), generator=g)
     single = run_pipeline_generate(cfg, src, prompts, 10, 0, 1, device=DEV, batch=4, microbatches=3, max_seq=64,
                                    dtype=torch.bfloat16)
-    multi = drive_local_pipeline(cfg, src, prompts, 10, n_stages, DEV, batch=4, microbatches=3, max_seq=64)
+    multi = drive_local_pipeline(cfg, src, prompts, 10, n_stages, DEV, batch=4, microbatches=3, max_seq=64,
+                                 streams=streams)
     assert multi.tolist() == single.tolist()
+
+
+def test_concurrent_microbatch_streams_match_serial():
+    """Micro-batches replayed concurrently on 3 HIP streams (one scratch set each) generate
+    exactly the tokens of the one-stream loop (Llama-2-7B layer shapes: coop GEMV split-K
+    tickets and attention merges must not be shared between concurrently running graphs)."""
+    from llm_sharding_amd.parallel.pipeline import run_pipeline_generate
+    cfg = LlamaConfig(num_hidden_layers=2, vocab_size=32000, max_position_embeddings=512, name="7B-2L")
+    src = RandomSource(cfg, seed=4)
+    g = torch.Generator().manual_seed(8)
+    prompts = torch.randint(3, cfg.vocab_size, (4, 40, 12), generator=g)
+    kw = dict(device=DEV, batch=40, microbatches=4, max_seq=64, dtype=torch.bfloat16)
+    serial = run_pipeline_generate(cfg, src, prompts, 12, 0, 1, streams=1, **kw)
+    conc = run_pipeline_generate(cfg, src, prompts, 12, 0, 1, streams=3, **kw)
+    assert conc.tolist() == serial.tolist()
 
 
 def test_node_worker_chain_on_gpu(tiny_shards_bf16):
