@@ -11,9 +11,11 @@ a rank:
     irecv(hidden | token ids)  ->  stream-wait  ->  replay the micro-batch's hipGraph
     (layers [+ embed] [+ final-norm/lm_head/argmax])  ->  isend(hidden | token ids)
 
-The RCCL p2p ops run on the NCCL stream and are ordered against the compute stream by
-events (no host synchronisation per token); the host only throttles its run-ahead to two
-steps. Hidden states go rank r -> r+1 over xGMI, token ids go last -> 0 (the ring back-edge,
+The RCCL p2p ops run on the NCCL streams (one communicator per ring edge) and are ordered
+against the compute streams by events - no host synchronisation per token; the host runs
+ahead until the HIP queues fill. Micro-batch mb runs on compute stream mb % S (S concurrent
+streams per stage, each with its own engine scratch set), so S decode graphs share a GPU at
+once. Hidden states go rank r -> r+1 over xGMI, token ids go last -> 0 (the ring back-edge,
 ``receive_next_token`` with the embedding co-located on the first stage).
 """
 from __future__ import annotations
