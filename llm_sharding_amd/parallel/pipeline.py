@@ -265,21 +265,19 @@ class PipelineStage:
         self.mode = mode
         self.graphs = []
         for mb in range(self.M):
+            # micro-batches that share a stream replay one after another: one scratch set each
+            extra = {"scratch": mb % self.S} if self.gpu else {}
+            cls = DecodeGraph if self.gpu else EagerDecode
             if self.split and mode in ("first", "last"):
                 # stage 0 re-derives token s at step s: one more history row than the last stage keeps
-                cls = DecodeGraph if self.gpu else EagerDecode
                 g = cls(self.eng, self.B, mode, slots=self.slots(mb),
-                        history_len=history_len + 1 if self.first else 0, split_head=True)
+                        history_len=history_len + 1 if self.first else 0, split_head=True, **extra)
                 if self.first and self.seed[mb] is not None:
                     g.h_fin.copy_(self.seed[mb][0])
                     g.keys_in.copy_(self.seed[mb][1])
             else:
-                if self.gpu:
-                    g = DecodeGraph(self.eng, self.B, mode, slots=self.slots(mb),
-                                    history_len=history_len if self.last else 0, scratch=mb % self.S)
-                else:
-                    g = EagerDecode(self.eng, self.B, mode, slots=self.slots(mb),
-                                    history_len=history_len if self.last else 0)
+                g = cls(self.eng, self.B, mode, slots=self.slots(mb),
+                        history_len=history_len if self.last else 0, **extra)
                 if first_tokens is not None and mode in ("full", "first"):
                     g.tokens.copy_(first_tokens[mb])
             if self.use_graph:

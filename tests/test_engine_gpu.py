@@ -163,6 +163,21 @@ def test_concurrent_microbatch_streams_match_serial():
     assert conc.tolist() == serial.tolist()
 
 
+def test_multistage_concurrent_streams_7b_shapes():
+    """Two pipeline stages (split lm_head, stream-event hand-off) whose micro-batches run on 3
+    concurrent streams, at Llama-2-7B layer shapes (kernels long enough to overlap): same tokens
+    as the one-stage, one-stream loop."""
+    from llm_sharding_amd.parallel.pipeline import drive_local_pipeline, run_pipeline_generate
+    cfg = LlamaConfig(num_hidden_layers=4, vocab_size=32000, max_position_embeddings=512, name="7B-4L")
+    src = RandomSource(cfg, seed=6)
+    g = torch.Generator().manual_seed(9)
+    prompts = torch.randint(3, cfg.vocab_size, (4, 40, 10), generator=g)
+    single = run_pipeline_generate(cfg, src, prompts, 10, 0, 1, device=DEV, batch=40, microbatches=4, max_seq=64,
+                                   dtype=torch.bfloat16)
+    multi = drive_local_pipeline(cfg, src, prompts, 10, 2, DEV, batch=40, microbatches=4, max_seq=64, streams=3)
+    assert multi.tolist() == single.tolist()
+
+
 def test_node_worker_chain_on_gpu(tiny_shards_bf16):
     """Reference-API NodeWorkers on the GPU (tcp hand-off on loopback) == single-stage engine."""
     import socket
