@@ -34,7 +34,13 @@ def main():
         eng.seq_len[s] = 128
     gs = [DecodeGraph(eng, rows, "full", slots=list(range(k * rows, (k + 1) * rows)), scratch=k).capture()
           for k in range(nstreams)]
-    streams = [torch.cuda.Stream(dev) for _ in range(nstreams)]
+    mode = sys.argv[3] if len(sys.argv) > 3 else "pool"
+    if mode == "prio":      # high-priority pool (a different set of HW queues)
+        streams = [torch.cuda.Stream(dev, priority=-1) for _ in range(nstreams)]
+    elif mode == "skip":    # every other pool stream
+        streams = [torch.cuda.Stream(dev) for _ in range(2 * nstreams)][::2]
+    else:
+        streams = [torch.cuda.Stream(dev) for _ in range(nstreams)]
     reps = 12
     one = timed(lambda: gs[0].replay(), reps)
     serial = timed(lambda: [g.replay() for g in gs], reps)
@@ -49,7 +55,7 @@ def main():
         for st in streams:
             cur.wait_stream(st)
     concurrent = timed(conc, reps)
-    print(json.dumps({"rows_per_graph": rows, "graphs": nstreams, "one_graph_ms": round(one, 3),
+    print(json.dumps({"rows_per_graph": rows, "graphs": nstreams, "stream_mode": mode, "one_graph_ms": round(one, 3),
                       "serial_ms": round(serial, 3), "concurrent_ms": round(concurrent, 3),
                       "tok_s_one": round(rows / one * 1e3), "tok_s_serial": round(rows * nstreams / serial * 1e3),
                       "tok_s_concurrent": round(rows * nstreams / concurrent * 1e3)}), flush=True)
