@@ -467,23 +467,35 @@ def drive_local_pipeline(cfg, source, prompts: torch.Tensor, n_new: int, n_stage
 def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int = 64, warmup: int = 8,
                          batch: int = 16, prompt_len: int = 128, max_seq: int = 0,
                          microbatches: int = 0, seed: int = 0, use_graph: bool = True,
-                         verbose: bool = True, weight_dtype: str = "bf16", streams: int = 1) -> Optional[dict]:
+                         verbose: bool = True, weight_dtype: str = "bf16", streams: int = 1,
+                         device: str = "cuda") -> Optional[dict]:
     """``microbatches`` 0 = ``streams`` x stages (every GPU holds ``streams`` micro-batches of
     ``batch`` sequences: weak scaling); ``max_seq`` 0 = what the run needs, rounded up to 64."""
     cfg = get_preset(model)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    # one rank per visible GPU; modulo the device count so a 1-GPU box can rehearse the
-    # multi-rank RCCL path (identity on an 8-GPU node)
-    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     if n_gpus != world:
         raise ValueError(f"n_gpus={n_gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # device "cpu": the same flow on gloo + the torch CPU path (rehearsal of the multi-rank
+    # schedule in CPU tests); otherwise one rank per GPU over RCCL
+    gpu = device != "cpu"
+    if gpu:
+        local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+    else:
+        dev = torch.device("cpu")
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if gpu:
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+
+    def sync():
+        if gpu:
+            torch.cuda.synchronize()
     M = microbatches or streams * world
     need = prompt_len + warmup + steps + 1
     max_seq = max_seq or -(-need // 64) * 64
@@ -496,8 +508,9 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
     t0 = time.perf_counter()
     stage = PipelineStage(cfg, rank, world, st.start, st.end, dev, batch, M, max_seq,
                           RandomSource(cfg, seed), use_graph=use_graph,
-                          max_prefill_rows=batch * prompt_len, weight_dtype=weight_dtype, streams=streams)
-    torch.cuda.synchronize()
+                          max_prefill_rows=batch * prompt_len, weight_dtype=weight_dtype, streams=streams,
+                          dtype=torch.bfloat16 if gpu else torch.float32)
+    sync()
     load_s = time.perf_counter() - t0
     if dist:
         dist.barrier()
@@ -506,23 +519,23 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
     if stage.first:
         g = torch.Generator().manual_seed(seed + 1)
         prompts = torch.randint(3, cfg.vocab_size, (M, batch, prompt_len), generator=g, dtype=torch.int32)
-    torch.cuda.synchronize()
+    sync()
     tp0 = time.perf_counter()
     firsts = stage.prefill(prompts, prompt_len)
-    torch.cuda.synchronize()
+    sync()
     ttft_ms = (time.perf_counter() - tp0) * 1e3 / M  # per micro-batch prefill through the pipeline
     stage.build_graphs(firsts, history_len=warmup + steps)
-    torch.cuda.synchronize()
+    sync()
     if dist:
         dist.barrier()
 
     for s in range(warmup):
         stage.step(s)
     stage.drain()
-    torch.cuda.synchronize()
+    sync()
     if dist:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     stage.tl.spans.clear()
     stage.tl.start()  # ranks aligned on the barrier above
     events: list = []
@@ -530,10 +543,10 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
     for s in range(steps):
         stage.step(warmup + s, events if stage.last else None)
     stage.drain()
-    torch.cuda.synchronize()
+    sync()
     if dist:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     elapsed = time.perf_counter() - t_start
 
     # per-token latency of each sequence = time between its consecutive tokens (last stage)
@@ -547,6 +560,8 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
                 tpot.append(a.elapsed_time(b))
     stats = torch.tensor([elapsed, ttft_ms, _percentile(tpot, 0.5) if tpot else 0.0,
                           _percentile(tpot, 0.9) if tpot else 0.0, load_s], dtype=torch.float64, device=dev)
+    if not gpu and stage.last:  # no device events on CPU: wall-clock step time stands in for TPOT
+        stats[2] = stats[3] = elapsed * 1e3 / steps
     if dist:
         gathered = [torch.zeros_like(stats) for _ in range(world)]
         dist.all_gather(gathered, stats)

@@ -110,3 +110,37 @@ def test_local_multistage_matches_single(n_stages, single):
     out = drive_local_pipeline(cfg, RandomSource(cfg, seed=7), _prompts(cfg), NEW, n_stages, "cpu",
                                batch=B, microbatches=M, max_seq=64, dtype=torch.float32)
     assert out.tolist() == single
+
+
+def _bench_worker(rank, world, port, q):
+    """bench.py's driver (run_decode_benchmark) on gloo/CPU: the exact multi-rank schedule of
+    the N-GPU headline run - prefill, warm-up, drain, timed steps, drain, stats gather."""
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    torch.set_num_threads(1)
+    from llm_sharding_amd.parallel.pipeline import run_decode_benchmark
+    res = run_decode_benchmark(model="tiny", n_gpus=world, steps=3, warmup=2, batch=2, prompt_len=4,
+                               streams=2, device="cpu", verbose=False)
+    if rank == 0:
+        q.put(res)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_driver_multi_rank_cpu(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_bench_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    try:
+        res = q.get(timeout=240)
+    finally:
+        for p in ps:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+    assert res["microbatches"] == 2 * world and res["global_batch"] == 4 * world
+    assert res["tok_s"] > 0 and res["ms_per_step"] > 0 and res["p50_tpot_ms"] > 0
+    assert len(res["plan"]) == world
