@@ -25,6 +25,7 @@ which keeps the graph static.
 """
 from __future__ import annotations
 
+import contextlib
 import queue
 import threading
 import time
@@ -102,7 +103,7 @@ class PipelineServer:
     def __init__(self, cfg, source, rank: int = 0, world: int = 1, start: int = 0, end: Optional[int] = None,
                  device="cpu", batch: int = 8, microbatches: int = 1, max_seq: int = 2048,
                  prefill_budget: int = 2048, use_graph: bool = True, dtype=torch.bfloat16,
-                 ctrl_group=None, p2p=None, causal: bool = True, verbose: bool = False):
+                 ctrl_group=None, p2p=None, causal: bool = True, verbose: bool = False, streams: int = 1):
         self.cfg, self.rank, self.world = cfg, rank, world
         end = cfg.num_hidden_layers if end is None else end
         self.first, self.last = rank == 0, rank == world - 1
@@ -120,10 +121,21 @@ class PipelineServer:
         self.ctrl = ctrl_group
         self.hdr = _Header(batch)
         self.graphs: List = []
+        # Concurrent micro-batches (one GPU, graph mode): every command of micro-batch mb -
+        # prefill, decode replay, result collection - runs on stream mb % S against engine
+        # scratch set mb % S (sized for the prefill budget), so up to S micro-batches share the
+        # GPU at once (see pipeline.PipelineStage); a micro-batch's own commands stay ordered.
+        self.S = max(1, min(streams, microbatches)) if (self.graph_mode and world == 1) else 1
+        self.streams = [torch.cuda.Stream(self.device) for _ in range(self.S)] if self.S > 1 else []
+        for k in range(1, self.S):
+            self.eng.decode_scratch(k, rows=self.eng.max_prefill_rows)
         if self.graph_mode:
             mode = "full" if world == 1 else ("first" if self.first else ("last" if self.last else "mid"))
             for mb in range(microbatches):
-                self.graphs.append(DecodeGraph(self.eng, batch, mode, slots=self._slots(mb)).capture())
+                self.graphs.append(DecodeGraph(self.eng, batch, mode, slots=self._slots(mb),
+                                               scratch=mb % self.S).capture())
+        for st in self.streams:  # after weight loading and graph capture on the current stream
+            st.wait_stream(torch.cuda.current_stream(self.device))
         # rank 0 state
         self.incoming: "queue.Queue[Request]" = queue.Queue()
         self.waiting: List[Request] = []
@@ -142,6 +154,15 @@ class PipelineServer:
         self.tl = tracing.from_env(rank, self.device)  # LSA_TRACE=dir -> per-rank Chrome trace
 
     # ------------------------------------------------------------------ helpers
+    def _mb_ctx(self, mb: int):
+        """Stream + engine scratch set of micro-batch ``mb`` (no-op with one stream)."""
+        if self.S == 1:
+            return contextlib.nullcontext()
+        es = contextlib.ExitStack()
+        es.enter_context(torch.cuda.stream(self.streams[mb % self.S]))
+        es.enter_context(self.eng.use_scratch(mb % self.S))
+        return es
+
     def _slots(self, mb: int) -> list:
         return list(range(mb * self.B, (mb + 1) * self.B))
 
@@ -195,7 +216,7 @@ class PipelineServer:
     def _exec(self, cmd, mb, items, resets, ids=None):
         """Run one command on this stage. Returns the last stage's token ids (world == 1)."""
         name = {CMD_PREFILL: "prefill", CMD_DECODE: "decode"}.get(cmd, "cmd")
-        with self.tl.span(name, mb=mb, items=len(items)):
+        with self.tl.span(name, mb=mb, items=len(items)), self._mb_ctx(mb):
             return self._exec_body(cmd, mb, items, resets, ids)
 
     def _exec_body(self, cmd, mb, items, resets, ids=None):
@@ -319,6 +340,10 @@ class PipelineServer:
 
     def _collect(self, mb: int) -> None:
         """Receive/process the return of micro-batch ``mb``'s outstanding command."""
+        with self._mb_ctx(mb):
+            self._collect_body(mb)
+
+    def _collect_body(self, mb: int) -> None:
         o = self.outstanding[mb]
         if o is None:
             return
@@ -412,8 +437,9 @@ class PipelineServer:
         self.pending_resets[mb] = []
         self._bcast_header(hdr)
         if not run:
-            for s in resets:
-                self._set_pos(s, 0)
+            with self._mb_ctx(mb):
+                for s in resets:
+                    self._set_pos(s, 0)
             return
         local = self._exec(cmd, mb, items, resets, ids=ids)
         self.outstanding[mb] = (cmd, info, local)

@@ -368,20 +368,24 @@ class StageEngine:
 
     # buffers a forward pass writes besides the KV cache: one set per concurrently running graph
     SCRATCH_ATTRS = ("buf_h", "buf_xn", "buf_q", "buf_attn", "buf_act", "part_o", "part_lse", "attn_cnt",
-                     "coop_ws", "w_scratch")
+                     "coop_ws", "w_scratch", "keys", "tokens", "ws_rows")
 
-    def decode_scratch(self, k: int) -> dict:
-        """Scratch set ``k`` for decode graphs that run CONCURRENTLY on different streams (a
+    def decode_scratch(self, k: int, rows: Optional[int] = None) -> dict:
+        """Scratch set ``k`` for forward passes that run CONCURRENTLY on different streams (a
         hipGraph bakes in its buffer addresses, so two graphs replayed at once must not share
         activations, attention partials or split-K tickets). Set 0 is the engine's own; sets
-        k >= 1 are allocated on first use, sized for DECODE_MAX_ROWS rows."""
+        k >= 1 are allocated on first use for ``rows`` rows (default: a decode graph's
+        DECODE_MAX_ROWS; a server that also prefills on the set asks for its prefill budget)."""
         if k == 0:
             return {a: getattr(self, a) for a in self.SCRATCH_ATTRS}
+        R = max(self.DECODE_MAX_ROWS, rows or 0)
+        if k in self._scratch and self._scratch[k]["buf_h"].shape[0] < R:
+            raise ValueError(f"scratch set {k} was allocated for fewer than {R} rows")
         if k not in self._scratch:
             from ..ops import hip
-            cfg, dev, bf, R = self.cfg, self.device, torch.bfloat16, self.DECODE_MAX_ROWS
+            cfg, dev, bf = self.cfg, self.device, torch.bfloat16
             H, I, nh, hd = cfg.hidden_size, cfg.intermediate_size, cfg.num_attention_heads, cfg.head_dim
-            ws_rows = R * self.max_decode_nsplit
+            ws_rows = max(self.DECODE_MAX_ROWS * self.max_decode_nsplit, R * 4 if R > self.DECODE_MAX_ROWS else 0)
             self._scratch[k] = {
                 "buf_h": torch.zeros((R, H), dtype=bf, device=dev),
                 "buf_xn": torch.zeros((R, H), dtype=bf, device=dev),
@@ -394,6 +398,9 @@ class StageEngine:
                 "coop_ws": hip.CoopWorkspace(dev, slab_floats=self.coop_ws.slab.numel(),
                                              groups=self.coop_ws.counters.numel()),
                 "w_scratch": None if self.w_scratch is None else torch.empty_like(self.w_scratch),
+                "keys": torch.zeros(R, dtype=torch.int64, device=dev),
+                "tokens": torch.zeros(R, dtype=torch.int32, device=dev),
+                "ws_rows": ws_rows,
             }
         return self._scratch[k]
 

@@ -24,6 +24,7 @@ class RuntimeConfig:
     backend: str = "rccl"         # stage hand-off: rccl (torch.distributed/RCCL), tcp, local
     batch: int = 32               # KV slots per micro-batch (0 = as many as HBM holds, <= 128)
     microbatches: int = 0         # 0 = max(2, pipeline stages)
+    streams: int = 1              # one GPU: micro-batches on this many concurrent HIP streams
     max_seq: int = 2048
     prefill_budget: int = 2048    # prompt tokens per prefill command (longer prompts are chunked)
     max_new_tokens: int = 128

@@ -133,7 +133,8 @@ def main():
         log.info(f"{cfg.name}: {world} stage(s) {plan.ranges()}, {M} x {rc.batch} slots")
     srv = PipelineServer(cfg, source, rank, world, st.start, st.end, dev, batch=rc.batch, microbatches=M,
                          max_seq=rc.max_seq, prefill_budget=rc.prefill_budget, use_graph=rc.use_graph,
-                         dtype=rc.torch_dtype(dev) if gpu else torch.float32, ctrl_group=ctrl, causal=rc.causal)
+                         dtype=rc.torch_dtype(dev) if gpu else torch.float32, ctrl_group=ctrl, causal=rc.causal,
+                         streams=rc.streams)
     if rank != 0:
         srv.serve()
     elif a.requests:

@@ -305,6 +305,24 @@ def test_pipeline_server_graph_mode_on_gpu():
     assert agree / tot >= 0.8
 
 
+def test_pipeline_server_concurrent_streams_on_gpu():
+    """The server with micro-batches on 3 concurrent streams (prefill + decode + collection of a
+    micro-batch on its stream, one scratch set each) serves exactly what the one-stream server
+    serves, at Llama-2-7B layer shapes."""
+    from llm_sharding_amd.parallel.server import PipelineServer
+    cfg = LlamaConfig(num_hidden_layers=2, vocab_size=32000, max_position_embeddings=512, name="7B-2L")
+    g = torch.Generator().manual_seed(11)
+    prompts = [torch.randint(3, cfg.vocab_size, (n,), generator=g).tolist()
+               for n in (5, 40, 17, 3, 64, 9, 33, 12, 50, 7, 21, 2)]
+    outs = {}
+    for streams in (1, 3):
+        srv = PipelineServer(cfg, RandomSource(cfg, 3), device=DEV, batch=4, microbatches=3, max_seq=128,
+                             prefill_budget=64, use_graph=True, streams=streams)
+        assert srv.S == streams
+        outs[streams] = srv.generate(prompts, 10, eos_ids=())
+    assert outs[3] == outs[1]
+
+
 def test_fp8_weights_engine():
     """weight_dtype="fp8" (W8A16): prefill (dequantised scratch + bf16 GEMM), decode rows <= 64
     (native fp8 GEMV) and > 64 (scratch + coop) against the bf16 engine on the same weights."""
