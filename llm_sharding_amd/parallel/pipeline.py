@@ -87,12 +87,13 @@ class LocalP2P:
             self.hub, self.rank = hub, rank
 
         def isend(self, t, dst):
-            # snapshot on the sender's current stream; the receiver's stream waits on its event
-            ev = None
+            # snapshot on the sender's current stream, then an event behind the copy: the
+            # receiver's stream waits on it before reading the snapshot
+            snap, ev = t.clone(), None
             if t.is_cuda:
                 ev = torch.cuda.Event()
                 ev.record()
-            self.hub.boxes.setdefault((self.rank, dst), []).append((t.clone(), ev))
+            self.hub.boxes.setdefault((self.rank, dst), []).append((snap, ev))
             return LocalP2P._Done()
 
         def recv(self, t, src):
@@ -101,8 +102,12 @@ class LocalP2P:
                 raise RuntimeError(f"local p2p: no message from stage {src} to {self.rank} (drive order?)")
             snap, ev = box.pop(0)
             if ev is not None:
-                torch.cuda.current_stream(t.device).wait_event(ev)
-            t.copy_(snap)
+                cur = torch.cuda.current_stream(t.device)
+                cur.wait_event(ev)
+                t.copy_(snap)
+                snap.record_stream(cur)  # the allocator must not recycle it before this copy ran
+            else:
+                t.copy_(snap)
 
 
 def _percentile(xs, q):
