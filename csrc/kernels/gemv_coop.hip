@@ -335,15 +335,18 @@ __global__ __launch_bounds__(NW * KW * 64) void gemv_coop_kernel(
 #pragma unroll
       for (int r = 0; r < 4; ++r) red[(tl * MR + rb * 16 + (ln >> 4) * 4 + r) * 16 + (ln & 15)] = sum[j][r];
     }
-    if (NORM && tid < MR) {
-      float t2 = 0.f;
-      for (int q = 0; q < SK; ++q)
-        t2 += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(sr, ((q * G + g) * MR + tid) * 4, ss_base * 4, 16));
-      s_ss[tid] = t2;
+    if (NORM) {
+      for (int r = tid; r < MR; r += NTHR) {  // NTHR may be < MR (single-wave workgroups)
+        float t2 = 0.f;
+        for (int q = 0; q < SK; ++q)
+          t2 += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(sr, ((q * G + g) * MR + r) * 4, ss_base * 4, 16));
+        s_ss[r] = t2;
+      }
     }
     if (tid == 0) __hip_atomic_store(&counters[g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  if (EPI == EPI_ARGMAX && tid < MR) s_key[tid] = 0ull;
+  if (EPI == EPI_ARGMAX)
+    for (int r = tid; r < MR; r += NTHR) s_key[r] = 0ull;
   __syncthreads();
 
   auto rstd = [&](int mm) -> float { return NORM ? rsqrtf(s_ss[mm] / (float)K + eps) : 1.f; };
@@ -401,7 +404,7 @@ __global__ __launch_bounds__(NW * KW * 64) void gemv_coop_kernel(
     }
     if (EPI == EPI_ARGMAX) {
       __syncthreads();
-      if (tid < M) atomicMax(&ep.keys[tid], s_key[tid]);
+      for (int r = tid; r < M; r += NTHR) atomicMax(&ep.keys[r], s_key[r]);
     }
   }
 }
