@@ -492,11 +492,15 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
         dev = torch.device("cpu")
     dist = None
     if world > 1:
+        import datetime
+
         import torch.distributed as dist
+        # a stuck peer surfaces as an error after 5 minutes instead of the 10-minute default
+        tmo = datetime.timedelta(seconds=int(os.environ.get("LSA_DIST_TIMEOUT_S", "300")))
         if gpu:
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=tmo)
         else:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=tmo)
 
     def sync():
         if gpu:
