@@ -48,6 +48,9 @@ def parse():
                     help="micro-batches resident per GPU; on one GPU they replay concurrently on this many "
                          "HIP streams")
     ap.add_argument("--microbatches", type=int, default=0, help="0 = streams x pipeline stages")
+    ap.add_argument("--dp", type=int, default=1,
+                    help="data-parallel pipeline replicas (gpus/dp stages each); 1 = the reference's "
+                         "layout, one pipeline over all GPUs")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--json-out", default="")
@@ -70,7 +73,7 @@ def main():
     res = run_decode_benchmark(model=a.model, n_gpus=a.gpus, steps=a.steps, warmup=a.warmup,
                                batch=a.batch, prompt_len=a.prompt_len, max_seq=a.max_seq,
                                microbatches=a.microbatches, seed=a.seed, use_graph=not a.no_graph,
-                               weight_dtype=a.weight_dtype, streams=a.streams)
+                               weight_dtype=a.weight_dtype, streams=a.streams, dp=a.dp)
     if res is None:  # non-zero ranks
         return
     line = {
@@ -88,7 +91,7 @@ def main():
         "data": f"synthetic prompts, random-init weights ({res['model_name']} architecture)",
         "config": {"model": res["model_name"], "global_batch": res["global_batch"],
                    "seq_len": a.prompt_len + a.warmup + a.steps,
-                   "parallelism": f"pp{a.gpus}", "microbatches": res["microbatches"],
+                   "parallelism": f"dp{res['dp']}_pp{res['pp']}" if res["dp"] > 1 else f"pp{res['pp']}", "microbatches": res["microbatches"],
                    "batch_per_microbatch": a.batch, "prompt_len": a.prompt_len,
                    "concurrent_streams": res["streams"], "max_seq": res["max_seq"]},
         "p50_tpot_ms": round(res["p50_tpot_ms"], 4),

@@ -45,25 +45,40 @@ class DistP2P:
     only the transport's eager buffering breaks (small messages), not the API contract. With a
     communicator per edge each stream carries one direction in FIFO order, so the pipeline's
     dataflow order alone guarantees progress, and sends / receives on different edges overlap.
-    Must be constructed on every rank at the same point (``new_group`` is collective)."""
+    Must be constructed on every rank at the same point (``new_group`` is collective).
 
-    def __init__(self):
+    ``ranks``: the global ranks of THIS pipeline's stages in stage order (stage indices passed
+    to isend/recv are translated through it; default: every rank, one pipeline). ``rings``: the
+    rank lists of every pipeline replica of a data-parallel job (each process must create every
+    replica's edge groups, in the same order)."""
+
+    def __init__(self, ranks: Optional[list] = None, rings: Optional[list] = None):
         import torch.distributed as dist
         self.groups = {}
+        self.ranks = ranks
         if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
             n = dist.get_world_size()
-            for r in range(n):
-                self.groups[(r, (r + 1) % n)] = dist.new_group([r, (r + 1) % n])
+            for ring in (rings if rings is not None else [list(range(n))]):
+                for i in range(len(ring) if len(ring) > 1 else 0):
+                    a, b = ring[i], ring[(i + 1) % len(ring)]
+                    self.groups[(a, b)] = dist.new_group([a, b])
+            if self.ranks is None:
+                self.ranks = list(range(n))
+
+    def _global(self, stage: int) -> int:
+        return self.ranks[stage] if self.ranks is not None else stage
 
     def _group(self, src: int, dst: int):
         return self.groups.get((src, dst))  # non-ring edges (none in the pipeline): default group
 
     def isend(self, t: torch.Tensor, dst: int):
         import torch.distributed as dist
+        dst = self._global(dst)
         return dist.isend(t, dst, group=self._group(dist.get_rank(), dst))
 
     def recv(self, t: torch.Tensor, src: int) -> None:
         import torch.distributed as dist
+        src = self._global(src)
         dist.irecv(t, src, group=self._group(src, dist.get_rank())).wait()
 
 
@@ -473,14 +488,25 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
                          batch: int = 16, prompt_len: int = 128, max_seq: int = 0,
                          microbatches: int = 0, seed: int = 0, use_graph: bool = True,
                          verbose: bool = True, weight_dtype: str = "bf16", streams: int = 1,
-                         device: str = "cuda") -> Optional[dict]:
+                         device: str = "cuda", dp: int = 1) -> Optional[dict]:
     """``microbatches`` 0 = ``streams`` x stages (every GPU holds ``streams`` micro-batches of
-    ``batch`` sequences: weak scaling); ``max_seq`` 0 = what the run needs, rounded up to 64."""
+    ``batch`` sequences: weak scaling); ``max_seq`` 0 = what the run needs, rounded up to 64.
+
+    ``dp`` > 1: data parallel x pipeline parallel - the ranks form ``dp`` independent pipelines
+    of ``n_gpus / dp`` stages each (replica ``rank // pp``, stage ``rank % pp``), each on its own
+    prompts; the numbers are whole-job aggregates (tokens of all replicas over the slowest
+    rank's time). The pipelines share no communicator, so a replica's ring stays on its own
+    xGMI links (adjacent ranks) and a 7B model fits one GPU many times over: dp8 trades the
+    pipeline's per-token latency for none of its bubbles."""
     cfg = get_preset(model)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     if n_gpus != world:
         raise ValueError(f"n_gpus={n_gpus} but WORLD_SIZE={world}")
+    if dp < 1 or world % dp:
+        raise ValueError(f"dp={dp} must divide the world size {world}")
+    pp = world // dp
+    replica, srank = divmod(rank, pp)
     # device "cpu": the same flow on gloo + the torch CPU path (rehearsal of the multi-rank
     # schedule in CPU tests); otherwise one rank per GPU over RCCL
     gpu = device != "cpu"
@@ -505,20 +531,24 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
     def sync():
         if gpu:
             torch.cuda.synchronize()
-    M = microbatches or streams * world
+    M = microbatches or streams * pp
     need = prompt_len + warmup + steps + 1
     max_seq = max_seq or -(-need // 64) * 64
-    plan = plan_stages(cfg, world, kv_tokens=max_seq * batch * M, head_split=world > 1)
-    st = plan.stages[rank]
+    plan = plan_stages(cfg, pp, kv_tokens=max_seq * batch * M, head_split=pp > 1)
+    st = plan.stages[srank]
     if need > max_seq:
         raise ValueError(f"prompt+warmup+steps ({need}) exceeds max_seq {max_seq}")
     if verbose and rank == 0:
-        print(f"[bench] {cfg.name} pp{world} plan: {plan.summary()}", flush=True)
+        print(f"[bench] {cfg.name} {'dp%d x ' % dp if dp > 1 else ''}pp{pp} plan: {plan.summary()}", flush=True)
+    rings = [list(range(d * pp, (d + 1) * pp)) for d in range(dp)]
+    p2p = DistP2P(ranks=rings[replica], rings=rings)
     t0 = time.perf_counter()
-    stage = PipelineStage(cfg, rank, world, st.start, st.end, dev, batch, M, max_seq,
+    stage = PipelineStage(cfg, srank, pp, st.start, st.end, dev, batch, M, max_seq,
                           RandomSource(cfg, seed), use_graph=use_graph,
                           max_prefill_rows=batch * prompt_len, weight_dtype=weight_dtype, streams=streams,
-                          dtype=torch.bfloat16 if gpu else torch.float32)
+                          dtype=torch.bfloat16 if gpu else torch.float32, p2p=p2p)
+    if dp > 1:  # trace files are named by rank: use the global one
+        stage.tl = tracing.from_env(rank, dev if gpu else "cpu")
     sync()
     load_s = time.perf_counter() - t0
     if dist:
@@ -526,7 +556,7 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
 
     prompts = None
     if stage.first:
-        g = torch.Generator().manual_seed(seed + 1)
+        g = torch.Generator().manual_seed(seed + 1 + replica)
         prompts = torch.randint(3, cfg.vocab_size, (M, batch, prompt_len), generator=g, dtype=torch.int32)
     sync()
     tp0 = time.perf_counter()
@@ -577,19 +607,21 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
         allst = torch.stack(gathered).cpu()
         elapsed = float(allst[:, 0].max())
         ttft_ms = float(allst[0, 1])
-        p50, p90 = float(allst[world - 1, 2]), float(allst[world - 1, 3])
+        p50, p90 = float(allst[pp - 1, 2]), float(allst[pp - 1, 3])  # replica 0's last stage
         load_s = float(allst[:, 4].max())
     else:
         p50, p90 = float(stats[2]), float(stats[3])
-    tokens = steps * M * batch
+    tokens = dp * steps * M * batch
     res = {
         "tok_s": tokens / elapsed,
         "ms_per_step": elapsed * 1e3 / steps,
         "p50_tpot_ms": p50,
         "p90_tpot_ms": p90,
         "ttft_ms": ttft_ms,
-        "global_batch": M * batch,
+        "global_batch": dp * M * batch,
         "microbatches": M,
+        "dp": dp,
+        "pp": pp,
         "streams": stage.S,
         "max_seq": max_seq,
         "model_name": "Llama-2-7B" if model == "llama2-7b" else cfg.name,

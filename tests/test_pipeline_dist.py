@@ -112,7 +112,7 @@ def test_local_multistage_matches_single(n_stages, single):
     assert out.tolist() == single
 
 
-def _bench_worker(rank, world, port, q):
+def _bench_worker(rank, world, port, q, dp=1):
     """bench.py's driver (run_decode_benchmark) on gloo/CPU: the exact multi-rank schedule of
     the N-GPU headline run - prefill, warm-up, drain, timed steps, drain, stats gather."""
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
@@ -120,7 +120,7 @@ def _bench_worker(rank, world, port, q):
     torch.set_num_threads(1)
     from llm_sharding_amd.parallel.pipeline import run_decode_benchmark
     res = run_decode_benchmark(model="tiny", n_gpus=world, steps=3, warmup=2, batch=2, prompt_len=4,
-                               streams=2, device="cpu", verbose=False)
+                               streams=2, device="cpu", verbose=False, dp=dp)
     if rank == 0:
         q.put(res)
 
@@ -144,3 +144,26 @@ def test_bench_driver_multi_rank_cpu(world):
     assert res["microbatches"] == 2 * world and res["global_batch"] == 4 * world
     assert res["tok_s"] > 0 and res["ms_per_step"] > 0 and res["p50_tpot_ms"] > 0
     assert len(res["plan"]) == world
+
+
+@pytest.mark.parametrize("world,dp", [(4, 2), (2, 2)])
+def test_bench_driver_dp_x_pp_cpu(world, dp):
+    """dp independent pipelines of world/dp stages: replica-local rings, whole-job totals."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_bench_worker, args=(r, world, port, q, dp)) for r in range(world)]
+    for p in ps:
+        p.start()
+    try:
+        res = q.get(timeout=240)
+    finally:
+        for p in ps:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+    pp = world // dp
+    assert res["dp"] == dp and res["pp"] == pp and len(res["plan"]) == pp
+    assert res["microbatches"] == 2 * pp and res["global_batch"] == dp * 2 * pp * 2
+    assert res["tok_s"] > 0 and res["p50_tpot_ms"] > 0
