@@ -112,14 +112,20 @@ def save_tensor_dict(d: dict, path: str) -> None:
 
 
 def dequantize(d: dict) -> dict:
-    """FP8 shards (ModelSharder dtype=float8_e4m3fn): ``w * w_scale[:, None]`` -> bf16."""
+    """Quantised shards (utils/model_sharder.py) -> bf16: fp8 / int8 with per-channel scales
+    (``q * scale[:, None]``), int4 packed two per byte with group-wise scales."""
     out = {}
     for k, v in d.items():
         if k.endswith("_scale"):
             continue
         s = d.get(k + "_scale")
         if s is not None:
-            v = (v.float() * s.float()[:, None].to(v.device)).to(torch.bfloat16)
+            s = s.to(v.device)
+            if v.dtype == torch.uint8 and s.dim() == 2:
+                from ..utils.model_sharder import dequantize_int4
+                v = dequantize_int4(v, s).to(torch.bfloat16)
+            else:
+                v = (v.float() * s.float()[:, None]).to(torch.bfloat16)
         out[k] = v
     return out
 

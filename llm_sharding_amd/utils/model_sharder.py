@@ -14,15 +14,26 @@ needs a device able to hold it), the checkpoint is streamed tensor by tensor fro
 ``*.safetensors`` shards (zero-copy mmap) or ``pytorch_model*.bin`` files (read with
 ``torch.load(weights_only=True, mmap=True)``), so a 70B model shards on a small host.
 
-Quantised shards: the reference's bitsandbytes int8/int4 path has no loader (Q12) and
-bitsandbytes is CUDA-only. The MI355X-native equivalent is OCP FP8 (``torch.float8_e4m3fn``):
-each projection weight is stored with a per-output-channel fp32 scale
-(``<name>_scale``); the loader (models/weights.py) dequantises to bf16.
+Quantised shards. The reference's ``dtype=torch.int8 / torch.int4`` branch
+(``/root/reference/utils/model_sharder.py:28-39``) hands the model to bitsandbytes
+(CUDA-only) and has no loader for the result (Q12). Here every 2-D projection / head
+matrix is quantised by the sharder itself and the loader (models/weights.py) dequantises
+it to bf16; norms and the embedding stay bf16 (suffixes as in the reference:
+``_int8``, ``_int4``, ``_float8_e4m3fn``):
+
+* ``torch.float8_e4m3fn`` - OCP FP8 (MI355X-native, decodes on the W8A16 fp8 kernels with
+  ``weight_dtype="fp8"``): ``<name>`` e4m3 [N, K] + ``<name>_scale`` fp32 [N];
+* ``torch.int8`` - symmetric per-output-channel int8: ``<name>`` int8 [N, K] +
+  ``<name>_scale`` fp32 [N] (w ~= q * scale, |q| <= 127);
+* ``torch.int4`` - symmetric group-wise int4 (``INT4_GROUP`` = 128 input channels per
+  scale), two values per byte, even k in the low nibble: ``<name>`` uint8 [N, K/2] +
+  ``<name>_scale`` fp32 [N, K/128] (|q| <= 7).
 """
 from __future__ import annotations
 
 import glob
 import json
+import math
 import os
 import re
 import shutil
@@ -55,6 +66,44 @@ def _iter_checkpoint(model_path: str) -> Iterator[tuple]:
             yield k, v
 
 
+INT4_GROUP = 128
+
+
+def quantize_int8(w: torch.Tensor) -> tuple:
+    """Per-output-channel symmetric int8: w ~= q * scale[:, None], q in [-127, 127]."""
+    scale = w.float().abs().amax(dim=1).clamp(min=1e-12) / 127.0
+    q = torch.round(w.float() / scale[:, None]).clamp(-127, 127).to(torch.int8)
+    return q, scale
+
+
+def quantize_int4(w: torch.Tensor, group: int = INT4_GROUP) -> tuple:
+    """Group-wise symmetric int4 packed two per byte (even k -> low nibble):
+    w[n, k] ~= q[n, k] * scale[n, k // group], q in [-7, 7]."""
+    N, K = w.shape
+    group = math.gcd(K, group)  # narrow matrices (K not a multiple of 128): the largest divisor
+    if group % 2:
+        raise ValueError(f"int4 needs an even input dimension, got K={K}")
+    wg = w.float().reshape(N, K // group, group)
+    scale = wg.abs().amax(dim=2).clamp(min=1e-12) / 7.0
+    q = torch.round(wg / scale[:, :, None]).clamp(-7, 7).to(torch.int8).reshape(N, K)
+    u = (q & 0xF).to(torch.uint8)
+    return (u[:, 0::2] | (u[:, 1::2] << 4)).contiguous(), scale
+
+
+def dequantize_int4(packed: torch.Tensor, scale: torch.Tensor) -> torch.Tensor:
+    """Inverse of :func:`quantize_int4` -> fp32 [N, K]."""
+    N = packed.shape[0]
+    lo = (packed & 0xF).to(torch.int8)
+    hi = (packed >> 4).to(torch.int8)
+    q = torch.stack((lo, hi), dim=2).reshape(N, -1)
+    q = torch.where(q > 7, q - 16, q).float()
+    G = q.shape[1] // scale.shape[1]
+    return (q.reshape(N, scale.shape[1], G) * scale.float()[:, :, None]).reshape(N, -1)
+
+
+QUANT_DTYPES = tuple(d for d in (FP8, torch.int8, getattr(torch, "int4", None)) if d is not None)
+
+
 def quantize_fp8(w: torch.Tensor) -> tuple:
     """Per-output-channel symmetric OCP e4m3 quantisation: w ~= q * scale[:, None]."""
     amax = w.float().abs().amax(dim=1).clamp(min=1e-12)
@@ -74,9 +123,6 @@ class ModelSharder:
         self.device = torch.device(device)
         self.dtype = dtype
         self.verbose = verbose
-        if dtype in (torch.int8, getattr(torch, "int4", None)):
-            raise NotImplementedError("bitsandbytes int8/int4 shards are CUDA-only and the reference has no loader "
-                                      "for them (Q12); use dtype=torch.float8_e4m3fn (OCP FP8, MI355X-native)")
         self.shard_save_folder = shard_save_folder + "_" + dtype_suffix(dtype)
         os.makedirs(self.shard_save_folder, exist_ok=True)
 
@@ -85,12 +131,17 @@ class ModelSharder:
             print(m, flush=True)
 
     def _cast(self, name: str, t: torch.Tensor) -> dict:
-        """Return {name: tensor} (and a scale for fp8 matrices)."""
+        """Return {name: tensor} (and a scale for quantised matrices)."""
         if not t.is_floating_point():
             return {name: t}
-        if FP8 is not None and self.dtype == FP8:
+        if self.dtype in QUANT_DTYPES:
             if t.dim() == 2 and name.endswith("weight"):
-                q, s = quantize_fp8(t)
+                if self.dtype == torch.int8:
+                    q, s = quantize_int8(t)
+                elif self.dtype == FP8:
+                    q, s = quantize_fp8(t)
+                else:
+                    q, s = quantize_int4(t)
                 return {name: q, name + "_scale": s}
             return {name: t.to(torch.bfloat16)}
         return {name: t.to(self.dtype)}
@@ -145,7 +196,7 @@ class ModelSharder:
             self._log(f"Saved block {j}")
         if embed is None or final is None:
             raise KeyError("checkpoint lacks model.embed_tokens.weight / model.norm.weight")
-        emb = {"weight": embed.to(torch.bfloat16 if FP8 is not None and self.dtype == FP8 else self.dtype)}
+        emb = {"weight": embed.to(torch.bfloat16 if self.dtype in QUANT_DTYPES else self.dtype)}
         self._save(emb, "embedding.pth")
         self._save({"weight": final.to(emb["weight"].dtype)}, "final_norm.pth")
         self._save(self._cast("weight", head if head is not None else embed), "lm_head.pth")
@@ -168,7 +219,7 @@ class ModelSharder:
                 lnf[name.split("ln_f.")[-1]] = t
             elif name == "lm_head.weight":
                 head = t
-        dt = self.dtype if not (FP8 is not None and self.dtype == FP8) else torch.bfloat16
+        dt = torch.bfloat16 if self.dtype in QUANT_DTYPES else self.dtype
         # nested dict layout of the reference (model_sharder.py:109-113)
         torch.save({"wte": {"weight": wte.to(dt)}, "wpe": {"weight": wpe.to(dt)}, "drop": {}},
                    os.path.join(self.shard_save_folder, "embedding.pth"))

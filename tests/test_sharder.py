@@ -83,6 +83,53 @@ def test_sharder_gpt2_layout(tmp_path):
     assert torch.equal(torch.load(os.path.join(out, "lm_head.pth"), weights_only=True)["weight"], t["wte.weight"].half())
 
 
-def test_sharder_rejects_int8(tmp_path):
-    with pytest.raises(NotImplementedError):
-        ModelSharder(str(tmp_path), "llama", str(tmp_path / "x"), dtype=torch.int8)
+@pytest.mark.parametrize("dtype,tol", [(torch.int8, 0.01), (getattr(torch, "int4", None), 0.12)])
+def test_sharder_int8_int4(hf_ckpt, tmp_path, dtype, tol):
+    """The reference's int8 / int4 sharding options (bitsandbytes there): self-contained
+    symmetric quantisation here, loaded back as bf16 by the engine."""
+    if dtype is None:
+        pytest.skip("no torch.int4")
+    cfg, d, layers = hf_ckpt
+    out = ModelSharder(d, "llama", str(tmp_path / "tiny"), dtype=dtype, verbose=False).save_shards()
+    assert out.endswith("_" + str(dtype).split(".")[-1])
+    raw = torch.load(os.path.join(out, "block_0.pth"), weights_only=True)
+    q, s = raw["mlp.down_proj.weight"], raw["mlp.down_proj.weight_scale"]
+    w = layers[0]["mlp.down_proj.weight"]
+    if dtype == torch.int8:
+        assert q.dtype == torch.int8 and q.shape == w.shape and s.shape == (w.shape[0],)
+    else:
+        assert q.dtype == torch.uint8 and q.shape == (w.shape[0], w.shape[1] // 2) and s.dim() == 2
+    assert raw["input_layernorm.weight"].dtype == torch.bfloat16
+    blk = W.load_block(out, 0)
+    for k in ("self_attn.q_proj.weight", "mlp.down_proj.weight"):
+        ref = layers[0][k]
+        assert blk[k].dtype == torch.bfloat16 and blk[k].shape == ref.shape
+        assert (blk[k].float() - ref).norm() / ref.norm() < tol
+    # the engine on the quantised shards == the golden model on the same (dequantised) weights
+    c2, emb, lays, fn, lm = W.load_full_model(out)
+    prompt = torch.tensor([[1, 11, 22, 33]])
+    want = ReferenceLlama(c2, emb, lays, fn, lm).generate(prompt, 4)[0].tolist()
+    eng = StageEngine(c2, 0, c2.num_hidden_layers, "cpu", torch.float32, has_embed=True, has_head=True,
+                      source=ShardFolderSource(out), max_seq=64)
+    ids, got = prompt[0], []
+    for _ in range(4):
+        sl, po = eng.prefill_rows([0], [ids.numel()])
+        h = eng.forward(eng.embed(ids), sl, po)
+        eng.advance([0], [ids.numel()])
+        ids = eng.head(h, [ids.numel() - 1])
+        got.append(int(ids[0]))
+    assert got == want
+
+
+def test_int4_pack_roundtrip():
+    from llm_sharding_amd.utils.model_sharder import dequantize_int4, quantize_int4
+    w = torch.randn(8, 256)
+    q, s = quantize_int4(w)
+    assert q.shape == (8, 128) and s.shape == (8, 2)
+    # on-grid values come back exactly
+    grid = (torch.randint(-7, 8, (8, 256)).float() * s.repeat_interleave(128, dim=1))
+    q2, s2 = quantize_int4(grid)
+    assert torch.allclose(dequantize_int4(q2, s2), grid, atol=1e-6)
+    # narrow K: group = gcd(K, 128)
+    q3, s3 = quantize_int4(torch.randn(4, 96))
+    assert s3.shape == (4, 3)
