@@ -11,9 +11,11 @@ generated on each device - no checkpoints are available offline):
   * rank r owns a contiguous layer range chosen by the master scheduler (rank 0 also holds
     the embedding, rank N-1 the final norm + lm_head), one process per GPU;
   * M = S x N micro-batches of B sequences each are in flight (S x B sequences per GPU,
-    fixed -> weak scaling); every sequence was prefilled with a P-token prompt first. On one
-    GPU the S micro-batches replay their decode graphs concurrently on S HIP streams (a 7B
-    decode graph alone leaves CUs idle); pipelines keep one compute stream per stage;
+    fixed -> weak scaling); every sequence was prefilled with a P-token prompt first. The
+    default is one micro-batch of 512 sequences per GPU: above 128 rows a decode step's
+    projections run on the library GEMM (hipBLASLt) + one fused epilogue pass each, which
+    beats the 128-row GEMV kernels on S concurrent streams (profiles/r1_big_batch_decode.txt);
+    with S > 1 each GPU replays its micro-batches' graphs on S HIP streams;
   * one timed "step" = every in-flight sequence produces one new token (greedy, fused
     lm_head+argmax on device); hidden states move stage->stage with RCCL send/recv over
     xGMI, token ids return last->first the same way.
@@ -40,11 +42,12 @@ def parse():
     ap.add_argument("--steps", type=int, default=64)
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--model", default="llama2-7b")
-    ap.add_argument("--batch", type=int, default=128,
-                    help="sequences per micro-batch (per GPU); 128 = the largest hipGraph decode batch")
+    ap.add_argument("--batch", type=int, default=512,
+                    help="sequences per micro-batch (per GPU, <= 1024); <= 128 decode on the fused GEMV "
+                         "kernels, more on the library GEMM + fused epilogue passes")
     ap.add_argument("--prompt-len", type=int, default=128)
     ap.add_argument("--max-seq", type=int, default=0, help="0 = prompt + warmup + steps, rounded up to 64")
-    ap.add_argument("--streams", type=int, default=3,
+    ap.add_argument("--streams", type=int, default=1,
                     help="micro-batches resident per GPU; on one GPU they replay concurrently on this many "
                          "HIP streams")
     ap.add_argument("--microbatches", type=int, default=0, help="0 = streams x pipeline stages")

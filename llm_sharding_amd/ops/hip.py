@@ -66,8 +66,9 @@ def lib() -> ctypes.CDLL:
     L.lsa_layernorm.argtypes = [vp, i, vp, vp, vp, vp, i, i, f, vp, i, vp]
     L.lsa_argmax_finalize.argtypes = [vp, i, vp, vp, i, vp, i, i, vp, vp]
     L.lsa_pos_advance.argtypes = [vp, i, i, vp]
+    L.lsa_epilogue_apply.argtypes = [vp, i, i, i, i, ctypes.POINTER(EpiArgs), vp]
     for name in ("lsa_gemv", "lsa_gemv_coop", "lsa_gemv_fp8", "lsa_dequant_fp8_packed", "lsa_gemv_coop_fp8", "lsa_gemm", "lsa_attn_decode", "lsa_attn_prefill", "lsa_embed", "lsa_rmsnorm", "lsa_layernorm",
-                 "lsa_argmax_finalize", "lsa_pos_advance", "lsa_version"):
+                 "lsa_argmax_finalize", "lsa_pos_advance", "lsa_epilogue_apply", "lsa_version"):
         getattr(L, name).restype = ctypes.c_int
     _lib = L
     return L
@@ -303,6 +304,19 @@ def gemm(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep
     rc = lib().lsa_gemm(_p(a), a.stride(0), _p(wp), M, N, K, epi, ctypes.byref(ep), tn, sk, _p(slab), _p(cnt),
                         _stream())
     _check(rc, "lsa_gemm")
+
+
+def epilogue_apply(c: torch.Tensor, M: int, N: int, epi: int, ep: EpiArgs) -> None:
+    """The fused projection epilogue as one pass over a finished bf16 GEMM output ``c``
+    [>= M, >= N] in packed column order (epilogue_apply.hip): RoPE + KV-cache append (QKV),
+    SwiGLU, residual add or store - the tail of a library-GEMM projection."""
+    _req(epi in (EPI_STORE, EPI_RESID, EPI_SWIGLU, EPI_QKV), f"epilogue_apply: epilogue {epi} not supported")
+    _req(_is_bf16_cuda(c) and c.dim() == 2 and c.stride(1) == 1, "epilogue_apply: bf16 cuda row-major C")
+    _req(c.shape[0] >= M >= 1 and c.shape[1] >= N and N % (32 if epi == EPI_SWIGLU else 16) == 0,
+         f"epilogue_apply: C {tuple(c.shape)} vs M={M} N={N}")
+    _req(c.stride(0) % 8 == 0 and c.data_ptr() % 16 == 0, "epilogue_apply: C rows must be 16-byte aligned")
+    _check_epi(epi, ep, N)
+    _check(lib().lsa_epilogue_apply(_p(c), c.stride(0), M, N, epi, ctypes.byref(ep), _stream()), "lsa_epilogue_apply")
 
 
 # ------------------------------------------------------------------------------ attention

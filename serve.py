@@ -124,7 +124,12 @@ def main():
         from llm_sharding_amd.parallel.scheduler import kv_slots_for_memory
         wplan = plan_stages(cfg, world, head_split=world > 1)
         mem = torch.cuda.get_device_properties(dev).total_memory if gpu else 64e9
-        rc.batch = min(kv_slots_for_memory(cfg, s.n_layers, rc.max_seq, mem, s.weight_bytes, microbatches=M)
+        # bf16 Llama stages keep a row-major copy of the projections for the library GEMM
+        # (StageEngine.library_gemm, same 40%-of-HBM rule): count it as weights
+        def wbytes(s):
+            lib = gpu and not cfg.is_gpt2 and 2 * s.weight_bytes <= 0.4 * mem
+            return s.weight_bytes * (2 if lib else 1)
+        rc.batch = min(kv_slots_for_memory(cfg, s.n_layers, rc.max_seq, mem, wbytes(s), microbatches=M)
                        for s in wplan.stages)
         log.info(f"KV cache sized from {mem / 1e9:.0f} GB HBM: {rc.batch} slots x {M} micro-batches")
     plan = plan_stages(cfg, world, kv_tokens=rc.max_seq * rc.batch * M)

@@ -91,6 +91,40 @@ def test_engine_prefill_then_decode_vs_golden(cfg_fn, S):
             assert got == int(lg.argmax(-1)[0])
 
 
+@pytest.mark.parametrize("library_gemm", [True, False])
+def test_big_batch_decode_graph_vs_golden(library_gemm):
+    """A decode graph above the 128-row GEMV range (160 sequences; library GEMM + epilogue pass,
+    or gemm.hip) against the fp32 golden model: prefill and decode-step hidden states, and the
+    greedy tokens wherever the top-2 margin is clear."""
+    cfg = _mid_cfg()
+    seed, rows, P = 13, 160, 5
+    eng = StageEngine(cfg, 0, cfg.num_hidden_layers, DEV, torch.bfloat16, has_embed=True, has_head=True,
+                      source=CpuGenSource(cfg, seed), max_slots=rows, max_seq=64, max_prefill_rows=rows * P,
+                      library_gemm=library_gemm)
+    assert eng.library_gemm == library_gemm
+    ref = _ref(cfg, seed)
+    ids = torch.randint(3, cfg.vocab_size, (rows, P), generator=torch.Generator().manual_seed(3))
+    slots = list(range(rows))
+    sl, po = eng.prefill_rows(slots, [P] * rows)
+    h = eng.forward(eng.embed(ids.reshape(-1).to(DEV)), sl, po)
+    eng.advance(slots, [P] * rows)
+    href = ref.forward_hidden(ref.embed[ids])
+    assert rel_err(h.reshape(rows, P, -1), href) < 3e-2
+    first = eng.head(h, [r * P + P - 1 for r in range(rows)]).cpu()
+    dg = DecodeGraph(eng, rows, "full", history_len=1)
+    dg.tokens.copy_(first.to(torch.int32))
+    dg.capture()
+    dg.replay()
+    torch.cuda.synchronize()
+    href2 = ref.forward_hidden(ref.embed[first[:, None]])[:, -1]
+    assert rel_err(dg.out_hidden, href2) < 3e-2
+    lg = ref.logits(href2)
+    top2 = lg.topk(2, dim=-1).values
+    clear = (top2[:, 0] - top2[:, 1]) > 0.05 * lg.abs().amax(-1)
+    got = dg.history[0].cpu().long()
+    assert bool(clear.any()) and bool((got[clear] == lg.argmax(-1)[clear]).all())
+
+
 def test_decode_graph_matches_eager():
     cfg = tiny()
     src = RandomSource(cfg, seed=4)
@@ -161,6 +195,19 @@ def test_concurrent_microbatch_streams_match_serial():
     serial = run_pipeline_generate(cfg, src, prompts, 12, 0, 1, streams=1, **kw)
     conc = run_pipeline_generate(cfg, src, prompts, 12, 0, 1, streams=3, **kw)
     assert conc.tolist() == serial.tolist()
+
+
+def test_multistage_big_batch_streams():
+    """Micro-batches of 160 sequences (decode graphs above the GEMV range) through 2 pipeline
+    stages on 2 concurrent streams: same tokens as the one-stage, one-stream loop."""
+    from llm_sharding_amd.parallel.pipeline import drive_local_pipeline, run_pipeline_generate
+    cfg = LlamaConfig(num_hidden_layers=4, vocab_size=32000, max_position_embeddings=512, name="7B-4L")
+    src = RandomSource(cfg, seed=6)
+    prompts = torch.randint(3, cfg.vocab_size, (2, 160, 6), generator=torch.Generator().manual_seed(9))
+    single = run_pipeline_generate(cfg, src, prompts, 6, 0, 1, device=DEV, batch=160, microbatches=2, max_seq=64,
+                                   dtype=torch.bfloat16)
+    multi = drive_local_pipeline(cfg, src, prompts, 6, 2, DEV, batch=160, microbatches=2, max_seq=64, streams=2)
+    assert multi.tolist() == single.tolist()
 
 
 def test_multistage_concurrent_streams_7b_shapes():

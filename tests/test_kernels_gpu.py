@@ -170,6 +170,29 @@ def test_gemv_swiglu(M):
     assert rel_err(out, ref) < 1e-2
 
 
+def test_library_gemm_epilogues():
+    """torch.matmul (vendor GEMM) + epilogue_apply.hip: SwiGLU on the packed gate|up column
+    order, residual add and plain store, against fp32 references."""
+    h = hip()
+    M, I, H = 200, 1024, 512
+    x = _rnd(M, H)
+    wg, wu = _rnd(I, H, scale=0.05), _rnd(I, H, scale=0.05)
+    c = torch.matmul(x, packing.fuse_gate_up(wg, wu).t())
+    out = torch.zeros(M, I, dtype=torch.bfloat16, device=DEV)
+    h.epilogue_apply(c, M, 2 * I, h.EPI_SWIGLU, h.make_epi(out=out, ldo=I))
+    ref = F.silu(x.float() @ wg.float().T) * (x.float() @ wu.float().T)
+    assert rel_err(out, ref) < 1e-2
+    w = _rnd(H, I, scale=0.02)
+    c2 = torch.matmul(out, w.t())
+    r = _rnd(M, H)
+    o2 = r.clone()
+    h.epilogue_apply(c2, M, H, h.EPI_RESID, h.make_epi(out=o2, resid=o2, ldo=H, ldr=H))
+    assert rel_err(o2, r.float() + out.float() @ w.float().T) < 8e-3
+    o3 = torch.zeros(M, H, dtype=torch.bfloat16, device=DEV)
+    h.epilogue_apply(c2, M, H, h.EPI_STORE, h.make_epi(out=o3, ldo=H))
+    assert torch.equal(o3, c2)
+
+
 def _rope_ref(t, pos, cos, sin):
     half = t.shape[-1] // 2
     c, s = cos[pos][:, None, :], sin[pos][:, None, :]
@@ -177,14 +200,14 @@ def _rope_ref(t, pos, cos, sin):
     return torch.cat([t1 * c - t2 * s, t2 * c + t1 * s], dim=-1)
 
 
-@pytest.mark.parametrize("path", ["gemv", "coop", "gemm"])
+@pytest.mark.parametrize("path", ["gemv", "coop", "gemm", "library"])
 @pytest.mark.parametrize("nh,nkv,hd", [(32, 32, 128), (8, 2, 64), (24, 8, 128)])
 def test_qkv_rope_kv_append(path, nh, nkv, hd):
     from llm_sharding_amd.config import tiny
     from llm_sharding_amd.models.rope import rope_table
     h = hip()
     H = 512
-    M = {"gemv": 5, "coop": 40, "gemm": 150}[path]
+    M = {"gemv": 5, "coop": 40, "gemm": 150, "library": 150}[path]
     slots, T = 3, 256
     wq, wk, wv = _rnd(nh * hd, H, scale=0.05), _rnd(nkv * hd, H, scale=0.05), _rnd(nkv * hd, H, scale=0.05)
     x = _rnd(M, H)
@@ -203,8 +226,11 @@ def test_qkv_rope_kv_append(path, nh, nkv, hd):
         h.gemv(x, wp, M, N, H, h.EPI_QKV, ep)
     elif path == "coop":
         h.gemv(x, wp, M, N, H, h.EPI_QKV, ep, coop=(1, 8, 4, 2))
-    else:
+    elif path == "gemm":
         h.gemm(x, wp, M, N, H, h.EPI_QKV, ep)
+    else:  # vendor GEMM on the row-major fused weights + the standalone epilogue pass
+        c = torch.matmul(x, packing.fuse_qkv(wq, wk, wv, nh, nkv, hd).t())
+        h.epilogue_apply(c, M, N, h.EPI_QKV, ep)
     xf = x.float()
     pl = pos.long()
     qr = _rope_ref((xf @ wq.float().T).view(M, nh, hd), pl, cos, sin).reshape(M, -1)
