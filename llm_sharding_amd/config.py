@@ -229,6 +229,7 @@ PRESETS = {
     "llama2-70b": llama2_70b,
     "llama3.2-3b": llama32_3b,
     "tiny": tiny,
+    "tiny8": lambda: tiny(layers=8),  # one layer per stage on 8 ranks (N=8 schedule rehearsal)
     "gpt2": gpt2,
     "gpt2-medium": lambda: gpt2("medium"),
     "gpt2-large": lambda: gpt2("large"),

@@ -112,15 +112,15 @@ def test_local_multistage_matches_single(n_stages, single):
     assert out.tolist() == single
 
 
-def _bench_worker(rank, world, port, q, dp=1):
+def _bench_worker(rank, world, port, q, dp=1, model="tiny", streams=2):
     """bench.py's driver (run_decode_benchmark) on gloo/CPU: the exact multi-rank schedule of
     the N-GPU headline run - prefill, warm-up, drain, timed steps, drain, stats gather."""
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
                        "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
     torch.set_num_threads(1)
     from llm_sharding_amd.parallel.pipeline import run_decode_benchmark
-    res = run_decode_benchmark(model="tiny", n_gpus=world, steps=3, warmup=2, batch=2, prompt_len=4,
-                               streams=2, device="cpu", verbose=False, dp=dp)
+    res = run_decode_benchmark(model=model, n_gpus=world, steps=3, warmup=2, batch=2, prompt_len=4,
+                               streams=streams, device="cpu", verbose=False, dp=dp)
     if rank == 0:
         q.put(res)
 
@@ -166,4 +166,27 @@ def test_bench_driver_dp_x_pp_cpu(world, dp):
     pp = world // dp
     assert res["dp"] == dp and res["pp"] == pp and len(res["plan"]) == pp
     assert res["microbatches"] == 2 * pp and res["global_batch"] == dp * 2 * pp * 2
+    assert res["tok_s"] > 0 and res["p50_tpot_ms"] > 0
+
+
+def test_bench_driver_eight_ranks_cpu():
+    """The driver's N=8 node run, rehearsed on gloo: bench.py's defaults (one stream, so M = 8
+    micro-batches), 8 one-layer stages, lm_head split between stage 7 and stage 0."""
+    world = 8
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_bench_worker, args=(r, world, port, q, 1, "tiny8", 1)) for r in range(world)]
+    for p in ps:
+        p.start()
+    try:
+        res = q.get(timeout=300)
+    finally:
+        for p in ps:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+    assert res["microbatches"] == world and res["global_batch"] == 2 * world
+    assert len(res["plan"]) == world
     assert res["tok_s"] > 0 and res["p50_tpot_ms"] > 0
