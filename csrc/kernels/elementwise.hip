@@ -51,6 +51,50 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const bf16_raw* __restrict
   }
 }
 
+// Register-resident RMSNorm for H = 2048 * NC (Llama-2-7B / 70B: NC = 2 / 4; other widths take
+// rmsnorm_kernel), used by the engine's standalone norms of >128-row forwards: every lane issues
+// its NC 16-B row loads (and the weight's) before the first use, so a row costs ONE memory round
+// trip and is not re-read for the scaling pass. Same per-lane accumulation order as rmsnorm_kernel.
+template <int NC>
+__global__ __launch_bounds__(256) void rmsnorm_reg_kernel(const bf16_raw* __restrict__ x, int ldx,
+                                                          const bf16_raw* __restrict__ w,
+                                                          float eps, bf16_raw* __restrict__ out,
+                                                          int ldo) {
+  constexpr int H = 2048 * NC;
+  __shared__ float s_part[4];
+  const int row = blockIdx.x, tid = threadIdx.x;
+  const bf16_raw* xr = x + (size_t)row * ldx;
+  u32x4_t v[NC], wv[NC];
+#pragma unroll
+  for (int j = 0; j < NC; ++j) v[j] = ld16(xr + (tid + j * 256) * 8);
+  if (w) {
+#pragma unroll
+    for (int j = 0; j < NC; ++j) wv[j] = ld16(w + (tid + j * 256) * 8);
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < NC; ++j) {
+    float f[8];
+    unpack8(v[j], f);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += f[k] * f[k];
+  }
+  s = wave_sum(s);
+  if ((tid & 63) == 0) s_part[tid >> 6] = s;
+  __syncthreads();
+  const float rs = rsqrtf((s_part[0] + s_part[1] + s_part[2] + s_part[3]) / (float)H + eps);
+  bf16_raw* orow = out + (size_t)row * ldo;
+#pragma unroll
+  for (int j = 0; j < NC; ++j) {
+    float f[8], g[8] = {1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
+    unpack8(v[j], f);
+    if (w) unpack8(wv[j], g);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) f[k] = f[k] * rs * g[k];
+    st16(orow + (tid + j * 256) * 8, pack8(f));
+  }
+}
+
 // Two-pass (mean, then centred variance) over the row held in L2; the optional position add
 // rounds to bf16 first, as HF's ``inputs_embeds + position_embeds`` in the model dtype does.
 __global__ __launch_bounds__(256) void layernorm_kernel(bf16_raw* __restrict__ x, int ldx,
@@ -141,9 +185,18 @@ extern "C" int lsa_embed(const int* ids, int rows, const void* table, int H, voi
 extern "C" int lsa_rmsnorm(const void* x, int ldx, const void* w, int rows, int H, float eps,
                            void* out, int ldo, hipStream_t stream) {
   if (rows < 1 || H % 8) return LSA_BAD_SHAPE;
-  rmsnorm_kernel<<<rows, 256, 0, stream>>>(static_cast<const bf16_raw*>(x), ldx,
-                                          static_cast<const bf16_raw*>(w), H, eps,
-                                          static_cast<bf16_raw*>(out), ldo);
+  const bf16_raw* xb = static_cast<const bf16_raw*>(x);
+  const bf16_raw* wb = static_cast<const bf16_raw*>(w);
+  bf16_raw* ob = static_cast<bf16_raw*>(out);
+  // 16-B row alignment of x/out is what ld16/st16 already assume (ldx, ldo multiples of 8)
+  switch (H) {
+    case 2048: rmsnorm_reg_kernel<1><<<rows, 256, 0, stream>>>(xb, ldx, wb, eps, ob, ldo); break;
+    case 4096: rmsnorm_reg_kernel<2><<<rows, 256, 0, stream>>>(xb, ldx, wb, eps, ob, ldo); break;
+    case 6144: rmsnorm_reg_kernel<3><<<rows, 256, 0, stream>>>(xb, ldx, wb, eps, ob, ldo); break;
+    case 8192: rmsnorm_reg_kernel<4><<<rows, 256, 0, stream>>>(xb, ldx, wb, eps, ob, ldo); break;
+    default:
+      rmsnorm_kernel<<<rows, 256, 0, stream>>>(xb, ldx, wb, H, eps, ob, ldo);
+  }
   LSA_CHECK_LAUNCH();
   return LSA_OK;
 }

@@ -357,6 +357,20 @@ def test_embed_and_rmsnorm():
     assert rel_err(o2, _rmsnorm(out, torch.ones_like(w), 1e-5)) < 5e-3
 
 
+@pytest.mark.parametrize("H", [2048, 3072, 4096, 6144, 8192])
+def test_rmsnorm_widths_strided(H):
+    """Register-resident widths (2048 * NC) and the generic loop (3072), strided rows."""
+    h = hip()
+    rows = 133
+    x = _rnd(rows, H + 64)[:, :H]  # ldx = H + 64
+    w = (1 + 0.1 * torch.randn(H, device=DEV)).to(torch.bfloat16)
+    o = torch.zeros(rows, H + 128, dtype=torch.bfloat16, device=DEV)[:, :H]
+    h.rmsnorm(x, w, o, rows, 1e-5)
+    assert rel_err(o, _rmsnorm(x, w, 1e-5)) < 5e-3
+    h.rmsnorm(x, None, o, rows, 1e-5, H)
+    assert rel_err(o, _rmsnorm(x, torch.ones_like(w), 1e-5)) < 5e-3
+
+
 def test_argmax_finalize_history_and_pos():
     h = hip()
     rows = 5
