@@ -60,7 +60,55 @@ def parse():
     ap.add_argument("--trace", default="", help="write per-rank Chrome-trace timelines of the timed steps here")
     ap.add_argument("--weight-dtype", default="bf16", choices=("bf16", "fp8"),
                     help="fp8: OCP e4m3 projection/lm_head weights with per-row scales (W8A16, not the headline)")
+    ap.add_argument("--latency-steps", type=int, default=32,
+                    help="after the throughput pass, time this many batch-1 decode steps through the same "
+                         "pipeline (b1_p50_tpot_ms / b1_tok_s in the JSON line); 0 = skip")
+    ap.add_argument("--device", default="cuda", choices=("cuda", "cpu"),
+                    help="cpu: the same schedule on gloo + the torch CPU path (multi-rank rehearsal)")
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int) -> int:
+    """``--gpus N`` without a launcher: start N copies of this script as child processes, one
+    rank per GPU (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT in their env),
+    BEFORE this process touches the GPU - the counterpart of the reference's run_this.sh
+    (/root/reference/run_this.sh:11-17), which starts its N stage processes itself. Rank 0's
+    output passes through; if any rank fails the others are stopped and the exit code is
+    non-zero."""
+    import signal
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PYTHONUNBUFFERED="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL, start_new_session=True))
+    rc = 0
+    pending = list(range(n))
+    while pending:
+        for r in list(pending):
+            code = procs[r].poll()
+            if code is None:
+                continue
+            pending.remove(r)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                print(f"[bench] rank {r} exited with {code}; stopping the other ranks", file=sys.stderr, flush=True)
+                for q in pending:  # only the process groups started here
+                    try:
+                        os.killpg(procs[q].pid, signal.SIGTERM)
+                    except ProcessLookupError:
+                        pass
+        time.sleep(0.2)
+    return rc
 
 
 def main():
@@ -68,15 +116,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if a.gpus != world and world != 1:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
-    if a.gpus > 1 and world == 1:
-        raise SystemExit("multi-GPU runs must be launched with torch.distributed.run (one rank per GPU)")
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(spawn_ranks(a.gpus))
     if a.trace:
         os.environ["LSA_TRACE"] = a.trace
     from llm_sharding_amd.parallel.pipeline import run_decode_benchmark
     res = run_decode_benchmark(model=a.model, n_gpus=a.gpus, steps=a.steps, warmup=a.warmup,
                                batch=a.batch, prompt_len=a.prompt_len, max_seq=a.max_seq,
                                microbatches=a.microbatches, seed=a.seed, use_graph=not a.no_graph,
-                               weight_dtype=a.weight_dtype, streams=a.streams, dp=a.dp)
+                               weight_dtype=a.weight_dtype, streams=a.streams, dp=a.dp,
+                               latency_steps=a.latency_steps, device=a.device)
     if res is None:  # non-zero ranks
         return
     line = {
@@ -100,6 +149,8 @@ def main():
         "p50_tpot_ms": round(res["p50_tpot_ms"], 4),
         "p90_tpot_ms": round(res["p90_tpot_ms"], 4),
         "ttft_ms": round(res["ttft_ms"], 3),
+        "b1_p50_tpot_ms": None if res["b1_p50_tpot_ms"] is None else round(res["b1_p50_tpot_ms"], 4),
+        "b1_tok_s": None if res["b1_tok_s"] is None else round(res["b1_tok_s"], 2),
         "reference_anecdote_tok_s": 4.3,
     }
     print(json.dumps(line), flush=True)

@@ -1,0 +1,508 @@
+// Projection GEMM for > 128 rows (prompt prefill and big decode batches):
+//   C[M, N] = A[M, K] @ W^T, bf16 in, fp32 accumulate, with the fused epilogues of epilogue.h
+// (RoPE + KV-cache append | SwiGLU | residual add | store), replacing the reference's
+// nn.Linear calls inside HF LlamaDecoderLayer (/root/reference/utils/shard_loader.py:66-74).
+//
+// Structure (cdna_hip_programming.md §5 "The 256² 8-phase template", T1-T5):
+//  * 256 x BN output tile (BN = 256 or 128) per 512-thread workgroup (8 waves, 2 per SIMD),
+//    K step 64, one workgroup per CU, all LDS in ONE __shared__ array.
+//  * Both operands reach LDS by LDS-DMA (global_load_lds_dwordx4): the packed-16x32 weights
+//    (common.h) are already one lane-linear 1 KiB block per (16 cols, 32 k) fragment; the A
+//    tile is gathered in the same fragment order (per-lane source address), so every MFMA
+//    operand read is a conflict-free lane-linear ds_read_b128.
+//  * Each K-tile runs as 4 phases (one output quadrant of 16 or 8 MFMAs each). The two wave
+//    groups (waves 0-3 / 4-7, i.e. the two waves of every SIMD) run one raw s_barrier apart, so
+//    one wave of a SIMD issues MFMAs while its partner issues LDS reads and DMA.
+//  * The DMA for a buffer region is issued 5-6 phases ahead of its first read and retired by a
+//    COUNTED s_waitcnt vmcnt (one K-tile of DMA stays in flight across every barrier).
+//  * Work is split "data-parallel + stream-K": full rounds of 256-row x BN tiles go one per
+//    workgroup (grouped tile order, XCD-aware block remap), the remaining tiles' K iterations
+//    are spread evenly over the grid; a tile split between workgroups is combined by the last
+//    arriving one (write-through fp32 slabs + an agent-scope ticket, §6 Guideline 16) which
+//    then runs the fused epilogue.
+//  * Epilogue: accumulators -> LDS (fp32) -> one thread per 16-column tile row -> the
+//    vectorised row16 epilogues of epilogue.h (16-B stores).
+#include "epilogue.h"
+
+namespace {
+
+constexpr int BM = 256, BK = 64, NTHR = 512;
+constexpr int ELD = 68;  // fp32 row stride of the epilogue transpose image (2-way banked writes)
+
+template <int BN, int NB>
+struct Geo {
+  static constexpr int WM = BN == 256 ? 2 : 4;   // wave grid
+  static constexpr int WN = 8 / WM;
+  static constexpr int TM = BM / WM, TN = BN / WN;  // per-wave output tile
+  static constexpr int FM = TM / 16, FN = TN / 16;  // 16x16 MFMA tiles per wave
+  static constexpr int AREG = (BM / 2) * BK * 2;    // bytes of one A region (16 KiB)
+  static constexpr int BREG = (BN / 2) * BK * 2;    // bytes of one B region
+  static constexpr int BUF = 2 * AREG + 2 * BREG;   // one K-tile
+  static constexpr int AGL = AREG / 1024 / 8;       // DMA instructions per wave per A region
+  static constexpr int BGL = BREG / 1024 / 8;       // ... per B region
+  static constexpr int NPT = 2 * AGL + 2 * BGL;     // DMA instructions per wave per K-tile
+  static constexpr int EPI_BYTES = 8 * 64 * ELD * 4;
+  static constexpr int SMEM = (NB * BUF > EPI_BYTES ? NB * BUF : EPI_BYTES) + 16;
+  static_assert(SMEM <= 160 * 1024, "LDS budget");
+};
+
+struct SkParams {
+  int M, N, K, lda;
+  int MT, NT, NKT;       // 256-row tiles, BN-col tiles, 64-deep K tiles
+  int G;                 // workgroups
+  int dp_rounds;         // full rounds of whole tiles (tile r*G + g)
+  int sk_tiles;          // tiles after the data-parallel rounds, spread by K iterations
+  int group_m;           // grouped tile order: this many row tiles share a column sweep
+};
+
+// counted wait on the DMA queue (no other vector-memory op is in flight in the main loop)
+template <int N>
+LSA_DEVICE void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
+LSA_DEVICE void barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+LSA_DEVICE void glds16(const void* src, unsigned char* lds_base) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
+}
+
+// tile id -> (row tile, col tile): group_m row tiles sweep the column tiles together so the
+// A panels and the weight panels of a round of 256 tiles both stay in L2 / the Infinity Cache
+LSA_DEVICE void tile_coords(const SkParams& p, int tile, int& mt, int& nt) {
+  const int per_group = p.group_m * p.NT;
+  const int grp = tile / per_group, first = grp * p.group_m;
+  const int gm = min(p.group_m, p.MT - first);
+  const int r = tile - grp * per_group;
+  mt = first + r % gm;
+  nt = r / gm;
+}
+
+template <int BN, int EPI, int NB>
+struct Kern {
+  using G_ = Geo<BN, NB>;
+  static constexpr int WM = G_::WM, WN = G_::WN, TM = G_::TM, TN = G_::TN, FM = G_::FM, FN = G_::FN;
+  static constexpr int AREG = G_::AREG, BREG = G_::BREG, BUF = G_::BUF, AGL = G_::AGL, BGL = G_::BGL,
+                       NPT = G_::NPT;
+  static constexpr int HM = FM / 2, HN = FN / 2;  // quadrant size in 16x16 tiles
+
+  unsigned char* smem;
+  const bf16_raw* A;
+  const bf16_raw* W;
+  int tid, lane, w, wr, wc, group;
+  const SkParams* p;
+
+  // ---- DMA staging of one LDS region of local K-tile t ------------------------------------------
+  // A region mh: blocks (wr', i, kf) = rows wr'*TM + mh*TM/2 + i*16 + (lane&15), k kt*64+kf*32+8*(lane>>4)
+  // Sources = wave-uniform segment base (SGPRs) + 32-bit per-lane offset (one VGPR per block
+  // instead of a 64-bit pointer: the 256-wide tile needs every register it can keep).
+  const unsigned char* a_seg;
+  const unsigned char* b_seg;
+  LSA_DEVICE void stage_a(int buf, int mh, const unsigned (&aoff)[2][AGL], int kt) {
+    unsigned char* dst = smem + buf * BUF + mh * AREG;
+    const unsigned char* base = a_seg + (size_t)kt * (BK * 2);
+#pragma unroll
+    for (int s = 0; s < AGL; ++s) glds16(base + aoff[mh][s], dst + (w * AGL + s) * 1024);
+  }
+  LSA_DEVICE void stage_b(int buf, int nh, const unsigned (&boff)[2][BGL], int kt) {
+    unsigned char* dst = smem + buf * BUF + 2 * AREG + nh * BREG;
+    const unsigned char* base = b_seg + (size_t)kt * 2048;
+#pragma unroll
+    for (int s = 0; s < BGL; ++s) glds16(base + boff[nh][s], dst + (w * BGL + s) * 1024);
+  }
+
+  // ---- one segment: K-tiles [ka, kb) of output tile (mt, nt), accumulated into acc -------------
+  LSA_DEVICE void run_segment(f32x4_t (&acc)[FM][FN], int mt, int nt, int ka, int kb) {
+    const SkParams& P = *p;
+    const int n = kb - ka;
+    const int m0 = mt * BM, n0 = nt * BN;
+    const int KT32 = P.K >> 5;
+    a_seg = reinterpret_cast<const unsigned char*>(A + (size_t)m0 * P.lda + ka * BK);
+    b_seg = reinterpret_cast<const unsigned char*>(W) + ((size_t)(n0 >> 4) * KT32 + ka * 2) * 1024;
+    unsigned aoff[2][AGL], boff[2][BGL];
+#pragma unroll
+    for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+      for (int s = 0; s < AGL; ++s) {
+        const int b = w * AGL + s, kf = b & 1, wi = b >> 1;
+        const int wr_ = wi / HM, i = wi % HM;
+        const int row = min(m0 + wr_ * TM + mh * (TM / 2) + i * 16 + (lane & 15), P.M - 1) - m0;
+        aoff[mh][s] = (unsigned)((row * P.lda + kf * 32 + 8 * (lane >> 4)) * 2);
+      }
+#pragma unroll
+    for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+      for (int s = 0; s < BGL; ++s) {
+        const int b = w * BGL + s, kf = b & 1, wj = b >> 1;
+        const int wc_ = wj / HN, j = wj % HN;
+        const int ntl = wc_ * FN + nh * HN + j;
+        boff[nh][s] = (unsigned)(((ntl * KT32 + kf) * 64 + lane) * 16);
+      }
+
+    // prologue. NB = 2: RA0(0) RB0(0) RB1(0) RA1(0) [RA0(1) RB0(1)];
+    //           NB = 3: all four regions of tiles 0 [and 1]
+    stage_a(0, 0, aoff, 0);
+    stage_b(0, 0, boff, 0);
+    stage_b(0, 1, boff, 0);
+    stage_a(0, 1, aoff, 0);
+    if (n > 1) {
+      stage_a(1, 0, aoff, 1);
+      stage_b(1, 0, boff, 1);
+      if (NB == 3) {
+        stage_b(1, 1, boff, 1);
+        stage_a(1, 1, aoff, 1);
+        vm_wait<BGL + AGL + NPT>();
+      } else {
+        vm_wait<NPT>();
+      }
+    } else {
+      vm_wait<AGL + BGL>();
+    }
+    barrier();
+    if (group) barrier();  // stagger: waves 4-7 run one barrier behind waves 0-3
+
+    u32x4_t a[HM][2], b0[HN][2], b1[HN][2];
+    auto rd_a = [&](int buf, int mh) {
+      const unsigned char* src = smem + buf * BUF + mh * AREG + lane * 16;
+#pragma unroll
+      for (int i = 0; i < HM; ++i)
+#pragma unroll
+        for (int kf = 0; kf < 2; ++kf) a[i][kf] = ld16(src + ((wr * HM + i) * 2 + kf) * 1024);
+    };
+    auto rd_b = [&](int buf, int nh, u32x4_t (&bb)[HN][2]) {
+      const unsigned char* src = smem + buf * BUF + 2 * AREG + nh * BREG + lane * 16;
+#pragma unroll
+      for (int j = 0; j < HN; ++j)
+#pragma unroll
+        for (int kf = 0; kf < 2; ++kf) bb[j][kf] = ld16(src + ((wc * HN + j) * 2 + kf) * 1024);
+    };
+    auto mma = [&](int mh, const u32x4_t (&bb)[HN][2], int nh) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kf = 0; kf < 2; ++kf)
+#pragma unroll
+        for (int i = 0; i < HM; ++i)
+#pragma unroll
+          for (int j = 0; j < HN; ++j)
+            acc[mh * HM + i][nh * HN + j] = mfma16(a[i][kf], bb[j][kf], acc[mh * HM + i][nh * HN + j]);
+      __builtin_amdgcn_s_setprio(0);
+    };
+
+    if (NB == 2) {
+      // 2 buffers: RB1/RA1 of tile t+1 go into the other buffer, RA0/RB0 of tile t+2 into this
+      // one right after their last reads; each region lands 5-6 phases after its DMA issue and
+      // the counted wait keeps one K-tile of DMA in flight
+      for (int t = 0; t < n; ++t) {
+        const int cur = t & 1, nxt = cur ^ 1;
+        rd_a(cur, 0);
+        rd_b(cur, 0, b0);
+        if (t + 1 < n) { stage_b(nxt, 1, boff, t + 1); vm_wait<NPT>(); } else vm_wait<0>();
+        barrier();
+        mma(0, b0, 0);
+        barrier();
+        rd_b(cur, 1, b1);
+        if (t + 1 < n) { stage_a(nxt, 1, aoff, t + 1); vm_wait<NPT>(); } else vm_wait<0>();
+        barrier();
+        mma(0, b1, 1);
+        barrier();
+        rd_a(cur, 1);
+        if (t + 2 < n) { stage_a(cur, 0, aoff, t + 2); vm_wait<NPT>(); } else vm_wait<0>();
+        barrier();
+        mma(1, b1, 1);
+        barrier();
+        if (t + 2 < n) { stage_b(cur, 0, boff, t + 2); vm_wait<NPT>(); } else vm_wait<0>();
+        barrier();
+        mma(1, b0, 0);
+        barrier();
+      }
+    } else {
+      // 3 buffers: tile t+2 is staged during tile t into the buffer tile t-1 used, in read
+      // order; the counted wait keeps the last 6 phases of DMA (~1.5 K-tiles) in flight
+      int cur = 0, nx2 = 2;
+      for (int t = 0; t < n; ++t) {
+        const bool st = t + 2 < n;
+        rd_a(cur, 0);
+        rd_b(cur, 0, b0);
+        if (st) { stage_a(nx2, 0, aoff, t + 2); vm_wait<NPT + 2 * AGL>(); } else vm_wait<0>();
+        barrier();
+        mma(0, b0, 0);
+        barrier();
+        rd_b(cur, 1, b1);
+        if (st) { stage_b(nx2, 0, boff, t + 2); vm_wait<NPT + AGL + BGL>(); } else vm_wait<0>();
+        barrier();
+        mma(0, b1, 1);
+        barrier();
+        rd_a(cur, 1);
+        if (st) { stage_b(nx2, 1, boff, t + 2); vm_wait<NPT + 2 * BGL>(); } else vm_wait<0>();
+        barrier();
+        mma(1, b1, 1);
+        barrier();
+        if (st) { stage_a(nx2, 1, aoff, t + 2); vm_wait<NPT + AGL + BGL>(); } else vm_wait<0>();
+        barrier();
+        mma(1, b0, 0);
+        barrier();
+        cur = cur == 2 ? 0 : cur + 1;
+        nx2 = nx2 == 2 ? 0 : nx2 + 1;
+      }
+    }
+    if (!group) barrier();  // re-align the two wave groups; every LDS read has retired
+  }
+
+  // ---- fp32 partial slab (fragment-native, write-through) ------------------------------------
+  LSA_DEVICE void slab_store(float* slab, size_t slot, const f32x4_t (&acc)[FM][FN]) {
+    const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc(slab + slot * (size_t)(BM * BN), (short)0,
+                                                                         BM * BN * 4, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, acc[i][j]), sr,
+                                               ((w * FM * FN + i * FN + j) * 64 + lane) * 16, 0, 16);
+  }
+  LSA_DEVICE void slab_add(const float* slab, size_t slot, f32x4_t (&acc)[FM][FN]) {
+    const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc((void*)(slab + slot * (size_t)(BM * BN)),
+                                                                         (short)0, BM * BN * 4, 0x00020000);
+    // one 16x16-tile row (FN loads) at a time: with every load hoisted ahead of the adds the
+    // 128 accumulator registers plus 128 load destinations would spill
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      u32x4_t v[FN];
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        v[j] = __builtin_amdgcn_raw_buffer_load_b128(sr, ((w * FM * FN + i * FN + j) * 64 + lane) * 16, 0, 16);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] += __builtin_bit_cast(f32x4_t, v[j]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+
+  // ---- fused epilogue through an LDS transpose -------------------------------------------------
+  LSA_DEVICE void epilogue(const EpiArgs& ep, const f32x4_t (&acc)[FM][FN], int mt, int nt) {
+    const SkParams& P = *p;
+    float* img = reinterpret_cast<float*>(smem) + w * (64 * ELD);
+    constexpr int PASSES = TM / 64;  // 64 rows of this wave's tile per pass
+#pragma unroll
+    for (int ps = 0; ps < PASSES; ++ps) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            img[(i * 16 + 4 * (lane >> 4) + r) * ELD + j * 16 + (lane & 15)] = acc[ps * 4 + i][j][r];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const int row_base = mt * BM + wr * TM + ps * 64;
+      const int col_base = nt * BN + wc * TN;
+      if (EPI == EPI_SWIGLU) {
+        // units: 64 rows x FN/2 gate|up tile pairs
+#pragma unroll
+        for (int s = 0; s < (64 * (FN / 2)) / 64; ++s) {
+          const int u = lane + 64 * s, row = u / (FN / 2), pr = u % (FN / 2);
+          const int m = row_base + row;
+          const float* src = img + row * ELD + pr * 32;
+          float g[16], uu[16], v[16];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            *reinterpret_cast<f32x4_t*>(g + 4 * q) = *reinterpret_cast<const f32x4_t*>(src + 4 * q);
+            *reinterpret_cast<f32x4_t*>(uu + 4 * q) = *reinterpret_cast<const f32x4_t*>(src + 16 + 4 * q);
+          }
+          const int c0 = col_base + pr * 32;
+          if (m < P.M) {
+            epi_bias16(ep, c0, g);
+            epi_bias16(ep, c0 + 16, uu);
+#pragma unroll
+            for (int q = 0; q < 16; ++q) v[q] = silu(g[q]) * uu[q];
+            bf16_raw* o = ep.out + (size_t)m * ep.ldo + (c0 >> 1);
+            st16(o, pack8(v));
+            st16(o + 8, pack8(v + 8));
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < (64 * FN) / 64; ++s) {
+          const int u = lane + 64 * s, row = u / FN, j = u % FN;
+          const int m = row_base + row;
+          const float* src = img + row * ELD + j * 16;
+          float v[16];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) *reinterpret_cast<f32x4_t*>(v + 4 * q) = *reinterpret_cast<const f32x4_t*>(src + 4 * q);
+          if (m < P.M) epi_row16<EPI>(ep, m, col_base + j * 16, v);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+  }
+};
+
+template <int BN, int EPI, int NB>
+__global__ __launch_bounds__(NTHR) void gemm_sk_kernel(const bf16_raw* __restrict__ A, const bf16_raw* __restrict__ W,
+                                                        SkParams prm, EpiArgs ep, float* __restrict__ slab,
+                                                        unsigned* __restrict__ counters) {
+  using K_ = Kern<BN, EPI, NB>;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[Geo<BN, NB>::SMEM];
+  K_ k;
+  k.smem = smem;
+  k.A = A;
+  k.W = W;
+  k.p = &prm;
+  k.tid = threadIdx.x;
+  k.lane = threadIdx.x & 63;
+  k.w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  k.wr = k.w / K_::WN;
+  k.wc = k.w % K_::WN;
+  k.group = k.w >> 2;
+  const int G = prm.G;
+  // XCD-aware remap (bijective): blocks that share an XCD get consecutive work ids
+  const int hw = blockIdx.x;
+  int g;
+  {
+    const int q = G / 8, r = G % 8, x = hw % 8;
+    g = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + hw / 8;
+  }
+  f32x4_t acc[K_::FM][K_::FN];
+  auto zero = [&]() {
+#pragma unroll
+    for (int i = 0; i < K_::FM; ++i)
+#pragma unroll
+      for (int j = 0; j < K_::FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  };
+
+  // One work loop (a single inlined copy of the segment and epilogue code keeps register
+  // allocation within 256 VGPRs): first the data-parallel rounds (whole tiles r*G + g), then
+  // this workgroup's stream-K iterations [lo, hi) of the remaining tiles' K loops.
+  const long long S = (long long)prm.sk_tiles * prm.NKT;
+  const long long lo = prm.sk_tiles ? (long long)g * S / G : 0, hi = prm.sk_tiles ? (long long)(g + 1) * S / G : 0;
+  int* flag = reinterpret_cast<int*>(smem + Geo<BN, NB>::SMEM - 16);
+  int r = 0;
+  long long it = lo;
+  for (;;) {
+    int tile, ts = 0, ka = 0, kb = prm.NKT;
+    bool sk = false;
+    if (r < prm.dp_rounds) {
+      tile = r * G + g;
+      ++r;
+    } else if (it < hi) {
+      ts = (int)(it / prm.NKT);
+      ka = (int)(it - (long long)ts * prm.NKT);
+      const long long tile_end = (long long)(ts + 1) * prm.NKT;
+      kb = (int)((hi < tile_end ? hi : tile_end) - (long long)ts * prm.NKT);
+      tile = prm.dp_rounds * G + ts;
+      sk = true;
+    } else {
+      break;
+    }
+    const bool partial = ka != 0 || kb != prm.NKT;
+    int mt, nt;
+    tile_coords(prm, tile, mt, nt);
+    zero();
+    k.run_segment(acc, mt, nt, ka, kb);
+    bool do_epi = true;
+    if (partial) {
+      // contributors: the workgroups whose ranges intersect this tile's iterations
+      const long long t0 = (long long)ts * prm.NKT, t1 = t0 + prm.NKT;
+      const int g_first = (int)(((t0 + 1) * G - 1) / S);
+      const int g_last = (int)((t1 * G - 1) / S);
+      k.slab_store(slab, (size_t)g * 2 + (it == lo ? 0 : 1), acc);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (k.tid == 0) {
+        const unsigned old = __hip_atomic_fetch_add(&counters[ts], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *flag = old == (unsigned)(g_last - g_first);
+      }
+      __syncthreads();
+      do_epi = *flag != 0;
+      if (do_epi) {
+        // fixed summation order (bitwise-reproducible results): with two contributors the
+        // sum is commutative; with more, every partial - this one's too - is re-read in order
+        const bool all = g_last - g_first > 1;
+        if (all) zero();
+        for (int c = g_first; c <= g_last; ++c) {
+          if (c == g && !all) continue;
+          const long long lo_c = (long long)c * S / G;
+          k.slab_add(slab, (size_t)c * 2 + (lo_c >= t0 ? 0 : 1), acc);  // slot 0: c started in this tile
+        }
+        if (k.tid == 0) __hip_atomic_store(&counters[ts], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    if (do_epi) k.epilogue(ep, acc, mt, nt);
+    __syncthreads();
+    if (sk) it = (long long)ts * prm.NKT + kb;
+  }
+}
+
+template <int BN, int EPI, int NB>
+int launch(const bf16_raw* A, const bf16_raw* W, const SkParams& prm, const EpiArgs& ep, float* slab,
+           unsigned* cnt, hipStream_t s) {
+  gemm_sk_kernel<BN, EPI, NB><<<prm.G, NTHR, 0, s>>>(A, W, prm, ep, slab, cnt);
+  LSA_CHECK_LAUNCH();
+  return LSA_OK;
+}
+
+}  // namespace
+
+// bn: tile width 256 (2-buffer DMA ring) or 128 (nb = 2 or 3 buffers; 0 = 3); grid: workgroups (<= 1024); dp: 1 = whole tiles in data-parallel rounds first (0 = all
+// stream-K); slab: >= 2 * grid * 256 * bn floats and counters: >= tiles ints (zeroed) when
+// any tile is split. Returns LSA_BAD_SHAPE on any shape the kernel's indexing cannot take.
+extern "C" int lsa_gemm_sk(const void* a, int lda, const void* wp, int M, int N, int K, int epi,
+                           const EpiArgs* ep, int bn, int nb, int grid, int dp, int group_m, float* slab,
+                           unsigned* counters, long long slab_floats, int n_counters, hipStream_t stream) {
+  if (M < 1 || K < BK || K % BK || lda < K || lda % 8 || !ep) return LSA_BAD_SHAPE;
+  if (bn != 256 && bn != 128) return LSA_UNSUPPORTED;
+  if (nb == 0) nb = bn == 256 ? 2 : 3;
+  if (nb != 2 && !(nb == 3 && bn == 128)) return LSA_UNSUPPORTED;
+  if (N % bn) return LSA_BAD_SHAPE;
+  if (grid < 1 || grid > 1024 || group_m < 1) return LSA_BAD_SHAPE;
+  if (epi == EPI_RESID && !ep->resid) return LSA_BAD_SHAPE;
+  if (epi == EPI_QKV && (!ep->k_cache || !ep->v_cache || !ep->slot || !ep->pos)) return LSA_BAD_SHAPE;
+  if (!ep->out) return LSA_BAD_SHAPE;
+  SkParams prm;
+  prm.M = M;
+  prm.N = N;
+  prm.K = K;
+  prm.lda = lda;
+  prm.MT = (M + BM - 1) / BM;
+  prm.NT = N / bn;
+  prm.NKT = K / BK;
+  prm.group_m = group_m;
+  const long long tiles = (long long)prm.MT * prm.NT;
+  if (tiles >= (1LL << 30)) return LSA_BAD_SHAPE;
+  const long long iters = tiles * prm.NKT;
+  prm.G = (int)(grid < iters ? grid : iters);
+  prm.dp_rounds = dp ? (int)(tiles / prm.G) : 0;
+  prm.sk_tiles = (int)(tiles - (long long)prm.dp_rounds * prm.G);
+  if (prm.sk_tiles > 0 && (long long)prm.sk_tiles * prm.NKT < prm.G) {
+    if (prm.dp_rounds > 0) {  // too few stream-K iterations for the grid: fold one round in
+      prm.dp_rounds -= 1;
+      prm.sk_tiles += prm.G;
+    } else {
+      prm.G = prm.sk_tiles * prm.NKT;  // every workgroup gets >= 1 iteration
+    }
+  }
+  if (prm.sk_tiles > 0 && (!slab || !counters || slab_floats < 2LL * prm.G * BM * bn || n_counters < prm.sk_tiles))
+    return LSA_BAD_SHAPE;
+  const bf16_raw* A = static_cast<const bf16_raw*>(a);
+  const bf16_raw* W = static_cast<const bf16_raw*>(wp);
+#define LSA_G(E) (bn == 256 ? launch<256, E, 2>(A, W, prm, *ep, slab, counters, stream)      \
+                          : nb == 3 ? launch<128, E, 3>(A, W, prm, *ep, slab, counters, stream) \
+                                    : launch<128, E, 2>(A, W, prm, *ep, slab, counters, stream))
+  switch (epi) {
+    case EPI_STORE: return LSA_G(EPI_STORE);
+    case EPI_RESID: return LSA_G(EPI_RESID);
+    case EPI_QKV: return LSA_G(EPI_QKV);
+    case EPI_SWIGLU: return LSA_G(EPI_SWIGLU);
+    default: return LSA_UNSUPPORTED;
+  }
+#undef LSA_G
+}

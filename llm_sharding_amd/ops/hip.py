@@ -67,7 +67,10 @@ def lib() -> ctypes.CDLL:
     L.lsa_argmax_finalize.argtypes = [vp, i, vp, vp, i, vp, i, i, vp, vp]
     L.lsa_pos_advance.argtypes = [vp, i, i, vp]
     L.lsa_epilogue_apply.argtypes = [vp, i, i, i, i, ctypes.POINTER(EpiArgs), vp]
-    for name in ("lsa_gemv", "lsa_gemv_coop", "lsa_gemv_fp8", "lsa_dequant_fp8_packed", "lsa_gemv_coop_fp8", "lsa_gemm", "lsa_attn_decode", "lsa_attn_prefill", "lsa_embed", "lsa_rmsnorm", "lsa_layernorm",
+    L.lsa_gemm_sk.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(EpiArgs), i, i, i, i, i, vp, vp, ctypes.c_longlong, i,
+                              vp]
+    for name in ("lsa_gemv", "lsa_gemv_coop", "lsa_gemv_fp8", "lsa_dequant_fp8_packed", "lsa_gemv_coop_fp8", "lsa_gemm",
+                 "lsa_gemm_sk", "lsa_attn_decode", "lsa_attn_prefill", "lsa_embed", "lsa_rmsnorm", "lsa_layernorm",
                  "lsa_argmax_finalize", "lsa_pos_advance", "lsa_epilogue_apply", "lsa_version"):
         getattr(L, name).restype = ctypes.c_int
     _lib = L
@@ -304,6 +307,77 @@ def gemm(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep
     rc = lib().lsa_gemm(_p(a), a.stride(0), _p(wp), M, N, K, epi, ctypes.byref(ep), tn, sk, _p(slab), _p(cnt),
                         _stream())
     _check(rc, "lsa_gemm")
+
+
+SK_BM = 256  # gemm_sk.hip row tile
+
+
+class SkWorkspace:
+    """Stream-K partial slabs (2 per workgroup, 256 x BN fp32 each) + per-tile arrival tickets
+    for ``lsa_gemm_sk``. Tickets reset themselves (the last arriver zeroes its tile's); slabs
+    need no initialisation. One workspace per stream / concurrently replayed graph."""
+
+    def __init__(self, device, grid: int = 256, bn: int = 256):
+        self.grid, self.bn = grid, bn
+        self.slab = torch.empty(2 * grid * SK_BM * bn, dtype=torch.float32, device=device)
+        self.counters = torch.zeros(4 * grid, dtype=torch.int32, device=device)
+
+
+_SKWS = {}
+
+
+def default_sk_workspace(device=None) -> SkWorkspace:
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    key = (dev.index, torch.cuda.current_stream(dev).cuda_stream)
+    if key not in _SKWS:
+        _SKWS[key] = SkWorkspace(dev)
+    return _SKWS[key]
+
+
+N_CU = 256
+
+
+def gemm_sk_plan(M: int, N: int, K: int) -> tuple:
+    """(bn, grid, dp) for ``gemm_sk``: 256 x 256 tiles where the grid stays filled, 256 x 128
+    tiles when a 256-column tiling leaves each tile split over many workgroups (few, long
+    tiles: o/down projections of a 512-row decode batch). Grid = one workgroup per CU (the
+    kernel holds 136 KiB of LDS); stream-K spreads the leftover tiles' K loops over it."""
+    mt = -(-M // SK_BM)
+    nkt = K // 64
+    bn = 256 if N % 256 == 0 else 128
+    if bn == 256 and N % 128 == 0:
+        tiles = mt * (N // 256)
+        if tiles < N_CU and tiles * nkt < 16 * N_CU:  # > 4 contributors per 256-col tile
+            bn = 128
+    tiles = mt * (N // bn)
+    grid = min(N_CU, tiles * nkt)
+    return bn, grid, 1
+
+
+def gemm_sk(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep: EpiArgs,
+            bn: int = 0, grid: int = 0, dp: int = 1, group_m: int = 8, nb: int = 0,
+            ws: Optional[SkWorkspace] = None) -> None:
+    """Projection GEMM for any M (gemm_sk.hip): 256 x ``bn`` tiles, LDS-DMA staged, data-parallel
+    rounds + stream-K, fused epilogue. ``wp`` = pack_b(W[N, K]); N % bn == 0, K % 64 == 0."""
+    _req(_is_bf16_cuda(a, wp), "gemm_sk: bf16 cuda tensors required")
+    _req(wp.numel() == N * K and K % 64 == 0 and K >= 64, "gemm_sk: packed weight shape")
+    _req(a.dim() == 2 and a.shape[0] >= M >= 1 and a.shape[1] >= K and a.stride(1) == 1 and a.stride(0) % 8 == 0,
+         "gemm_sk: A must be [>=M, >=K] row-major with 16-B aligned rows")
+    _req(a.data_ptr() % 16 == 0, "gemm_sk: A must be 16-byte aligned")
+    _check_epi(epi, ep, N)
+    _req(epi in (EPI_STORE, EPI_RESID, EPI_SWIGLU, EPI_QKV), f"gemm_sk: epilogue {epi} not supported")
+    pb, pg, pd = gemm_sk_plan(M, N, K)
+    bn = bn or pb
+    grid = grid or pg
+    _req(bn in (128, 256) and N % bn == 0, f"gemm_sk: N={N} not a multiple of bn={bn}")
+    _req(1 <= grid <= 1024, "gemm_sk: grid")
+    if ws is None:
+        ws = default_sk_workspace(a.device)
+    _req(ws.slab.numel() >= 2 * grid * SK_BM * bn and ws.counters.numel() >= 2 * grid,
+         f"gemm_sk: workspace too small for grid={grid} bn={bn}")
+    rc = lib().lsa_gemm_sk(_p(a), a.stride(0), _p(wp), M, N, K, epi, ctypes.byref(ep), bn, nb, grid, dp, group_m,
+                           _p(ws.slab), _p(ws.counters), ws.slab.numel(), ws.counters.numel(), _stream())
+    _check(rc, "lsa_gemm_sk")
 
 
 def epilogue_apply(c: torch.Tensor, M: int, N: int, epi: int, ep: EpiArgs) -> None:

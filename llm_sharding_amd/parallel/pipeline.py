@@ -141,7 +141,10 @@ class PipelineStage:
                  microbatches: int, max_seq: int, source, use_graph: bool = True,
                  max_prefill_rows: int = 2048, dtype=torch.bfloat16, p2p=None,
                  split_head: Optional[bool] = None, weight_dtype: str = "bf16", streams: int = 1,
-                 pp_streams: Optional[bool] = None):
+                 pp_streams: Optional[bool] = None, engine: Optional[StageEngine] = None):
+        """``engine``: reuse a loaded StageEngine (its weights, KV cache and scratch) instead of
+        building one - e.g. a batch-1 latency pass after a throughput pass; it must cover this
+        stage's layers and hold >= batch x microbatches KV slots."""
         self.cfg, self.rank, self.world = cfg, rank, world
         self.p2p = p2p if p2p is not None else DistP2P()
         self.first, self.last = rank == 0, rank == world - 1
@@ -162,11 +165,19 @@ class PipelineStage:
             head_cols = (0, v1)
         elif self.split and self.first:
             head_cols = (v1, V)
-        self.eng = StageEngine(cfg, start, end, device, self.dtype, has_embed=self.first,
-                               has_head=self.last or (self.split and self.first), source=source,
-                               max_slots=batch * microbatches, max_seq=max_seq,
-                               max_prefill_rows=max(max_prefill_rows, batch), head_cols=head_cols,
-                               weight_dtype=weight_dtype)
+        if engine is not None:
+            ok = (engine.start, engine.end) == (start, end) and engine.max_slots >= batch * microbatches
+            if engine.has_head:
+                ok = ok and (engine.head_v0, engine.head_v1) == (head_cols or (0, cfg.head_rows))
+            if not ok:
+                raise ValueError("PipelineStage: the shared engine does not match this stage")
+            self.eng = engine
+        else:
+            self.eng = StageEngine(cfg, start, end, device, self.dtype, has_embed=self.first,
+                                   has_head=self.last or (self.split and self.first), source=source,
+                                   max_slots=batch * microbatches, max_seq=max_seq,
+                                   max_prefill_rows=max(max_prefill_rows, batch), head_cols=head_cols,
+                                   weight_dtype=weight_dtype)
         H = cfg.hidden_size
         self.h_out = [torch.zeros((batch, H), dtype=self.dtype, device=self.device) for _ in range(microbatches)]
         self.tok_out = [torch.zeros(batch, dtype=torch.int32, device=self.device) for _ in range(microbatches)]
@@ -484,11 +495,60 @@ def drive_local_pipeline(cfg, source, prompts: torch.Tensor, n_new: int, n_stage
     return torch.cat([first, hist], dim=0)
 
 
+LAT_WARMUP = 4  # untimed steps of the batch-1 latency pass
+
+
+def _tpot_from_events(events: list) -> list:
+    """Per-token latencies (ms) between consecutive decode replays of each micro-batch."""
+    by_mb: dict = {}
+    for s, mb, ev in events:
+        by_mb.setdefault(mb, []).append(ev)
+    out = []
+    for evs in by_mb.values():
+        for a, b in zip(evs, evs[1:]):
+            out.append(a.elapsed_time(b))
+    return out
+
+
+def _latency_pass(cfg, stage: "PipelineStage", srank: int, pp: int, st, dev, max_seq: int, prompts,
+                  prompt_len: int, steps: int, dist, sync, p2p) -> tuple:
+    """Batch-1 decode through the pipeline on the already loaded stage engine (KV slot 0 is
+    reused): prefill one prompt, LAT_WARMUP untimed steps, ``steps`` timed ones. Returns (p50
+    per-token latency in ms on the last stage - 0.0 elsewhere -, timed wall seconds)."""
+    eng = stage.eng
+    eng.reset([0])
+    b1 = PipelineStage(cfg, srank, pp, st.start, st.end, dev, 1, 1, max_seq, None,
+                       use_graph=stage.use_graph, dtype=stage.dtype, p2p=p2p, engine=eng)
+    b1.tl = stage.tl
+    p1 = prompts[:1, :1].contiguous() if prompts is not None else None
+    firsts = b1.prefill(p1, prompt_len)
+    b1.build_graphs(firsts, history_len=LAT_WARMUP + steps)
+    for s in range(LAT_WARMUP):
+        b1.step(s)
+    b1.drain()
+    sync()
+    if dist:
+        dist.barrier()
+    sync()
+    events: list = []
+    t0 = time.perf_counter()
+    for s in range(steps):
+        b1.step(LAT_WARMUP + s, events if b1.last else None)
+    b1.drain()
+    sync()
+    if dist:
+        dist.barrier()
+    sync()
+    el = time.perf_counter() - t0
+    tp = _tpot_from_events(events) if b1.last else []
+    return (_percentile(tp, 0.5) if tp else 0.0), el
+
+
 def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int = 64, warmup: int = 8,
                          batch: int = 16, prompt_len: int = 128, max_seq: int = 0,
                          microbatches: int = 0, seed: int = 0, use_graph: bool = True,
                          verbose: bool = True, weight_dtype: str = "bf16", streams: int = 1,
-                         device: str = "cuda", dp: int = 1) -> Optional[dict]:
+                         device: str = "cuda", dp: int = 1, latency_steps: int = 0) -> Optional[dict]:
     """``microbatches`` 0 = ``streams`` x stages (every GPU holds ``streams`` micro-batches of
     ``batch`` sequences: weak scaling); ``max_seq`` 0 = what the run needs, rounded up to 64.
 
@@ -532,7 +592,7 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
         if gpu:
             torch.cuda.synchronize()
     M = microbatches or streams * pp
-    need = prompt_len + warmup + steps + 1
+    need = prompt_len + max(warmup + steps, (LAT_WARMUP + latency_steps) if latency_steps else 0) + 1
     max_seq = max_seq or -(-need // 64) * 64
     plan = plan_stages(cfg, pp, kv_tokens=max_seq * batch * M, head_split=pp > 1)
     st = plan.stages[srank]
@@ -589,16 +649,27 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
     elapsed = time.perf_counter() - t_start
 
     # per-token latency of each sequence = time between its consecutive tokens (last stage)
-    tpot = []
-    if stage.last:
-        by_mb: dict = {}
-        for s, mb, ev in events:
-            by_mb.setdefault(mb, []).append(ev)
-        for evs in by_mb.values():
-            for a, b in zip(evs, evs[1:]):
-                tpot.append(a.elapsed_time(b))
+    tpot = _tpot_from_events(events) if stage.last else []
+    # the first warmup + steps generated ids of micro-batch 0 (for parity checks across layouts)
+    tokens_mb0 = None
+    if stage.history_stage and stage.graphs[0].history is not None:
+        n_tok = warmup + steps
+        hist = stage.graphs[0].history.cpu()
+        if stage.split:  # row k = generated token k (re-derived at step k)
+            tokens_mb0 = hist[:n_tok].T.tolist()
+        else:  # row k = token produced at decode step k, after the prefill's first token
+            tokens_mb0 = torch.cat([firsts[0].cpu()[None].to(hist.dtype), hist[:n_tok - 1]]).T.tolist() \
+                if firsts else None
+
+    # batch-1 latency pass (the reference's only mode, node_worker.py:493-559): ONE sequence
+    # through the same pipeline and weights, a 1-row decode graph per stage
+    lat_p50 = lat_el = 0.0
+    if latency_steps > 0:
+        lat_p50, lat_el = _latency_pass(cfg, stage, srank, pp, st, dev, max_seq, prompts, prompt_len,
+                                        latency_steps, dist, sync, p2p)
     stats = torch.tensor([elapsed, ttft_ms, _percentile(tpot, 0.5) if tpot else 0.0,
-                          _percentile(tpot, 0.9) if tpot else 0.0, load_s], dtype=torch.float64, device=dev)
+                          _percentile(tpot, 0.9) if tpot else 0.0, load_s, lat_el, lat_p50],
+                         dtype=torch.float64, device=dev)
     if not gpu and stage.last:  # no device events on CPU: wall-clock step time stands in for TPOT
         stats[2] = stats[3] = elapsed * 1e3 / steps
     if dist:
@@ -609,8 +680,12 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
         ttft_ms = float(allst[0, 1])
         p50, p90 = float(allst[pp - 1, 2]), float(allst[pp - 1, 3])  # replica 0's last stage
         load_s = float(allst[:, 4].max())
+        lat_el, lat_p50 = float(allst[:, 5].max()), float(allst[pp - 1, 6])
     else:
         p50, p90 = float(stats[2]), float(stats[3])
+        lat_el, lat_p50 = float(stats[5]), float(stats[6])
+    if latency_steps > 0 and not gpu:
+        lat_p50 = lat_el * 1e3 / latency_steps
     tokens = dp * steps * M * batch
     res = {
         "tok_s": tokens / elapsed,
@@ -627,6 +702,9 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
         "model_name": "Llama-2-7B" if model == "llama2-7b" else cfg.name,
         "load_s": load_s,
         "plan": plan.ranges(),
+        "tokens_mb0": tokens_mb0,  # rank 0 only when it holds the history (1 stage or split head)
+        "b1_p50_tpot_ms": lat_p50 if latency_steps > 0 else None,
+        "b1_tok_s": (dp * latency_steps / lat_el) if latency_steps > 0 and lat_el > 0 else None,
     }
     trace = tracing.export_env(stage.tl)
     if trace and verbose:

@@ -1,0 +1,147 @@
+"""gemm_sk.hip (LDS-DMA 256 x BN tiles, data-parallel rounds + stream-K, fused epilogues)
+against plain PyTorch fp32 references: every epilogue, both tile widths, grids that split tiles
+between workgroups (stream-K partial slabs + last-arriver combine) and grids that do not."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from llm_sharding_amd.ops import packing
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def hip():
+    from llm_sharding_amd.ops import hip as h
+    h.lib()
+    return h
+
+
+def rel_err(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def _rnd(*shape, scale=1.0):
+    return (torch.randn(*shape, device=DEV) * scale).to(torch.bfloat16)
+
+
+@pytest.fixture(scope="module")
+def ws():
+    return hip().SkWorkspace(DEV, grid=1024, bn=256)
+
+
+# (bn, grid, dp): planner default, whole-tile rounds, pure stream-K, odd grids (bijective XCD remap)
+CFGS = [(0, 0, 1), (256, 256, 1), (128, 256, 1), (256, 37, 0), (128, 13, 1), (256, 1000, 0)]
+
+
+@pytest.mark.parametrize("M", [1, 129, 256, 300, 512, 777])
+@pytest.mark.parametrize("N,K", [(1024, 512), (512, 4096), (768, 1216)])
+def test_gemm_sk_store_resid(M, N, K, ws):
+    h = hip()
+    a = _rnd(M, K)
+    w = _rnd(N, K, scale=0.02)
+    wp = packing.pack_b(w)
+    ref = a.float() @ w.float().T
+    r = _rnd(M, N)
+    for (bn, grid, dp) in CFGS:
+        if bn and N % bn:
+            continue
+        out = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
+        h.gemm_sk(a, wp, M, N, K, h.EPI_STORE, h.make_epi(out=out, ldo=N), bn=bn, grid=grid, dp=dp, ws=ws)
+        assert rel_err(out, ref) < 8e-3, (bn, grid, dp)
+        o2 = r.clone()
+        h.gemm_sk(a, wp, M, N, K, h.EPI_RESID, h.make_epi(out=o2, resid=o2, ldo=N, ldr=N), bn=bn, grid=grid, dp=dp,
+                  ws=ws)
+        assert rel_err(o2, r.float() + ref) < 8e-3, (bn, grid, dp)
+    assert int(ws.counters.abs().sum()) == 0  # every split tile's ticket was reset
+
+
+def test_gemm_sk_strided_a_and_big_m(ws):
+    """A with a row stride > K (a view into a wider buffer) and enough rows for several
+    data-parallel rounds plus a stream-K tail."""
+    h = hip()
+    M, N, K = 4100, 1280, 320
+    buf = _rnd(M, K + 64)
+    a = buf[:, 32:32 + K]
+    w = _rnd(N, K, scale=0.05)
+    out = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
+    h.gemm_sk(a, packing.pack_b(w), M, N, K, h.EPI_STORE, h.make_epi(out=out, ldo=N), bn=256, grid=16, ws=ws)
+    assert rel_err(out, a.float() @ w.float().T) < 8e-3
+
+
+@pytest.mark.parametrize("M", [200, 512, 1030])
+def test_gemm_sk_swiglu(M, ws):
+    h = hip()
+    I, H = 1024, 512
+    x = _rnd(M, H)
+    wg, wu = _rnd(I, H, scale=0.05), _rnd(I, H, scale=0.05)
+    wp = packing.pack_b(packing.fuse_gate_up(wg, wu))
+    ref = F.silu(x.float() @ wg.float().T) * (x.float() @ wu.float().T)
+    for (bn, grid, dp) in CFGS:
+        out = torch.zeros(M, I, dtype=torch.bfloat16, device=DEV)
+        h.gemm_sk(x, wp, M, 2 * I, H, h.EPI_SWIGLU, h.make_epi(out=out, ldo=I), bn=bn, grid=grid, dp=dp, ws=ws)
+        assert rel_err(out, ref) < 1e-2, (bn, grid, dp)
+
+
+def _rope_ref(t, pos, cos, sin):
+    half = t.shape[-1] // 2
+    c, s = cos[pos][:, None, :], sin[pos][:, None, :]
+    t1, t2 = t[..., :half], t[..., half:]
+    return torch.cat([t1 * c - t2 * s, t2 * c + t1 * s], dim=-1)
+
+
+@pytest.mark.parametrize("nh,nkv,hd", [(32, 32, 128), (8, 2, 64), (24, 8, 128)])
+@pytest.mark.parametrize("cfg", [(0, 0, 1), (128, 29, 0)])
+def test_gemm_sk_qkv_rope_kv_append(nh, nkv, hd, cfg, ws):
+    from llm_sharding_amd.config import tiny
+    from llm_sharding_amd.models.rope import rope_table
+    h = hip()
+    H, M, slots, T = 512, 300, 3, 512
+    wq, wk, wv = _rnd(nh * hd, H, scale=0.05), _rnd(nkv * hd, H, scale=0.05), _rnd(nkv * hd, H, scale=0.05)
+    x = _rnd(M, H)
+    cos, sin = rope_table(tiny(head_dim=hd), T, DEV)
+    slot = torch.randint(0, slots, (M,), device=DEV, dtype=torch.int32)
+    pos = torch.randperm(T, device=DEV)[:M].to(torch.int32)
+    q = torch.zeros(M, nh * hd, dtype=torch.bfloat16, device=DEV)
+    kc = torch.zeros(slots, nkv, T, hd, dtype=torch.bfloat16, device=DEV)
+    vc = torch.zeros_like(kc)
+    wp = packing.pack_b(packing.fuse_qkv(wq, wk, wv, nh, nkv, hd))
+    N = (nh + 2 * nkv) * hd
+    ep = h.make_epi(out=q, k_cache=kc, v_cache=vc, slot=slot, pos=pos, cos=cos, sin=sin, ldo=nh * hd,
+                    n_heads=nh, n_kv=nkv, head_dim=hd, t_max=T)
+    bn, grid, dp = cfg
+    if bn and N % bn:
+        pytest.skip("N not a multiple of bn")
+    h.gemm_sk(x, wp, M, N, H, h.EPI_QKV, ep, bn=bn, grid=grid, dp=dp, ws=ws)
+    xf, pl, sl = x.float(), pos.long(), slot.long()
+    qr = _rope_ref((xf @ wq.float().T).view(M, nh, hd), pl, cos, sin).reshape(M, -1)
+    kr = _rope_ref((xf @ wk.float().T).view(M, nkv, hd), pl, cos, sin)
+    vr = (xf @ wv.float().T).view(M, nkv, hd)
+    assert rel_err(q, qr) < 1e-2
+    assert rel_err(kc[sl, :, pl], kr) < 1e-2
+    assert rel_err(vc[sl, :, pl], vr) < 1e-2
+
+
+def test_gemm_sk_graph_replay(ws):
+    """Captured in a hipGraph and replayed: the self-resetting tickets must leave every replay
+    identical to the eager result."""
+    h = hip()
+    M, N, K = 512, 4096, 1024
+    a = _rnd(M, K)
+    w = _rnd(N, K, scale=0.02)
+    wp = packing.pack_b(w)
+    out = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
+    ep = h.make_epi(out=out, ldo=N)
+    h.gemm_sk(a, wp, M, N, K, h.EPI_STORE, ep, bn=128, grid=256, ws=ws)
+    torch.cuda.synchronize()
+    first = out.clone()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        h.gemm_sk(a, wp, M, N, K, h.EPI_STORE, ep, bn=128, grid=256, ws=ws)
+    for _ in range(3):
+        out.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert rel_err(out, first) < 1e-6
+    assert rel_err(first, a.float() @ w.float().T) < 8e-3

@@ -190,3 +190,12 @@ def test_bench_driver_eight_ranks_cpu():
     assert res["microbatches"] == world and res["global_batch"] == 2 * world
     assert len(res["plan"]) == world
     assert res["tok_s"] > 0 and res["p50_tpot_ms"] > 0
+    # token parity: micro-batch 0 of the 8-stage split-head ring generates exactly what one
+    # process generates for the same prompts (same seed -> same first micro-batch) and weights
+    from llm_sharding_amd.parallel.pipeline import run_decode_benchmark
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        assert k not in os.environ
+    one = run_decode_benchmark(model="tiny8", n_gpus=1, steps=3, warmup=2, batch=2, prompt_len=4, streams=1,
+                               device="cpu", verbose=False)
+    assert res["tokens_mb0"] is not None and one["tokens_mb0"] is not None
+    assert res["tokens_mb0"] == one["tokens_mb0"]
