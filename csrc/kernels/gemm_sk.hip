@@ -51,7 +51,11 @@ struct SkParams {
   int MT, NT, NKT;       // 256-row tiles, BN-col tiles, 64-deep K tiles
   int G;                 // workgroups
   int dp_rounds;         // full rounds of whole tiles (tile r*G + g)
-  int sk_tiles;          // tiles after the data-parallel rounds, spread by K iterations
+  int sk_tiles;          // tiles after the data-parallel rounds (the remainder)
+  int split;             // 0: remainder spread by K iterations over the grid (stream-K);
+                         // S >= 1: each remainder tile split into S equal K ranges (workgroup
+                         // g < sk_tiles * S takes tile g % sk_tiles, range g / sk_tiles), so
+                         // concurrently running workgroups stream the same K offsets (L2 reuse)
   int group_m;           // grouped tile order: this many row tiles share a column sweep
 };
 
@@ -60,6 +64,21 @@ template <int N>
 LSA_DEVICE void vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
 }
+
+// Diagnostic build only (-DLSA_GEMM_STAMPS, scripts/gemm_stamps.py): per-workgroup
+// s_memrealtime stamps (100 MHz) at the phase boundaries of each work item, written by thread 0
+// to a buffer nothing else reads. The production library never defines it.
+#ifdef LSA_GEMM_STAMPS
+__device__ unsigned long long* g_stamps;
+#define LSA_STAMP(slot)                                                                        \
+  do {                                                                                         \
+    if (threadIdx.x == 0 && g_stamps) g_stamps[blockIdx.x * 32 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define LSA_STAMP(slot) \
+  do {                  \
+  } while (0)
+#endif
 
 LSA_DEVICE void barrier() {
   __builtin_amdgcn_sched_barrier(0);
@@ -116,7 +135,9 @@ struct Kern {
   }
 
   // ---- one segment: K-tiles [ka, kb) of output tile (mt, nt), accumulated into acc -------------
+  int stamp_base = 0;
   LSA_DEVICE void run_segment(f32x4_t (&acc)[FM][FN], int mt, int nt, int ka, int kb) {
+    LSA_STAMP(stamp_base + 0);
     const SkParams& P = *p;
     const int n = kb - ka;
     const int m0 = mt * BM, n0 = nt * BN;
@@ -164,6 +185,7 @@ struct Kern {
     }
     barrier();
     if (group) barrier();  // stagger: waves 4-7 run one barrier behind waves 0-3
+    LSA_STAMP(stamp_base + 1);
 
     u32x4_t a[HM][2], b0[HN][2], b1[HN][2];
     auto rd_a = [&](int buf, int mh) {
@@ -265,19 +287,37 @@ struct Kern {
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, acc[i][j]), sr,
                                                ((w * FM * FN + i * FN + j) * 64 + lane) * 16, 0, 16);
   }
+  // Adds partial slab ``slot`` into acc. The slab's fragment blocks (1 KiB, lane-linear) go
+  // LDS-DMA -> this wave's private LDS ring (2 buffers of RP tile rows) -> registers, so RP*FN
+  // write-through reads stay in flight while the previous group is added (the slab lines are
+  // read sc1: they bypass this CU's L1, which may hold stale copies). Caller: every wave, LDS
+  // free (and a barrier before the LDS is reused by other waves).
   LSA_DEVICE void slab_add(const float* slab, size_t slot, f32x4_t (&acc)[FM][FN]) {
-    const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc((void*)(slab + slot * (size_t)(BM * BN)),
-                                                                         (short)0, BM * BN * 4, 0x00020000);
-    // one 16x16-tile row (FN loads) at a time: with every load hoisted ahead of the adds the
-    // 128 accumulator registers plus 128 load destinations would spill
+    constexpr int RP = 2, NP = FM / RP, PB = RP * FN;  // tile rows per pass, passes, blocks per pass
+    const unsigned char* src = reinterpret_cast<const unsigned char*>(slab + slot * (size_t)(BM * BN)) +
+                               (size_t)(w * FM * FN) * 1024 + lane * 16;
+    unsigned char* ring = smem + w * (2 * PB * 1024);
+    auto issue = [&](int pass) {
 #pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      u32x4_t v[FN];
+      for (int q = 0; q < PB; ++q)
+        __builtin_amdgcn_global_load_lds(src + ((pass * RP + q / FN) * FN + q % FN) * 1024,
+                                         (__attribute__((address_space(3))) void*)(ring + ((pass & 1) * PB + q) * 1024),
+                                         16, 0, 16 /* sc1 */);
+    };
+    issue(0);
 #pragma unroll
-      for (int j = 0; j < FN; ++j)
-        v[j] = __builtin_amdgcn_raw_buffer_load_b128(sr, ((w * FM * FN + i * FN + j) * 64 + lane) * 16, 0, 16);
+    for (int pass = 0; pass < NP; ++pass) {
+      if (pass + 1 < NP) {
+        issue(pass + 1);
+        vm_wait<PB>();
+      } else {
+        vm_wait<0>();
+      }
+      const unsigned char* rb = ring + (pass & 1) * PB * 1024 + lane * 16;
 #pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] += __builtin_bit_cast(f32x4_t, v[j]);
+      for (int q = 0; q < PB; ++q)
+        acc[pass * RP + q / FN][q % FN] += __builtin_bit_cast(f32x4_t, ld16(rb + q * 1024));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads retired before the buffer is refilled
       __builtin_amdgcn_sched_barrier(0);
     }
   }
@@ -387,12 +427,28 @@ __global__ __launch_bounds__(NTHR) void gemm_sk_kernel(const bf16_raw* __restric
   int* flag = reinterpret_cast<int*>(smem + Geo<BN, NB>::SMEM - 16);
   int r = 0;
   long long it = lo;
+  bool split_done = false;
+  // split mode: U = sk_tiles * split work units spread EVENLY over the XCDs (units u, u+1 of
+  // one K range - neighbouring tiles that share A or W panels - on one XCD); blocks beyond U idle
+  int su = -1;
+  if (prm.split) {
+    const int U = prm.sk_tiles * prm.split, q = U / 8, rr = U % 8, x = hw % 8, j = hw / 8;
+    if (j < (x < rr ? q + 1 : q)) su = (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + j;
+  }
   for (;;) {
     int tile, ts = 0, ka = 0, kb = prm.NKT;
     bool sk = false;
     if (r < prm.dp_rounds) {
       tile = r * G + g;
       ++r;
+    } else if (prm.split) {
+      if (split_done || su < 0) break;
+      ts = su % prm.sk_tiles;
+      const int sp = su / prm.sk_tiles;
+      ka = sp * prm.NKT / prm.split;
+      kb = (sp + 1) * prm.NKT / prm.split;
+      tile = prm.dp_rounds * G + ts;
+      split_done = true;
     } else if (it < hi) {
       ts = (int)(it / prm.NKT);
       ka = (int)(it - (long long)ts * prm.NKT);
@@ -408,13 +464,15 @@ __global__ __launch_bounds__(NTHR) void gemm_sk_kernel(const bf16_raw* __restric
     tile_coords(prm, tile, mt, nt);
     zero();
     k.run_segment(acc, mt, nt, ka, kb);
+    LSA_STAMP(k.stamp_base + 2);
     bool do_epi = true;
     if (partial) {
-      // contributors: the workgroups whose ranges intersect this tile's iterations
+      // contributors of this tile, in K order: split mode - workgroups ts + s * sk_tiles
+      // (slot 0); stream-K - the workgroups whose iteration ranges intersect the tile's
       const long long t0 = (long long)ts * prm.NKT, t1 = t0 + prm.NKT;
-      const int g_first = (int)(((t0 + 1) * G - 1) / S);
-      const int g_last = (int)((t1 * G - 1) / S);
-      k.slab_store(slab, (size_t)g * 2 + (it == lo ? 0 : 1), acc);
+      const int g_first = prm.split ? 0 : (int)(((t0 + 1) * G - 1) / S);
+      const int g_last = prm.split ? prm.split - 1 : (int)((t1 * G - 1) / S);
+      k.slab_store(slab, prm.split ? (size_t)su * 2 : (size_t)g * 2 + (it == lo ? 0 : 1), acc);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (k.tid == 0) {
@@ -422,21 +480,33 @@ __global__ __launch_bounds__(NTHR) void gemm_sk_kernel(const bf16_raw* __restric
         *flag = old == (unsigned)(g_last - g_first);
       }
       __syncthreads();
+      LSA_STAMP(k.stamp_base + 3);
       do_epi = *flag != 0;
       if (do_epi) {
         // fixed summation order (bitwise-reproducible results): with two contributors the
         // sum is commutative; with more, every partial - this one's too - is re-read in order
         const bool all = g_last - g_first > 1;
         if (all) zero();
-        for (int c = g_first; c <= g_last; ++c) {
-          if (c == g && !all) continue;
-          const long long lo_c = (long long)c * S / G;
-          k.slab_add(slab, (size_t)c * 2 + (lo_c >= t0 ? 0 : 1), acc);  // slot 0: c started in this tile
+        for (int ci = g_first; ci <= g_last; ++ci) {
+          int c, slot;
+          if (prm.split) {
+            c = ts + ci * prm.sk_tiles;
+            slot = 0;
+          } else {
+            c = ci;
+            slot = (long long)c * S / G >= t0 ? 0 : 1;  // slot 0: c's range starts in this tile
+          }
+          if (c == (prm.split ? su : g) && !all) continue;
+          k.slab_add(slab, (size_t)c * 2 + slot, acc);
         }
         if (k.tid == 0) __hip_atomic_store(&counters[ts], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();  // every wave's slab ring reads are done before the epilogue reuses LDS
       }
     }
+    LSA_STAMP(k.stamp_base + 4);
     if (do_epi) k.epilogue(ep, acc, mt, nt);
+    LSA_STAMP(k.stamp_base + 5);
+    k.stamp_base = k.stamp_base + 6 < 30 ? k.stamp_base + 6 : 24;
     __syncthreads();
     if (sk) it = (long long)ts * prm.NKT + kb;
   }
@@ -452,11 +522,13 @@ int launch(const bf16_raw* A, const bf16_raw* W, const SkParams& prm, const EpiA
 
 }  // namespace
 
-// bn: tile width 256 (2-buffer DMA ring) or 128 (nb = 2 or 3 buffers; 0 = 3); grid: workgroups (<= 1024); dp: 1 = whole tiles in data-parallel rounds first (0 = all
-// stream-K); slab: >= 2 * grid * 256 * bn floats and counters: >= tiles ints (zeroed) when
+// bn: tile width 256 (2-buffer DMA ring) or 128 (nb = 2 or 3 buffers; 0 = 3); grid: workgroups
+// (<= 1024); dp: 1 = whole tiles in data-parallel rounds first (0 = all tiles are remainder);
+// split: 0 = remainder by stream-K, S >= 1 = remainder tiles split into up to S K ranges
+// (clamped to NKT and to grid / remainder tiles; stream-K when the remainder exceeds the grid); slab: >= 2 * grid * 256 * bn floats and counters: >= remainder tiles (zeroed) when
 // any tile is split. Returns LSA_BAD_SHAPE on any shape the kernel's indexing cannot take.
 extern "C" int lsa_gemm_sk(const void* a, int lda, const void* wp, int M, int N, int K, int epi,
-                           const EpiArgs* ep, int bn, int nb, int grid, int dp, int group_m, float* slab,
+                           const EpiArgs* ep, int bn, int nb, int grid, int dp, int split, int group_m, float* slab,
                            unsigned* counters, long long slab_floats, int n_counters, hipStream_t stream) {
   if (M < 1 || K < BK || K % BK || lda < K || lda % 8 || !ep) return LSA_BAD_SHAPE;
   if (bn != 256 && bn != 128) return LSA_UNSUPPORTED;
@@ -482,7 +554,12 @@ extern "C" int lsa_gemm_sk(const void* a, int lda, const void* wp, int M, int N,
   prm.G = (int)(grid < iters ? grid : iters);
   prm.dp_rounds = dp ? (int)(tiles / prm.G) : 0;
   prm.sk_tiles = (int)(tiles - (long long)prm.dp_rounds * prm.G);
-  if (prm.sk_tiles > 0 && (long long)prm.sk_tiles * prm.NKT < prm.G) {
+  prm.split = 0;
+  if (split > 0 && prm.sk_tiles > 0 && prm.sk_tiles <= prm.G) {
+    // at most NKT ranges per tile and sk_tiles * split <= G workgroups
+    prm.split = split < prm.NKT ? split : prm.NKT;
+    if (prm.split > prm.G / prm.sk_tiles) prm.split = prm.G / prm.sk_tiles;
+  } else if (prm.sk_tiles > 0 && (long long)prm.sk_tiles * prm.NKT < prm.G) {
     if (prm.dp_rounds > 0) {  // too few stream-K iterations for the grid: fold one round in
       prm.dp_rounds -= 1;
       prm.sk_tiles += prm.G;
@@ -506,3 +583,9 @@ extern "C" int lsa_gemm_sk(const void* a, int lda, const void* wp, int M, int N,
   }
 #undef LSA_G
 }
+
+#ifdef LSA_GEMM_STAMPS
+extern "C" int lsa_gemm_sk_set_stamps(unsigned long long* buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &buf, sizeof(buf)) == hipSuccess ? LSA_OK : LSA_LAUNCH_FAILED;
+}
+#endif

@@ -66,12 +66,11 @@ def lib() -> ctypes.CDLL:
     L.lsa_layernorm.argtypes = [vp, i, vp, vp, vp, vp, i, i, f, vp, i, vp]
     L.lsa_argmax_finalize.argtypes = [vp, i, vp, vp, i, vp, i, i, vp, vp]
     L.lsa_pos_advance.argtypes = [vp, i, i, vp]
-    L.lsa_epilogue_apply.argtypes = [vp, i, i, i, i, ctypes.POINTER(EpiArgs), vp]
-    L.lsa_gemm_sk.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(EpiArgs), i, i, i, i, i, vp, vp, ctypes.c_longlong, i,
+    L.lsa_gemm_sk.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(EpiArgs), i, i, i, i, i, i, vp, vp, ctypes.c_longlong, i,
                               vp]
     for name in ("lsa_gemv", "lsa_gemv_coop", "lsa_gemv_fp8", "lsa_dequant_fp8_packed", "lsa_gemv_coop_fp8", "lsa_gemm",
                  "lsa_gemm_sk", "lsa_attn_decode", "lsa_attn_prefill", "lsa_embed", "lsa_rmsnorm", "lsa_layernorm",
-                 "lsa_argmax_finalize", "lsa_pos_advance", "lsa_epilogue_apply", "lsa_version"):
+                 "lsa_argmax_finalize", "lsa_pos_advance", "lsa_version"):
         getattr(L, name).restype = ctypes.c_int
     _lib = L
     return L
@@ -280,9 +279,16 @@ def gemm_slab_floats(M: int, N: int, sk: int) -> int:
 
 
 def gemm(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep: EpiArgs,
-         tn: int = 2, sk: int = 0, ws: Optional["CoopWorkspace"] = None) -> None:
-    """Prefill projection (any M). N must be a multiple of 64*tn, K of 64. ``sk`` = split-K
-    factor (0 = :func:`gemm_split`; > 1 needs a workspace: ``ws`` or the per-stream default)."""
+         tn: int = 2, sk: int = 0, ws: Optional["CoopWorkspace"] = None,
+         sk_ws: Optional["SkWorkspace"] = None, legacy: bool = False) -> None:
+    """Projection GEMM for > 128 rows (any M). Shapes with N % 128 == 0 (every Llama / GPT-2
+    projection) run the stream-K LDS-DMA kernel (:func:`gemm_sk`, workspace ``sk_ws``); other
+    shapes (or ``legacy=True``) the 128-row-tile kernel of gemm.hip, N a multiple of 64*tn,
+    ``sk`` its split-K factor (0 = :func:`gemm_split`; > 1 uses ``ws``)."""
+    if not legacy and N % 128 == 0 and K % 64 == 0 and epi != EPI_ARGMAX and a.stride(0) % 8 == 0 \
+            and a.data_ptr() % 16 == 0:
+        gemm_sk(a, wp, M, N, K, epi, ep, ws=sk_ws)
+        return
     _req(_is_bf16_cuda(a, wp), "gemm: bf16 cuda tensors required")
     _req(wp.numel() == N * K and K % 64 == 0, "gemm: packed weight shape")
     _req(a.dim() == 2 and a.shape[0] >= M and a.shape[1] >= K and a.stride(1) == 1, "gemm: A shape")
@@ -338,24 +344,36 @@ N_CU = 256
 
 
 def gemm_sk_plan(M: int, N: int, K: int) -> tuple:
-    """(bn, grid, dp) for ``gemm_sk``: 256 x 256 tiles where the grid stays filled, 256 x 128
-    tiles when a 256-column tiling leaves each tile split over many workgroups (few, long
-    tiles: o/down projections of a 512-row decode batch). Grid = one workgroup per CU (the
-    kernel holds 136 KiB of LDS); stream-K spreads the leftover tiles' K loops over it."""
+    """(bn, grid, dp, split) for ``gemm_sk``. Grid = one workgroup per CU (the kernel holds
+    ~136-144 KiB of LDS). Whole tiles go out in data-parallel rounds; the remainder either as
+    equal K splits (concurrent workgroups stream the same K offsets: L2 reuse) or by stream-K.
+    Costs per 64-deep K step measured on MI355X (scripts/bench_gemm_sk.py): ~1.5 us for a
+    256x256 tile, ~1.1 us for 256x128; stream-K's staggered K offsets lose ~2x of that to L2
+    misses; every extra partial costs one 256 x bn fp32 slab read (~100 GB/s per workgroup)."""
     mt = -(-M // SK_BM)
     nkt = K // 64
-    bn = 256 if N % 256 == 0 else 128
-    if bn == 256 and N % 128 == 0:
-        tiles = mt * (N // 256)
-        if tiles < N_CU and tiles * nkt < 16 * N_CU:  # > 4 contributors per 256-col tile
-            bn = 128
-    tiles = mt * (N // bn)
-    grid = min(N_CU, tiles * nkt)
-    return bn, grid, 1
+    best = None
+    for bn, c_it in ((256, 1.5), (128, 1.1)):
+        if N % bn:
+            continue
+        tiles = mt * (N // bn)
+        rounds, rem = divmod(tiles, N_CU)
+        slab_us = SK_BM * bn * 4 / 100e3
+        cands = [(rounds * nkt * c_it if rem == 0 else float("inf"), (bn, N_CU, 1, 0))]
+        if rem:
+            for sp in range(1, min(8, nkt, N_CU // rem) + 1):
+                t = (rounds * nkt + -(-nkt // sp)) * c_it + (sp - 1) * slab_us
+                cands.append((t, (bn, N_CU, 1, sp)))
+            per = rem * nkt / N_CU
+            cands.append(((rounds * nkt + per) * c_it + per * c_it + 2 * slab_us, (bn, N_CU, 1, 0)))
+        for c in cands:
+            if best is None or c[0] < best[0]:
+                best = c
+    return best[1]
 
 
 def gemm_sk(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep: EpiArgs,
-            bn: int = 0, grid: int = 0, dp: int = 1, group_m: int = 8, nb: int = 0,
+            bn: int = 0, grid: int = 0, dp: int = 1, group_m: int = 8, nb: int = 0, split: int = -1,
             ws: Optional[SkWorkspace] = None) -> None:
     """Projection GEMM for any M (gemm_sk.hip): 256 x ``bn`` tiles, LDS-DMA staged, data-parallel
     rounds + stream-K, fused epilogue. ``wp`` = pack_b(W[N, K]); N % bn == 0, K % 64 == 0."""
@@ -366,31 +384,21 @@ def gemm_sk(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int,
     _req(a.data_ptr() % 16 == 0, "gemm_sk: A must be 16-byte aligned")
     _check_epi(epi, ep, N)
     _req(epi in (EPI_STORE, EPI_RESID, EPI_SWIGLU, EPI_QKV), f"gemm_sk: epilogue {epi} not supported")
-    pb, pg, pd = gemm_sk_plan(M, N, K)
-    bn = bn or pb
+    pb, pg, pd, ps = gemm_sk_plan(M, N, K)
+    if not bn:
+        bn, grid, split = pb, grid or pg, ps if split < 0 else split
     grid = grid or pg
+    if split < 0:
+        split = 0
     _req(bn in (128, 256) and N % bn == 0, f"gemm_sk: N={N} not a multiple of bn={bn}")
     _req(1 <= grid <= 1024, "gemm_sk: grid")
     if ws is None:
         ws = default_sk_workspace(a.device)
     _req(ws.slab.numel() >= 2 * grid * SK_BM * bn and ws.counters.numel() >= 2 * grid,
          f"gemm_sk: workspace too small for grid={grid} bn={bn}")
-    rc = lib().lsa_gemm_sk(_p(a), a.stride(0), _p(wp), M, N, K, epi, ctypes.byref(ep), bn, nb, grid, dp, group_m,
+    rc = lib().lsa_gemm_sk(_p(a), a.stride(0), _p(wp), M, N, K, epi, ctypes.byref(ep), bn, nb, grid, dp, split, group_m,
                            _p(ws.slab), _p(ws.counters), ws.slab.numel(), ws.counters.numel(), _stream())
     _check(rc, "lsa_gemm_sk")
-
-
-def epilogue_apply(c: torch.Tensor, M: int, N: int, epi: int, ep: EpiArgs) -> None:
-    """The fused projection epilogue as one pass over a finished bf16 GEMM output ``c``
-    [>= M, >= N] in packed column order (epilogue_apply.hip): RoPE + KV-cache append (QKV),
-    SwiGLU, residual add or store - the tail of a library-GEMM projection."""
-    _req(epi in (EPI_STORE, EPI_RESID, EPI_SWIGLU, EPI_QKV), f"epilogue_apply: epilogue {epi} not supported")
-    _req(_is_bf16_cuda(c) and c.dim() == 2 and c.stride(1) == 1, "epilogue_apply: bf16 cuda row-major C")
-    _req(c.shape[0] >= M >= 1 and c.shape[1] >= N and N % (32 if epi == EPI_SWIGLU else 16) == 0,
-         f"epilogue_apply: C {tuple(c.shape)} vs M={M} N={N}")
-    _req(c.stride(0) % 8 == 0 and c.data_ptr() % 16 == 0, "epilogue_apply: C rows must be 16-byte aligned")
-    _check_epi(epi, ep, N)
-    _check(lib().lsa_epilogue_apply(_p(c), c.stride(0), M, N, epi, ctypes.byref(ep), _stream()), "lsa_epilogue_apply")
 
 
 # ------------------------------------------------------------------------------ attention

@@ -15,8 +15,13 @@ Same constructor and methods as the reference - ``Communicator(src_addr, dst_add
   tensor in it is replaced by a (shape, dtype) placeholder and its bytes go device-to-device
   with ``torch.distributed`` send/recv to the neighbouring rank - RCCL over xGMI on MI355X
   (gloo on CPU). Ranks default to the ring of a torchrun job in stage order (receive from
-  rank-1, send to rank+1); ``rccl_ranks=(src_rank, dst_rank)`` overrides. Received tensors
-  land on ``device``.
+  rank-1, send to rank+1); ``rccl_ranks=(src_rank, dst_rank)`` overrides, and
+  :meth:`Communicator.change_ranks` re-points a live communicator (hot re-configuration).
+  Each DIRECTED edge has its own process group (own RCCL communicator and stream), created
+  collectively once per job by :func:`init_edge_groups`: a send queued ahead of a receive on
+  one shared communicator can wait forever for a peer whose stream holds the mirror image
+  (the cycle :class:`..pipeline.DistP2P` documents), and with several messages in flight both
+  ring directions are busy at once. Receives give up after ``recv_timeout_s`` with an error.
 
 ``receive_data(no_block=True)`` raises :class:`Again` when nothing is queued, like
 ``zmq.Again``; ``timeout_ms`` adds a bounded blocking wait (the reference only offers busy
@@ -52,6 +57,32 @@ def reset_local_transport() -> None:
 
 
 _TENSOR_KEY = "__rccl_tensor__"
+_EDGE_GROUPS: dict = {}
+
+
+def init_edge_groups(ranks=None) -> dict:
+    """Create one process group per ORDERED pair (a, b), a != b, of ``ranks`` (default: every
+    rank of the job). Collective: every rank of the default group must call it, in the same
+    order, before rccl-backend Communicators are built (start_node.py does right after
+    ``init_process_group``). Groups are cheap until first used (RCCL communicators are created
+    lazily), so all pairs are registered and any later ring - a re-plan, a failover over the
+    survivors - finds its edges."""
+    import torch.distributed as dist
+    n = dist.get_world_size()
+    ranks = list(range(n)) if ranks is None else list(ranks)
+    for a in ranks:
+        for b in ranks:
+            if a != b and (a, b) not in _EDGE_GROUPS:
+                _EDGE_GROUPS[(a, b)] = dist.new_group([a, b])
+    return _EDGE_GROUPS
+
+
+def edge_group(src: int, dst: int):
+    g = _EDGE_GROUPS.get((src, dst))
+    if g is None:
+        raise RuntimeError(f"rccl backend: no process group for edge {src} -> {dst}; call "
+                           "communicator.init_edge_groups() on every rank after init_process_group")
+    return g
 
 
 def _extract_tensors(obj, out: list):
@@ -82,8 +113,9 @@ def _restore_tensors(obj, fetch):
 
 class Communicator:
     def __init__(self, src_addr: str, dst_addr: str, backend: str = "tcp", device=None,
-                 rccl_ranks: Optional[tuple] = None):
+                 rccl_ranks: Optional[tuple] = None, recv_timeout_s: float = 300.0):
         self.backend = backend
+        self.recv_timeout_s = recv_timeout_s
         self.src_addr = src_addr
         self.dst_addr = dst_addr
         self.sent_messages = 0
@@ -96,7 +128,7 @@ class Communicator:
             if not dist.is_initialized():
                 raise RuntimeError("rccl backend: torch.distributed is not initialised (launch with torchrun)")
             r, w = dist.get_rank(), dist.get_world_size()
-            self.src_rank, self.dst_rank = rccl_ranks if rccl_ranks is not None else ((r - 1) % w, (r + 1) % w)
+            self.change_ranks(*(rccl_ranks if rccl_ranks is not None else ((r - 1) % w, (r + 1) % w)))
         if backend in ("tcp", "rccl"):
             self.recv_socket = PullSocket(src_addr)
             self.actual_src_addr = self.recv_socket.last_endpoint
@@ -120,6 +152,15 @@ class Communicator:
             self.actual_src_addr = new_src_addr
         self.src_addr = new_src_addr
         return self.src_addr
+
+    def change_ranks(self, src_rank: int, dst_rank: int) -> None:
+        """Point the tensor side channel at new neighbours (rccl backend); the directed-edge
+        groups come from :func:`init_edge_groups`."""
+        import torch.distributed as dist
+        me = dist.get_rank()
+        self.src_rank, self.dst_rank = int(src_rank), int(dst_rank)
+        self._send_group = edge_group(me, self.dst_rank) if self.dst_rank != me else None
+        self._recv_group = edge_group(self.src_rank, me) if self.src_rank != me else None
 
     def change_dst_addr(self, new_dst_addr: str) -> str:
         if self.backend in ("tcp", "rccl") and new_dst_addr != self.dst_addr:
@@ -175,7 +216,7 @@ class Communicator:
             t = t.contiguous()
             if self.device is not None and t.device != self.device and str(self.device) != "cpu":
                 t = t.to(self.device)
-            self._pending_sends.append((dist.isend(t, self.dst_rank), t))
+            self._pending_sends.append((dist.isend(t, self.dst_rank, group=self._send_group), t))
         # bound the outstanding sends (their tensors must stay alive until complete)
         while len(self._pending_sends) > 16:
             w, _ = self._pending_sends.pop(0)
@@ -185,8 +226,16 @@ class Communicator:
         import torch
         import torch.distributed as dist
         dev = self.device if self.device is not None else "cpu"
+        import datetime
         t = torch.empty(ph["shape"], dtype=getattr(torch, ph["dtype"]), device=dev)
-        dist.recv(t, self.src_rank)
+        work = dist.irecv(t, self.src_rank, group=self._recv_group)
+        try:
+            ok = work.wait(timeout=datetime.timedelta(seconds=self.recv_timeout_s))
+        except RuntimeError as e:  # backend-specific timeout error
+            raise RuntimeError(f"rccl recv from rank {self.src_rank} failed or timed out "
+                               f"({self.recv_timeout_s:.0f} s): {e}") from e
+        if ok is False:
+            raise RuntimeError(f"rccl recv from rank {self.src_rank} timed out ({self.recv_timeout_s:.0f} s)")
         return t
 
     def flush(self, timeout_ms: int = 5000) -> bool:
@@ -196,7 +245,11 @@ class Communicator:
         return self.send_socket.flush(timeout_ms) if self.backend in ("tcp", "rccl") else True
 
     def inject_faults(self, drop_every: int = 0, delay_ms: int = 0) -> None:
-        """Test hook: drop every Nth outgoing message / delay each one (tcp backend)."""
+        """Test hook: drop every Nth outgoing message / delay each one (tcp backend; rccl:
+        delays only - a dropped envelope would leave its tensors unmatched on the side channel
+        and desynchronise every later message instead of simulating one lost message)."""
+        if self.backend == "rccl" and drop_every > 0:
+            raise ValueError("inject_faults: message drops are not supported on the rccl backend")
         if self.backend in ("tcp", "rccl"):
             self.send_socket.inject_faults(drop_every, delay_ms)
 
@@ -209,4 +262,4 @@ class Communicator:
             self.recv_socket.close()
 
 
-__all__ = ["Communicator", "Again", "reset_local_transport"]
+__all__ = ["Communicator", "Again", "reset_local_transport", "init_edge_groups", "edge_group"]

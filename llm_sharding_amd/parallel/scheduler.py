@@ -167,6 +167,21 @@ def kv_slots_for_memory(cfg: LlamaConfig, n_layers: int, max_seq: int, mem_bytes
     return int(min(max_per_microbatch, free // (per_slot * microbatches)))
 
 
+def scratch_bytes(cfg: LlamaConfig, rows: int, sets: int = 1) -> float:
+    """Device bytes a stage engine allocates besides weights and KV cache, per ``sets``
+    concurrently replayed scratch sets of ``rows`` rows (StageEngine._alloc_runtime /
+    decode_scratch): activations, attention split partials, the coop-GEMV and gemm_sk
+    workspaces."""
+    H, I, nh, hd = cfg.hidden_size, cfg.intermediate_size, cfg.num_attention_heads, cfg.head_dim
+    R = max(rows, 128)
+    act = R * (2 * H + 2 * cfg.q_size + I) * 2
+    ws_rows = max(128 * 16, 4 * R)
+    attn = ws_rows * nh * (hd + 1) * 4
+    coop = (1 << 24) * 4
+    sk = 2 * 256 * 256 * 256 * 4 if R > 128 else 0
+    return float(sets * (act + attn + coop + sk))
+
+
 def even_split(n_layers: int, n_stages: int) -> list:
     base, extra = divmod(n_layers, n_stages)
     out, s = [], 0

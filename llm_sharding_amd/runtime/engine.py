@@ -151,12 +151,6 @@ class LayerWeights:
     o_b: Optional[torch.Tensor] = None
     gate_up_b: Optional[torch.Tensor] = None
     down_b: Optional[torch.Tensor] = None
-    # row-major bf16 images of the packed projections (same fused row order, norms folded) for
-    # the library-GEMM path of >128-row forwards (StageEngine.library_gemm)
-    qkv_rm: Optional[torch.Tensor] = None
-    o_rm: Optional[torch.Tensor] = None
-    gate_up_rm: Optional[torch.Tensor] = None
-    down_rm: Optional[torch.Tensor] = None
 
 
 def _is_gpu(device: torch.device) -> bool:
@@ -189,8 +183,7 @@ class StageEngine:
                  dtype=torch.bfloat16, *, has_embed: bool = False, has_head: bool = False,
                  source: Optional[WeightSource] = None, max_slots: int = 1, max_seq: int = 2048,
                  max_prefill_rows: int = 2048, causal: bool = True, load: bool = True,
-                 verbose: bool = False, head_cols: Optional[tuple] = None, weight_dtype: str = "bf16",
-                 library_gemm: Optional[bool] = None):
+                 verbose: bool = False, head_cols: Optional[tuple] = None, weight_dtype: str = "bf16"):
         if not (0 <= start < end <= cfg.num_hidden_layers):
             raise ValueError(f"[ERROR] invalid layer range [{start}, {end})")
         self.cfg = cfg
@@ -229,8 +222,6 @@ class StageEngine:
         self.seq_len = [0] * self.max_slots  # host-side KV length per slot
         self._graphs: dict = {}
         self._scratch: dict = {}  # decode scratch sets of concurrent graphs (decode_scratch)
-        self.buf_qkv = self.buf_gu = None
-        self.library_gemm = self._want_library_gemm(library_gemm)
         if self.gpu:
             from ..ops import hip as _hip  # noqa: F401  (fail loudly if the .so is missing)
             _hip.lib()
@@ -241,29 +232,6 @@ class StageEngine:
     def _log(self, msg: str) -> None:
         if self.verbose:
             print(msg, flush=True)
-
-    def _want_library_gemm(self, req: Optional[bool]) -> bool:
-        """Row-major bf16 copies of the projections for the vendor GEMM (torch.matmul ->
-        hipBLASLt) on forwards above DECODE_MAX_ROWS rows - prefill and big decode batches, where
-        it runs ~2x gemm.hip (profiles/r1_gemm_vs_hipblaslt.jsonl) - with the fused RoPE/KV-append
-        and SwiGLU epilogues as one pass after it (epilogue_apply.hip). ``None`` = auto (env
-        LSA_LIBRARY_GEMM=0/1 overrides): bf16 Llama-family GPU stages whose doubled projection
-        weights stay under 40% of the device memory (Llama-2-7B: +13 GB; all 80 layers of a 70B
-        on one GPU: no)."""
-        ok = self.gpu and not self.fp8 and not self.cfg.is_gpt2
-        env = os.environ.get("LSA_LIBRARY_GEMM")
-        if req is None and env in ("0", "1"):
-            req = env == "1" and ok
-        if req is not None:
-            if req and not ok:
-                raise ValueError("library_gemm needs bf16 weights of a Llama-family model on a GPU")
-            return bool(req)
-        if not ok:
-            return False
-        c = self.cfg
-        per_layer = 2 * c.hidden_size * (c.qkv_size + c.q_size + c.mlp_in_size + c.intermediate_size)
-        total = torch.cuda.get_device_properties(self.device).total_memory
-        return 2 * per_layer * self.n_layers <= 0.4 * total
 
     def load(self) -> None:
         cfg, dev, dt = self.cfg, self.device, self.dtype
@@ -333,9 +301,7 @@ class StageEngine:
             ln_in, ln_post = lw["input_layernorm.weight"], lw["post_attention_layernorm.weight"]
             mats = (packing.fold_norm(qkv, ln_in), lw["self_attn.o_proj.weight"], packing.fold_norm(gu, ln_post),
                     lw["mlp.down_proj.weight"])
-            rm = tuple(m.contiguous() for m in mats) if self.library_gemm else (None,) * 4
-            return LayerWeights(*(packing.pack_b(m) for m in mats), ln_in.contiguous(), ln_post.contiguous(),
-                                qkv_rm=rm[0], o_rm=rm[1], gate_up_rm=rm[2], down_rm=rm[3])
+            return LayerWeights(*(packing.pack_b(m) for m in mats), ln_in.contiguous(), ln_post.contiguous())
         return LayerWeights(None, None, None, None, lw["input_layernorm.weight"],
                             lw["post_attention_layernorm.weight"], raw=lw)
 
@@ -375,9 +341,6 @@ class StageEngine:
             self.buf_q = torch.zeros((R, cfg.q_size), dtype=bf, device=dev)
             self.buf_attn = torch.zeros((R, cfg.q_size), dtype=bf, device=dev)
             self.buf_act = torch.zeros((R, I), dtype=bf, device=dev)
-            if self.library_gemm:  # library-GEMM outputs ahead of their epilogue pass
-                self.buf_qkv = torch.zeros((R, cfg.qkv_size), dtype=bf, device=dev)
-                self.buf_gu = torch.zeros((R, cfg.mlp_in_size), dtype=bf, device=dev)
             self.max_decode_nsplit = int(min(16, max(1, ceil_div(self.max_seq, 256))))
             ws_rows = max(self.DECODE_MAX_ROWS * self.max_decode_nsplit, R * 4)
             self.part_o = torch.zeros(ws_rows * cfg.num_attention_heads * hd, dtype=torch.float32, device=dev)
@@ -397,13 +360,15 @@ class StageEngine:
             floats, groups = packing.coop_workspace_need(shapes, self.DECODE_MAX_ROWS, even_n=even)
             # the prefill GEMM's split-K slabs (small-M grids only) share it: <= 64 MB
             self.coop_ws = hip.CoopWorkspace(dev, slab_floats=max(floats, 1 << 24), groups=max(groups, 4096))
+            # stream-K / split-K partial slabs + tickets of the > 128-row GEMM (gemm_sk.hip)
+            self.sk_ws = hip.SkWorkspace(dev) if R > self.DECODE_MAX_ROWS else None
             self.w_scratch = None
             if self.fp8:  # one projection's bf16 weights, for the >64-row paths
                 self.w_scratch = torch.empty(max(n * k for n, k in shapes), dtype=torch.bfloat16, device=dev)
 
     # buffers a forward pass writes besides the KV cache: one set per concurrently running graph
-    SCRATCH_ATTRS = ("buf_h", "buf_xn", "buf_q", "buf_attn", "buf_act", "buf_qkv", "buf_gu", "part_o", "part_lse", "attn_cnt",
-                     "coop_ws", "w_scratch", "keys", "tokens", "ws_rows")
+    SCRATCH_ATTRS = ("buf_h", "buf_xn", "buf_q", "buf_attn", "buf_act", "part_o", "part_lse", "attn_cnt",
+                     "coop_ws", "sk_ws", "w_scratch", "keys", "tokens", "ws_rows")
 
     def decode_scratch(self, k: int, rows: Optional[int] = None) -> dict:
         """Scratch set ``k`` for forward passes that run CONCURRENTLY on different streams (a
@@ -427,13 +392,12 @@ class StageEngine:
                 "buf_q": torch.zeros((R, cfg.q_size), dtype=bf, device=dev),
                 "buf_attn": torch.zeros((R, cfg.q_size), dtype=bf, device=dev),
                 "buf_act": torch.zeros((R, I), dtype=bf, device=dev),
-                "buf_qkv": torch.zeros((R, cfg.qkv_size), dtype=bf, device=dev) if self.library_gemm else None,
-                "buf_gu": torch.zeros((R, cfg.mlp_in_size), dtype=bf, device=dev) if self.library_gemm else None,
                 "part_o": torch.zeros(ws_rows * nh * hd, dtype=torch.float32, device=dev),
                 "part_lse": torch.zeros(ws_rows * nh, dtype=torch.float32, device=dev),
                 "attn_cnt": torch.zeros(ws_rows * cfg.num_key_value_heads, dtype=torch.int32, device=dev),
                 "coop_ws": hip.CoopWorkspace(dev, slab_floats=self.coop_ws.slab.numel(),
                                              groups=self.coop_ws.counters.numel()),
+                "sk_ws": hip.SkWorkspace(dev) if R > self.DECODE_MAX_ROWS else None,
                 "w_scratch": None if self.w_scratch is None else torch.empty_like(self.w_scratch),
                 "keys": torch.zeros(R, dtype=torch.int64, device=dev),
                 "tokens": torch.zeros(R, dtype=torch.int32, device=dev),
@@ -657,9 +621,8 @@ class StageEngine:
                 hip.gemv(x, wbf(w, s, N, K), rows, N, K, epi, ep, norm=norm, eps=eps, ws=ws)
 
         def pre(x, w, s, N, K, epi, ep):
-            hip.gemm(x, wbf(w, s, N, K), rows, N, K, epi, ep, ws=ws)
+            hip.gemm(x, wbf(w, s, N, K), rows, N, K, epi, ep, ws=ws, sk_ws=self.sk_ws)
 
-        lib = self.library_gemm and not decode
         for li, lw in enumerate(self.layers):
             kc, vc = self.k_cache[li], self.v_cache[li]
             ep_qkv = hip.make_epi(out=q, k_cache=kc, v_cache=vc, slot=slot, pos=pos, cos=self.cos, sin=self.sin,
@@ -668,12 +631,7 @@ class StageEngine:
                 dec(hbuf, lw.qkv, lw.qkv_s, cfg.qkv_size, H, hip.EPI_QKV, ep_qkv, norm=True)
             else:
                 hip.rmsnorm(hbuf, None, xn, rows, eps, H)
-                if lib:  # vendor GEMM, then RoPE + KV-cache append as one pass
-                    c = self.buf_qkv[:rows]
-                    torch.matmul(xn, lw.qkv_rm.t(), out=c)
-                    hip.epilogue_apply(c, rows, cfg.qkv_size, hip.EPI_QKV, ep_qkv)
-                else:
-                    pre(xn, lw.qkv, lw.qkv_s, cfg.qkv_size, H, hip.EPI_QKV, ep_qkv)
+                pre(xn, lw.qkv, lw.qkv_s, cfg.qkv_size, H, hip.EPI_QKV, ep_qkv)
             if tiles is not None:
                 hip.attn_prefill(q, kc, vc, tiles[1], nh, nkv, hd, attn_o, causal=kv_len is None, tiles_host=tiles[0])
             else:
@@ -685,13 +643,6 @@ class StageEngine:
                 dec(attn_o, lw.o, lw.o_s, H, cfg.q_size, hip.EPI_RESID, ep_o)
                 dec(hbuf, lw.gate_up, lw.gate_up_s, 2 * I, H, hip.EPI_SWIGLU, ep_gu, norm=True)
                 dec(act, lw.down, lw.down_s, H, I, hip.EPI_RESID, ep_o)
-            elif lib:  # the residual adds are the GEMMs' beta = 1
-                hbuf.addmm_(attn_o, lw.o_rm.t())
-                hip.rmsnorm(hbuf, None, xn, rows, eps, H)
-                c = self.buf_gu[:rows]
-                torch.matmul(xn, lw.gate_up_rm.t(), out=c)
-                hip.epilogue_apply(c, rows, 2 * I, hip.EPI_SWIGLU, ep_gu)
-                hbuf.addmm_(act, lw.down_rm.t())
             else:
                 pre(attn_o, lw.o, lw.o_s, H, cfg.q_size, hip.EPI_RESID, ep_o)
                 hip.rmsnorm(hbuf, None, xn, rows, eps, H)
@@ -719,7 +670,7 @@ class StageEngine:
             if decode:
                 hip.gemv(x, wb, rows, N, K, epi, ep, ws=ws)
             else:
-                hip.gemm(x, wb, rows, N, K, epi, ep, ws=ws)
+                hip.gemm(x, wb, rows, N, K, epi, ep, ws=ws, sk_ws=self.sk_ws)
 
         for li, lw in enumerate(self.layers):
             kc, vc = self.k_cache[li], self.v_cache[li]
@@ -859,7 +810,7 @@ class DecodeGraph:
         from ..ops import hip
         if not eng.gpu:
             raise RuntimeError("DecodeGraph needs a GPU stage")
-        # above DECODE_MAX_ROWS the step runs the >128-row projections (library GEMM + epilogue
+        # above DECODE_MAX_ROWS the step runs the >128-row projections (gemm_sk.hip stream-K GEMM
         # pass, or gemm.hip) on buffers sized by max_prefill_rows; argmax_finalize takes <= 1024
         cap = min(1024, max(eng.DECODE_MAX_ROWS, eng.max_prefill_rows))
         if rows > cap:

@@ -398,6 +398,13 @@ class NodeController:
         else:
             w.communicator.change_src_addr(new["src_addr"])
             w.communicator.change_dst_addr(new["dst_addr"])
+            if w.communicator.backend == "rccl":
+                # the tensor side channel follows the new ring too: explicit (src, dst) ranks
+                # from the config, else the default torchrun ring
+                import torch.distributed as dist
+                r, n = dist.get_rank(), dist.get_world_size()
+                src, dst = new["rccl_ranks"] if new.get("rccl_ranks") is not None else ((r - 1) % n, (r + 1) % n)
+                w.communicator.change_ranks(src, dst)
             self._set_first_node_addr(new)  # Q8: no-op for non-ingress nodes
             if (new["shards_start"], new["shards_end"]) != (w.start, w.end):
                 w.load_shards(new["shards_start"], new["shards_end"])

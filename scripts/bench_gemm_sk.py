@@ -3,7 +3,7 @@
 epilogue) against torch.matmul (hipBLASLt, plain GEMM) on the same random data, weights rotated
 over > 600 MB of copies so they stream from HBM as in a decode step.
 
-usage: bench_gemm_sk.py [rows,rows,...] [--configs bn:grid:dp[:nb],...] [--model llama2-7b]
+usage: bench_gemm_sk.py [rows,rows,...] [--configs bn:grid:dp[:nb[:split]],...] [--model llama2-7b]
 Prints one JSON line per (shape, M) with every config's time and the library's."""
 import argparse
 import json
@@ -54,17 +54,17 @@ def main():
             ep = hip.make_epi(out=out, ldo=N)
             fl = 2.0 * M * N * K
             rec = {"shape": name, "M": M, "N": N, "K": K, "plan": list(hip.gemm_sk_plan(M, N, K))}
-            todo = [(0, 0, 1, 0)] + [c + (0,) * (4 - len(c)) for c in cfgs]
-            for (bn, grid, dp, nb) in todo:
+            todo = [(0, 0, 1, 0, -1)] + [c + (0, -1)[len(c) - 3:] if len(c) < 5 else c for c in cfgs]
+            for (bn, grid, dp, nb, split) in todo:
                 if bn and N % bn:
                     continue
-                hip.gemm_sk(x, wps[0], M, N, K, hip.EPI_STORE, ep, bn=bn, grid=grid, dp=dp, nb=nb, ws=ws)
+                hip.gemm_sk(x, wps[0], M, N, K, hip.EPI_STORE, ep, bn=bn, grid=grid, dp=dp, nb=nb, split=split, ws=ws)
                 torch.matmul(x, w_rm[0].t(), out=ref)
                 torch.cuda.synchronize()
                 err = ((out.float() - ref.float()).norm() / ref.float().norm()).item()
                 t = timeit(lambda i: hip.gemm_sk(x, wps[i % nbuf], M, N, K, hip.EPI_STORE, ep, bn=bn, grid=grid, dp=dp,
-                                                 nb=nb, ws=ws), iters=args.iters)
-                key = "sk" if (bn, grid, dp, nb) == (0, 0, 1, 0) else f"sk_{bn}_{grid}_{dp}_{nb}"
+                                                 nb=nb, split=split, ws=ws), iters=args.iters)
+                key = "sk" if (bn, grid, dp, nb, split) == (0, 0, 1, 0, -1) else f"sk_{bn}_{grid}_{dp}_{nb}_{split}"
                 rec[key + "_us"] = round(t, 2)
                 rec[key + "_tflops"] = round(fl / t / 1e6, 1)
                 rec[key + "_relerr"] = float(f"{err:.2e}")

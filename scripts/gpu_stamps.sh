@@ -1,0 +1,7 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+for cfg in "512 12288 4096 256 256 1 2" "512 12288 4096 256 256 1 1" "512 4096 4096 128 256 1 4" "512 22016 4096 256 256 1 1" "16384 12288 4096 256 256 1 0"; do
+  timeout -k 10 60 python -u scripts/gemm_stamps.py $cfg 5 >> gpurun_out/stamps.log 2>&1 || exit 1
+done
+echo rc=$?

@@ -120,17 +120,19 @@ def main():
         ctrl = dist.new_group(backend="gloo")
     cfg, source = rc.model_and_source()
     M = rc.microbatches or max(2, world)
-    if rc.batch == 0:  # size the KV cache from this GPU's HBM (bottleneck stage of a weights-only plan)
-        from llm_sharding_amd.parallel.scheduler import kv_slots_for_memory
-        wplan = plan_stages(cfg, world, head_split=world > 1)
+    if rc.batch == 0:  # size the KV cache from this GPU's HBM
+        from llm_sharding_amd.parallel.scheduler import kv_slots_for_memory, scratch_bytes
         mem = torch.cuda.get_device_properties(dev).total_memory if gpu else 64e9
-        # bf16 Llama stages keep a row-major copy of the projections for the library GEMM
-        # (StageEngine.library_gemm, same 40%-of-HBM rule): count it as weights
-        def wbytes(s):
-            lib = gpu and not cfg.is_gpt2 and 2 * s.weight_bytes <= 0.4 * mem
-            return s.weight_bytes * (2 if lib else 1)
-        rc.batch = min(kv_slots_for_memory(cfg, s.n_layers, rc.max_seq, mem, wbytes(s), microbatches=M)
-                       for s in wplan.stages)
+        # activations / workspaces of every concurrently replayed scratch set, plus 8 GB slack
+        reserve = 8e9 + scratch_bytes(cfg, rc.prefill_budget, sets=max(1, rc.streams))
+        plan = plan_stages(cfg, world)
+        for _ in range(8):  # the KV budget moves layer boundaries: iterate to a fixed point
+            rc.batch = min(kv_slots_for_memory(cfg, s.n_layers, rc.max_seq, mem, s.weight_bytes, reserve_bytes=reserve,
+                                               microbatches=M) for s in plan.stages)
+            nxt = plan_stages(cfg, world, kv_tokens=rc.max_seq * rc.batch * M)
+            if nxt.ranges() == plan.ranges():
+                break
+            plan = nxt
         log.info(f"KV cache sized from {mem / 1e9:.0f} GB HBM: {rc.batch} slots x {M} micro-batches")
     plan = plan_stages(cfg, world, kv_tokens=rc.max_seq * rc.batch * M)
     st = plan.stages[rank]

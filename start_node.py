@@ -41,6 +41,8 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device(device))
         else:
             dist.init_process_group("gloo")
+        from llm_sharding_amd.parallel.communicator import init_edge_groups
+        init_edge_groups()  # collective: one RCCL communicator per directed stage edge
         port += rank
     ctrl = NodeController(a.shards, device=device, dtype=getattr(torch, a.dtype), listen_port=port,
                           backend=a.backend, worker_kwargs={"noncausal_prefill": a.noncausal_prefill})

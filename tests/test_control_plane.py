@@ -267,6 +267,8 @@ def _rccl_chain_worker(rank, port, ports, shards, n_new, q):
     from llm_sharding_amd.utils.node_worker import NodeWorker
     torch.set_num_threads(1)
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=2)
+    from llm_sharding_amd.parallel.communicator import init_edge_groups
+    init_edge_groups()
     try:
         w = NodeWorker(f"tcp://*:{ports[rank]}", f"tcp://127.0.0.1:{ports[1 - rank]}", rank == 0, shards,
                        device="cpu", dtype=torch.float32, backend="rccl", verbose=False)

@@ -31,8 +31,10 @@ def ws():
     return hip().SkWorkspace(DEV, grid=1024, bn=256)
 
 
-# (bn, grid, dp): planner default, whole-tile rounds, pure stream-K, odd grids (bijective XCD remap)
-CFGS = [(0, 0, 1), (256, 256, 1), (128, 256, 1), (256, 37, 0), (128, 13, 1), (256, 1000, 0)]
+# (bn, grid, dp, split): planner default, whole-tile rounds + stream-K, pure stream-K, odd grids
+# (bijective XCD remap), equal K splits of the remainder (2-, 3- and 8-way), 128-wide 2-buffer ring
+CFGS = [(0, 0, 1, -1), (256, 256, 1, 0), (128, 256, 1, 0), (256, 37, 0, 0), (128, 13, 1, 0), (256, 1000, 0, 0),
+        (256, 256, 1, 2), (128, 256, 0, 3), (256, 512, 1, 8), (128, 96, 1, 1)]
 
 
 @pytest.mark.parametrize("M", [1, 129, 256, 300, 512, 777])
@@ -44,16 +46,21 @@ def test_gemm_sk_store_resid(M, N, K, ws):
     wp = packing.pack_b(w)
     ref = a.float() @ w.float().T
     r = _rnd(M, N)
-    for (bn, grid, dp) in CFGS:
+    for (bn, grid, dp, split) in CFGS:
         if bn and N % bn:
             continue
+        nb = 2 if (bn, grid) == (128, 96) else 0
+        tiles = -(-M // 256) * (N // (bn or 256))
+        if split > 0 and tiles * split > grid:
+            continue
         out = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
-        h.gemm_sk(a, wp, M, N, K, h.EPI_STORE, h.make_epi(out=out, ldo=N), bn=bn, grid=grid, dp=dp, ws=ws)
-        assert rel_err(out, ref) < 8e-3, (bn, grid, dp)
+        h.gemm_sk(a, wp, M, N, K, h.EPI_STORE, h.make_epi(out=out, ldo=N), bn=bn, grid=grid, dp=dp, split=split,
+                  nb=nb, ws=ws)
+        assert rel_err(out, ref) < 8e-3, (bn, grid, dp, split)
         o2 = r.clone()
         h.gemm_sk(a, wp, M, N, K, h.EPI_RESID, h.make_epi(out=o2, resid=o2, ldo=N, ldr=N), bn=bn, grid=grid, dp=dp,
-                  ws=ws)
-        assert rel_err(o2, r.float() + ref) < 8e-3, (bn, grid, dp)
+                  split=split, nb=nb, ws=ws)
+        assert rel_err(o2, r.float() + ref) < 8e-3, (bn, grid, dp, split)
     assert int(ws.counters.abs().sum()) == 0  # every split tile's ticket was reset
 
 
@@ -78,10 +85,14 @@ def test_gemm_sk_swiglu(M, ws):
     wg, wu = _rnd(I, H, scale=0.05), _rnd(I, H, scale=0.05)
     wp = packing.pack_b(packing.fuse_gate_up(wg, wu))
     ref = F.silu(x.float() @ wg.float().T) * (x.float() @ wu.float().T)
-    for (bn, grid, dp) in CFGS:
+    for (bn, grid, dp, split) in CFGS:
+        tiles = -(-M // 256) * (2 * I // (bn or 256))
+        if split > 0 and tiles * split > grid:
+            continue
         out = torch.zeros(M, I, dtype=torch.bfloat16, device=DEV)
-        h.gemm_sk(x, wp, M, 2 * I, H, h.EPI_SWIGLU, h.make_epi(out=out, ldo=I), bn=bn, grid=grid, dp=dp, ws=ws)
-        assert rel_err(out, ref) < 1e-2, (bn, grid, dp)
+        h.gemm_sk(x, wp, M, 2 * I, H, h.EPI_SWIGLU, h.make_epi(out=out, ldo=I), bn=bn, grid=grid, dp=dp, split=split,
+                  ws=ws)
+        assert rel_err(out, ref) < 1e-2, (bn, grid, dp, split)
 
 
 def _rope_ref(t, pos, cos, sin):
@@ -92,7 +103,7 @@ def _rope_ref(t, pos, cos, sin):
 
 
 @pytest.mark.parametrize("nh,nkv,hd", [(32, 32, 128), (8, 2, 64), (24, 8, 128)])
-@pytest.mark.parametrize("cfg", [(0, 0, 1), (128, 29, 0)])
+@pytest.mark.parametrize("cfg", [(0, 0, 1, -1), (128, 29, 0, 0), (256, 256, 1, 3)])
 def test_gemm_sk_qkv_rope_kv_append(nh, nkv, hd, cfg, ws):
     from llm_sharding_amd.config import tiny
     from llm_sharding_amd.models.rope import rope_table
@@ -110,10 +121,10 @@ def test_gemm_sk_qkv_rope_kv_append(nh, nkv, hd, cfg, ws):
     N = (nh + 2 * nkv) * hd
     ep = h.make_epi(out=q, k_cache=kc, v_cache=vc, slot=slot, pos=pos, cos=cos, sin=sin, ldo=nh * hd,
                     n_heads=nh, n_kv=nkv, head_dim=hd, t_max=T)
-    bn, grid, dp = cfg
+    bn, grid, dp, split = cfg
     if bn and N % bn:
         pytest.skip("N not a multiple of bn")
-    h.gemm_sk(x, wp, M, N, H, h.EPI_QKV, ep, bn=bn, grid=grid, dp=dp, ws=ws)
+    h.gemm_sk(x, wp, M, N, H, h.EPI_QKV, ep, bn=bn, grid=grid, dp=dp, split=split, ws=ws)
     xf, pl, sl = x.float(), pos.long(), slot.long()
     qr = _rope_ref((xf @ wq.float().T).view(M, nh, hd), pl, cos, sin).reshape(M, -1)
     kr = _rope_ref((xf @ wk.float().T).view(M, nkv, hd), pl, cos, sin)

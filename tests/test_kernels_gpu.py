@@ -170,29 +170,6 @@ def test_gemv_swiglu(M):
     assert rel_err(out, ref) < 1e-2
 
 
-def test_library_gemm_epilogues():
-    """torch.matmul (vendor GEMM) + epilogue_apply.hip: SwiGLU on the packed gate|up column
-    order, residual add and plain store, against fp32 references."""
-    h = hip()
-    M, I, H = 200, 1024, 512
-    x = _rnd(M, H)
-    wg, wu = _rnd(I, H, scale=0.05), _rnd(I, H, scale=0.05)
-    c = torch.matmul(x, packing.fuse_gate_up(wg, wu).t())
-    out = torch.zeros(M, I, dtype=torch.bfloat16, device=DEV)
-    h.epilogue_apply(c, M, 2 * I, h.EPI_SWIGLU, h.make_epi(out=out, ldo=I))
-    ref = F.silu(x.float() @ wg.float().T) * (x.float() @ wu.float().T)
-    assert rel_err(out, ref) < 1e-2
-    w = _rnd(H, I, scale=0.02)
-    c2 = torch.matmul(out, w.t())
-    r = _rnd(M, H)
-    o2 = r.clone()
-    h.epilogue_apply(c2, M, H, h.EPI_RESID, h.make_epi(out=o2, resid=o2, ldo=H, ldr=H))
-    assert rel_err(o2, r.float() + out.float() @ w.float().T) < 8e-3
-    o3 = torch.zeros(M, H, dtype=torch.bfloat16, device=DEV)
-    h.epilogue_apply(c2, M, H, h.EPI_STORE, h.make_epi(out=o3, ldo=H))
-    assert torch.equal(o3, c2)
-
-
 def _rope_ref(t, pos, cos, sin):
     half = t.shape[-1] // 2
     c, s = cos[pos][:, None, :], sin[pos][:, None, :]
@@ -200,14 +177,14 @@ def _rope_ref(t, pos, cos, sin):
     return torch.cat([t1 * c - t2 * s, t2 * c + t1 * s], dim=-1)
 
 
-@pytest.mark.parametrize("path", ["gemv", "coop", "gemm", "library"])
+@pytest.mark.parametrize("path", ["gemv", "coop", "gemm", "gemm_legacy"])
 @pytest.mark.parametrize("nh,nkv,hd", [(32, 32, 128), (8, 2, 64), (24, 8, 128)])
 def test_qkv_rope_kv_append(path, nh, nkv, hd):
     from llm_sharding_amd.config import tiny
     from llm_sharding_amd.models.rope import rope_table
     h = hip()
     H = 512
-    M = {"gemv": 5, "coop": 40, "gemm": 150, "library": 150}[path]
+    M = {"gemv": 5, "coop": 40, "gemm": 150, "gemm_legacy": 150}[path]
     slots, T = 3, 256
     wq, wk, wv = _rnd(nh * hd, H, scale=0.05), _rnd(nkv * hd, H, scale=0.05), _rnd(nkv * hd, H, scale=0.05)
     x = _rnd(M, H)
@@ -228,9 +205,8 @@ def test_qkv_rope_kv_append(path, nh, nkv, hd):
         h.gemv(x, wp, M, N, H, h.EPI_QKV, ep, coop=(1, 8, 4, 2))
     elif path == "gemm":
         h.gemm(x, wp, M, N, H, h.EPI_QKV, ep)
-    else:  # vendor GEMM on the row-major fused weights + the standalone epilogue pass
-        c = torch.matmul(x, packing.fuse_qkv(wq, wk, wv, nh, nkv, hd).t())
-        h.epilogue_apply(c, M, N, h.EPI_QKV, ep)
+    else:  # the 128-row-tile kernel of gemm.hip (shapes the stream-K kernel does not take)
+        h.gemm(x, wp, M, N, H, h.EPI_QKV, ep, legacy=True)
     xf = x.float()
     pl = pos.long()
     qr = _rope_ref((xf @ wq.float().T).view(M, nh, hd), pl, cos, sin).reshape(M, -1)
@@ -267,19 +243,20 @@ def test_gemv_argmax_with_rows(M):
     assert torch.all(keys == 0)  # finalize resets the keys
 
 
+@pytest.mark.parametrize("legacy", [False, True])
 @pytest.mark.parametrize("M", [17, 128, 333])
 @pytest.mark.parametrize("N,K", [(4096, 4096), (512, 11008), (192, 256)])
-def test_gemm_store_resid(M, N, K):
+def test_gemm_store_resid(M, N, K, legacy):
     h = hip()
     a = _rnd(M, K)
     w = _rnd(N, K, scale=0.02)
     out = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
-    h.gemm(a, packing.pack_b(w), M, N, K, h.EPI_STORE, h.make_epi(out=out, ldo=N))
+    h.gemm(a, packing.pack_b(w), M, N, K, h.EPI_STORE, h.make_epi(out=out, ldo=N), legacy=legacy)
     ref = a.float() @ w.float().T
     assert rel_err(out, ref) < 8e-3
     r = _rnd(M, N)
     o2 = r.clone()
-    h.gemm(a, packing.pack_b(w), M, N, K, h.EPI_RESID, h.make_epi(out=o2, resid=o2, ldo=N, ldr=N))
+    h.gemm(a, packing.pack_b(w), M, N, K, h.EPI_RESID, h.make_epi(out=o2, resid=o2, ldo=N, ldr=N), legacy=legacy)
     assert rel_err(o2, r.float() + ref) < 8e-3
 
 
