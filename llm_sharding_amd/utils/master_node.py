@@ -14,7 +14,14 @@ the master that calls ``ConfigSender``; the repository only ships a hand-written
 4. failure detection / elastic recovery: :meth:`health` pings every
    controller's config port (``ping`` -> ``pong`` with its status); :meth:`failover` drops
    the devices that stopped answering, re-plans the layers over the survivors and hot
-   re-configures them (the reference's live re-shard path, ``node_worker.py:445-474``).
+   re-configures them (the reference's live re-shard path, ``node_worker.py:445-474``);
+5. the RCCL deployment on one node (BASELINE north star: "the master_node scheduler places
+   shards on the 8 GPUs of one node"): :meth:`deploy_pipeline` plans the stages over the
+   controllers of a torchrun job (``start_node.py --backend rccl``: controller i = rank i =
+   GPU i, config port base + i) and sends each the reference config extended with
+   ``mode="pipeline"``, its rank, the world size, the whole stage list and the serving
+   geometry; the controllers then run the micro-batched RCCL pipeline (PipelineServer) and
+   :meth:`submit` feeds requests to rank 0.
 """
 from __future__ import annotations
 
@@ -33,6 +40,7 @@ class MasterNode:
         self.kv_tokens = kv_tokens
         self.plan: Optional[Plan] = None
         self.senders: List[ConfigSender] = []
+        self.mode = "chain"
 
     @classmethod
     def from_shards(cls, shards_path: str, devices: Sequence[DeviceSpec], kv_tokens: int = 4096) -> "MasterNode":
@@ -67,6 +75,34 @@ class MasterNode:
             self.senders.append(s)
         return cfgs
 
+    def deploy_pipeline(self, batch: int = 8, microbatches: int = 0, max_seq: int = 2048,
+                        prefill_budget: int = 2048, streams: int = 1, use_graph: bool = True,
+                        timeout_ms: int = 10000) -> list:
+        """Plan contiguous layer ranges over the devices (device i = torchrun rank i, KV cache of
+        ``microbatches`` x ``batch`` sequences of ``max_seq`` tokens counted against each GPU's
+        HBM) and configure every controller for the micro-batched RCCL pipeline. Returns the
+        configs sent (rank order)."""
+        n = len(self.devices)
+        M = microbatches or max(2, n)
+        self.plan = plan_stages(self.cfg, self.devices, kv_tokens=max_seq * batch * M)
+        stages = [[st.start, st.end] for st in self.plan.stages]
+        ing = self.plan.stages[0].device
+        cfgs, self.senders = [], []
+        for r, st in enumerate(self.plan.stages):
+            d, nxt = st.device, self.plan.stages[(r + 1) % n].device
+            s = ConfigSender(node_port=d.config_port)
+            c = s.build_config(st.start, st.end, r == 0, f"tcp://*:{d.data_port}", f"tcp://{nxt.host}:{nxt.data_port}",
+                               first_node_addr=f"tcp://{ing.host}:{ing.config_port}" if r == 0 else "",
+                               mode="pipeline", backend="rccl", rank=r, world_size=n, stages=stages, batch=batch,
+                               microbatches=M, max_seq=max_seq, prefill_budget=prefill_budget, streams=streams,
+                               use_graph=use_graph)
+            if not s.send_config(d.host, timeout_ms):
+                raise TimeoutError(f"config not delivered to {d.host}:{d.config_port}")
+            self.senders.append(s)
+            cfgs.append(dict(c))
+        self.mode = "pipeline"
+        return cfgs
+
     def health(self, timeout_ms: int = 2000) -> list:
         """[(DeviceSpec, status dict | None)] for every device of the current plan."""
         devs = [st.device for st in self.plan.stages] if self.plan is not None else self.devices
@@ -79,6 +115,10 @@ class MasterNode:
         dead = [d for d, st in status if st is None]
         if not dead:
             return []
+        if self.mode == "pipeline":
+            # an RCCL job cannot lose a rank and continue: the torchrun world is fixed
+            raise RuntimeError(f"[ERROR] pipeline ranks unreachable: {[(d.host, d.config_port) for d in dead]}; "
+                               "restart the torchrun job and redeploy")
         alive = [d for d, st in status if st is not None]
         if not alive:
             raise RuntimeError("[ERROR] every controller is unreachable")
@@ -90,12 +130,16 @@ class MasterNode:
         self.deploy(timeout_ms=max(timeout_ms, 10000))
         return dead
 
-    def submit(self, text: str = "", input_ids=None) -> None:
+    def submit(self, text: str = "", input_ids=None, max_new_tokens: Optional[int] = None,
+               reply_to: Optional[str] = None) -> None:
         ing = self.plan.stages[0].device
-        send_user_request(ing.host, ing.config_port, text=text, input_ids=input_ids)
+        send_user_request(ing.host, ing.config_port, text=text, input_ids=input_ids, max_new_tokens=max_new_tokens,
+                          reply_to=reply_to)
 
     def shutdown(self) -> None:
-        for st in self.plan.stages:
+        # pipeline mode: rank 0 stops the whole job (its STOP header reaches every stage)
+        stages = self.plan.stages[:1] if self.mode == "pipeline" else self.plan.stages
+        for st in stages:
             send_shutdown(st.device.host, st.device.config_port)
         for s in self.senders:
             s.close()

@@ -21,6 +21,14 @@ poll (Q6); a real request ingress (Q7: ``{"command": "user_request", ...}`` on t
 or :meth:`NodeController.receive_request`); no AttributeError when a non-ingress node keeps
 its role (Q8); sockets closed on a role change (Q9).
 
+Pipeline mode (the master's RCCL deployment, ``MasterNode.deploy_pipeline``): a config with
+``"mode": "pipeline"`` plus ``rank`` / ``world_size`` (the controller's torchrun rank) makes the
+controller build a :class:`..parallel.server.PipelineServer` for its layer range instead of a
+NodeWorker - micro-batched continuous batching, hidden states over RCCL on one communicator
+per ring edge, hipGraph decode replays, tokens on the device. Rank 0 is the ingress: its config
+port takes the reference ``user_request`` messages (optionally with ``reply_to``) and
+``shutdown``. No cos/sin tables travel (every stage derives positions from its own KV state).
+
 On ROCm devices the engine computes in bfloat16: ``dtype=torch.float16`` is accepted (the
 reference default) and mapped to bfloat16 with a notice.
 """
@@ -66,7 +74,7 @@ class NodeWorker:
                  device="cpu", dtype=torch.float16, backend: str = "tcp", max_batch: int = 8,
                  max_seq: int = 4096, noncausal_prefill: bool = False,
                  source: Optional[WeightSource] = None, verbose: bool = True,
-                 rccl_ranks: Optional[tuple] = None):
+                 rccl_ranks: Optional[tuple] = None, ship_rope: bool = False):
         # backend "rccl": envelopes over TCP, tensors device-to-device over torch.distributed
         self.communicator = Communicator(src_addr=src_addr, dst_addr=dst_addr, backend=backend,
                                          device=torch.device(device), rccl_ranks=rccl_ranks)
@@ -84,6 +92,7 @@ class NodeWorker:
         self.noncausal_prefill = noncausal_prefill
         self.source = source or ShardFolderSource(shards_path, self.config)
         self.verbose = verbose
+        self.ship_rope = ship_rope  # send real cos/sin tables in next_state_info (reference wire parity)
 
         self.tokenizer = None
         self.embed_tokens = None   # embedding table [V, H] (ingress / head stage)
@@ -195,11 +204,15 @@ class NodeWorker:
         eng.advance(slots, [S] * B)
         if self.end == self.layer_num:
             return eng.head(h, [b * S + S - 1 for b in range(B)]).to("cpu", torch.long)
-        position_ids = torch.arange(past, past + S, dtype=torch.long)[None].expand(B, S)
-        if eng.cos is None:  # GPT-2 (learned positions): keep the message schema, empty tables
+        if eng.cos is None or not self.ship_rope:
+            # every stage derives its positions from its own KV length (the reference ships the
+            # first stage's tables down the chain, node_worker.py:267-271): keep the message
+            # schema with empty tables - no device->host copy, no bytes on the wire
             cos = sin = torch.empty((B, S, 0), dtype=eng.dtype)
-        else:
-            cos, sin = full_cos_sin(eng.cos.cpu(), eng.sin.cpu(), position_ids, dtype=eng.dtype)
+        else:  # ship_rope=True: the reference's [B, S, head_dim] tables (slice on device first)
+            position_ids = torch.arange(0, S, dtype=torch.long)[None].expand(B, S)
+            cos, sin = full_cos_sin(eng.cos[past:past + S].cpu(), eng.sin[past:past + S].cpu(), position_ids,
+                                    dtype=eng.dtype)
         return {"hidden_states": h.reshape(B, S, H).clone(), "cos": cos, "sin": sin}
 
     # ------------------------------------------------------------------ autoregression
@@ -297,6 +310,7 @@ class NodeController:
         self.running = False
         self.finished_outputs: list = []
         self.node_worker: Optional[NodeWorker] = None
+        self.server = None  # PipelineServer (pipeline mode)
         self.forwarded = 0
         self.t_boot = time.monotonic()
         self.received_config = config if config is not None else (self._receive_config() if wait_config else None)
@@ -339,6 +353,12 @@ class NodeController:
 
     def status(self) -> dict:
         """Liveness / role snapshot (answered to ``ping``; SURVEY.md §5.3 stage-liveness)."""
+        if self.server is not None:
+            c = self.received_config or {}
+            return {"listen_port": self.listen_port, "configured": True, "mode": "pipeline",
+                    "shards": [c.get("shards_start"), c.get("shards_end")], "rank": c.get("rank"),
+                    "ingress": c.get("rank") == 0, "finished_requests": len(self.finished_outputs),
+                    "uptime_s": time.monotonic() - self.t_boot}
         w = self.node_worker
         return {"listen_port": self.listen_port, "configured": w is not None,
                 "shards": [w.start, w.end] if w is not None else None,
@@ -361,6 +381,9 @@ class NodeController:
         for k in CONFIG_KEYS:
             if k not in cfg:
                 raise KeyError(f"[ERROR] configuration misses {k!r}")
+        if cfg.get("mode") == "pipeline":
+            self._apply_pipeline_role(cfg)
+            return
         if self.node_worker is not None:
             self.node_worker.close()  # Q9: release the old sockets before rebinding
             self.node_worker = None
@@ -372,6 +395,80 @@ class NodeController:
                                       self.shards_path, device=self.device, dtype=self.dtype, backend=self.backend,
                                       verbose=self.verbose, **kw)
         self.node_worker.load_shards(cfg["shards_start"], cfg["shards_end"])
+
+    def _apply_pipeline_role(self, cfg: dict) -> None:
+        """Build this rank's PipelineServer (collective: every rank of the job does it when its
+        config arrives - the control gloo group and the per-edge RCCL groups are created here)."""
+        import torch.distributed as dist
+        from ..parallel.server import PipelineServer
+        if not dist.is_initialized():
+            raise RuntimeError("[ERROR] pipeline mode needs torch.distributed (start_node.py --backend rccl "
+                               "under torch.distributed.run)")
+        r, n = dist.get_rank(), dist.get_world_size()
+        if int(cfg["rank"]) != r or int(cfg["world_size"]) != n:
+            raise RuntimeError(f"[ERROR] pipeline config for rank {cfg['rank']}/{cfg['world_size']} delivered to "
+                               f"rank {r}/{n}")
+        if self.server is not None:
+            raise RuntimeError("[ERROR] a pipeline is already deployed here: shut it down before re-planning")
+        if self.node_worker is not None:
+            self.node_worker.close()
+            self.node_worker = None
+        mcfg = LlamaConfig.from_pretrained(self.shards_path)
+        source = ShardFolderSource(self.shards_path, mcfg)
+        ctrl = dist.new_group(backend="gloo")  # rank 0's command headers (never blocks a GPU)
+        self.server = PipelineServer(mcfg, source, r, n, int(cfg["shards_start"]), int(cfg["shards_end"]),
+                                     self.device, batch=int(cfg.get("batch", 8)),
+                                     microbatches=int(cfg.get("microbatches", max(2, n))),
+                                     max_seq=int(cfg.get("max_seq", 2048)),
+                                     prefill_budget=int(cfg.get("prefill_budget", 2048)),
+                                     use_graph=bool(cfg.get("use_graph", True)), dtype=self.dtype, ctrl_group=ctrl,
+                                     causal=not self.worker_kwargs.get("noncausal_prefill", False),
+                                     streams=int(cfg.get("streams", 1)))
+        self.tokenizer = None
+        if r == 0:
+            try:
+                self.tokenizer = load_tokenizer(self.shards_path)
+            except Exception as e:  # noqa: BLE001 - token-id requests still work
+                _log(f"[WARNING] no tokenizer ({e}); only input_ids requests are served")
+        if self.verbose:
+            _log(f"[INFO] pipeline stage {r}/{n}: layers [{cfg['shards_start']}, {cfg['shards_end']}) on {self.device}")
+
+    def _run_pipeline(self, max_new_tokens: int) -> None:
+        """Pipeline mode: rank 0 reads requests from its config port on a thread and schedules;
+        the other ranks follow rank 0's commands until it stops (``shutdown``)."""
+        import threading
+        from ..parallel.ingress import Replies, run_ingress
+        stop = threading.Event()
+
+        def other(msg):
+            if isinstance(msg, dict) and msg.get("command") == "ping":
+                self._pong(msg)
+
+        if self.server.first:
+            replies = Replies(self.tokenizer, verbose=self.verbose,
+                              on_done=lambda r, text: self.finished_outputs.append(list(r.output_ids)))
+            th = threading.Thread(target=run_ingress, args=(self.server, self.recv_config_socket, self.tokenizer,
+                                                            stop, max_new_tokens, replies, other), daemon=True)
+            th.start()
+            self.server.serve(stop_when_idle=False, should_stop=stop.is_set)
+            stop.set()
+            th.join(timeout=5)
+            replies.close()
+        else:
+            def pings():
+                while not stop.is_set():
+                    try:
+                        raw = self.recv_config_socket.recv_bytes(200)
+                    except Again:
+                        continue
+                    msg = json.loads(raw.decode())
+                    other(msg)
+            th = threading.Thread(target=pings, daemon=True)
+            th.start()
+            self.server.serve()
+            stop.set()
+            th.join(timeout=5)
+        self.running = False
 
     def _set_first_node_addr(self, cfg: dict) -> None:
         new = cfg.get("first_node_addr", "") if cfg.get("can_receive_user_request") else ""
@@ -473,6 +570,9 @@ class NodeController:
     def run_worker_loop(self, max_new_tokens: int = 1024, max_idle_s: Optional[float] = None) -> None:
         """Serve until a ``shutdown`` command arrives (or ``max_idle_s`` without traffic)."""
         self.running = True
+        if self.server is not None:
+            self._run_pipeline(max_new_tokens)
+            return
         idle_since = time.monotonic()
         while self.running:
             try:
@@ -499,9 +599,15 @@ class NodeController:
         self.recv_config_socket.close()
 
 
-def send_user_request(node_ip: str, port: int, text: str = "", input_ids=None, max_new_tokens: int = None) -> None:
-    """Client helper: submit a request to an ingress NodeController's config port (fixes Q7)."""
+def send_user_request(node_ip: str, port: int, text: str = "", input_ids=None, max_new_tokens: int = None,
+                      reply_to: Optional[str] = None) -> None:
+    """Client helper: submit a request to an ingress NodeController's config port (fixes Q7).
+    ``reply_to``: a PULL address that receives the finished request (pipeline mode / serve.py)."""
     msg = {"command": "user_request", "text": text}
+    if max_new_tokens is not None:
+        msg["max_new_tokens"] = int(max_new_tokens)
+    if reply_to:
+        msg["reply_to"] = reply_to
     if input_ids is not None:
         msg["input_ids"] = [list(map(int, r)) for r in (input_ids.tolist() if hasattr(input_ids, "tolist") else input_ids)]
     s = PushSocket(f"tcp://{node_ip}:{port}")

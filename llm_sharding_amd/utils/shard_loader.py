@@ -97,8 +97,14 @@ class LlamaShardPart(torch.nn.Module):
             eng.reset(range(B))
         else:
             eng.advance(slots, [S] * B)
-        out = out.reshape(B, S, H)
         if self.final_norm is not None:
-            from ..models.reference import rmsnorm
-            out = rmsnorm(out, self.final_norm, self.config.rms_norm_eps).to(eng.dtype)
+            if eng.gpu:  # the HIP RMSNorm kernel (elementwise.hip), weight applied in-kernel
+                from ..ops import hip
+                normed = torch.empty((B * S, H), dtype=torch.bfloat16, device=self.device)
+                hip.rmsnorm(out.contiguous(), self.final_norm, normed, B * S, self.config.rms_norm_eps)
+                out = normed
+            else:
+                from ..models.reference import rmsnorm
+                out = rmsnorm(out, self.final_norm, self.config.rms_norm_eps).to(eng.dtype)
+        out = out.reshape(B, S, H)
         return out.to(self.dtype) if self.device.type == "cpu" else out

@@ -38,54 +38,16 @@ from llm_sharding_amd.utils.runtime_config import RuntimeConfig  # noqa: E402
 
 
 def _ingress(srv, port, tok, stop_evt, default_new):
-    from llm_sharding_amd.parallel import protocol
-    from llm_sharding_amd.parallel.transport import Again, PullSocket, PushSocket
+    from llm_sharding_amd.parallel.ingress import Replies, run_ingress
+    from llm_sharding_amd.parallel.transport import PullSocket
     sock = PullSocket(f"tcp://*:{port}")
     print(f"[INFO] ingress listening on tcp://*:{sock.port}", flush=True)
-    replies = {}
-
-    def done(r, t):
-        if t in r.eos_ids or len(r.output_ids) >= r.max_new_tokens:
-            text = tok.decode(r.output_ids) if tok is not None else ""
-            print(f"[INFO] request {r.rid} done: {len(r.output_ids)} tokens  ttft {r.ttft_ms:.1f} ms  "
-                  f"output: {text!r}", flush=True)
-            if r.reply_to:
-                if r.reply_to not in replies:
-                    replies[r.reply_to] = PushSocket(r.reply_to)
-                replies[r.reply_to].send_bytes(protocol.encode({
-                    "request_id": r.rid, "output_ids": list(r.output_ids), "text": text,
-                    "ttft_ms": r.ttft_ms, "tpot_ms": r.tpot_ms}))
-
-    while not stop_evt.is_set():
-        try:
-            raw = sock.recv_bytes(timeout_ms=200)
-        except Again:
-            continue
-        msg = json.loads(raw) if protocol.is_json_message(raw) else protocol.decode(raw)
-        cmd = msg.get("command")
-        if cmd == "shutdown":
-            stop_evt.set()
-            break
-        if cmd != "user_request":
-            print(f"[WARNING] ingress: unknown message {cmd!r}", flush=True)
-            continue
-        n_new = int(msg.get("max_new_tokens") or default_new)
-        rows = msg.get("input_ids")
-        if rows is None:
-            if tok is None:
-                print("[ERROR] text request but no tokenizer", flush=True)
-                continue
-            rows = [tok.encode(msg.get("text", ""))]
-        elif rows and not isinstance(rows[0], (list, tuple)):
-            rows = [rows]
-        for ids in rows:
-            try:
-                srv.submit(ids, n_new, on_token=done, reply_to=msg.get("reply_to"))
-            except ValueError as e:
-                print(f"[ERROR] request rejected: {e}", flush=True)
-    sock.close()
-    for s in replies.values():
-        s.close()
+    replies = Replies(tok)
+    try:
+        run_ingress(srv, sock, tok, stop_evt, default_new, replies)
+    finally:
+        sock.close()
+        replies.close()
 
 
 def main():

@@ -1,0 +1,104 @@
+"""Master -> ConfigSender -> NodeControllers -> micro-batched pipeline, end to end (SURVEY.md
+C16 + §2.5; BASELINE north star: "the master_node scheduler places shards on the GPUs of one
+node and the hand-off becomes a pipeline-parallel RCCL send/recv chain").
+
+Four controller processes form one torch.distributed job (gloo here; start_node.py --backend
+rccl uses RCCL on GPUs) and wait on their config ports like the reference's run_this.sh nodes.
+The master plans the layer ranges, sends every controller the reference config extended with
+``mode="pipeline"`` + rank/world, submits requests to rank 0's config port with a ``reply_to``
+address and receives the finished outputs, which must equal the fp32 golden model's greedy
+generation token for token."""
+import multiprocessing as mp
+import socket
+
+import pytest
+import torch
+
+from llm_sharding_amd.models import weights as W
+from llm_sharding_amd.models.reference import ReferenceLlama
+
+
+def _ports(n):
+    socks = [socket.socket() for _ in range(n)]
+    for s in socks:
+        s.bind(("127.0.0.1", 0))
+    ports = [s.getsockname()[1] for s in socks]
+    for s in socks:
+        s.close()
+    return ports
+
+
+def _node(rank, world, port, cfg_port, shards, q):
+    import torch.distributed as dist
+    from llm_sharding_amd.parallel.communicator import init_edge_groups
+    from llm_sharding_amd.utils.node_worker import NodeController
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        init_edge_groups()  # what start_node.py --backend rccl does after init_process_group
+        ctrl = NodeController(shards, device="cpu", dtype=torch.float32, listen_port=cfg_port, backend="rccl",
+                              verbose=False)
+        assert ctrl.server is not None and ctrl.status()["mode"] == "pipeline"
+        ctrl.run_worker_loop(max_new_tokens=8)
+        q.put((rank, ctrl.finished_outputs if rank == 0 else "ok"))
+        ctrl.close()
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [4])
+def test_master_deploys_rccl_pipeline_token_exact(tiny_shards, world):
+    from llm_sharding_amd.parallel import protocol
+    from llm_sharding_amd.parallel.scheduler import DeviceSpec
+    from llm_sharding_amd.parallel.transport import PullSocket
+    from llm_sharding_amd.utils.master_node import MasterNode
+    port = _ports(1)[0]
+    cfg_ports, data_ports = _ports(world), _ports(world)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_node, args=(r, world, port, cfg_ports[r], tiny_shards, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    reply = PullSocket("tcp://127.0.0.1:0")
+    try:
+        devs = [DeviceSpec(host="127.0.0.1", config_port=cfg_ports[i], data_port=data_ports[i]) for i in range(world)]
+        master = MasterNode.from_shards(tiny_shards, devs)
+        cfgs = master.deploy_pipeline(batch=2, microbatches=world, max_seq=64, prefill_budget=64)
+        assert [c["rank"] for c in cfgs] == list(range(world)) and all(c["mode"] == "pipeline" for c in cfgs)
+        ranges = [(c["shards_start"], c["shards_end"]) for c in cfgs]
+        assert ranges[0][0] == 0 and all(a[1] == b[0] for a, b in zip(ranges, ranges[1:]))
+        prompts = [[1, 33, 44, 55, 66], [7, 8, 9], [100, 5, 17, 200, 3, 41, 12], [2, 2, 2, 2]]
+        n_new = 6
+        for pr in prompts:
+            master.submit(input_ids=[pr], max_new_tokens=n_new, reply_to=f"tcp://127.0.0.1:{reply.port}")
+        got = {}
+        for _ in prompts:
+            m = protocol.decode(reply.recv_bytes(timeout_ms=120000))
+            got[m["request_id"]] = m["output_ids"]
+        st = master.health()
+        assert all(s is not None and s["mode"] == "pipeline" for _, s in st)
+        master.shutdown()
+        res = {}
+        for _ in range(world):
+            r, v = q.get(timeout=120)
+            res[r] = v
+    finally:
+        reply.close()
+        for p in ps:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    assert all(res[r] == "ok" for r in range(1, world)), res
+    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+    cfg, emb, layers, fn, lm = W.load_full_model(tiny_shards)
+    ref = ReferenceLlama(cfg, emb, layers, fn, lm)
+    eos = set(cfg.eos_ids)
+    for rid, pr in enumerate(prompts):
+        want = ref.generate(torch.tensor([pr]), n_new)[0].tolist()
+        if any(t in eos for t in want):
+            want = want[:next(i for i, t in enumerate(want) if t in eos) + 1]
+        assert got[rid] == want, (rid, got[rid], want)
+    assert sorted(map(tuple, res[0])) == sorted(tuple(got[r]) for r in range(len(prompts)))
