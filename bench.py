@@ -13,9 +13,10 @@ generated on each device - no checkpoints are available offline):
   * M = S x N micro-batches of B sequences each are in flight (S x B sequences per GPU,
     fixed -> weak scaling); every sequence was prefilled with a P-token prompt first. The
     default is one micro-batch of 512 sequences per GPU: above 128 rows a decode step's
-    projections run on the library GEMM (hipBLASLt) + one fused epilogue pass each, which
-    beats the 128-row GEMV kernels on S concurrent streams (profiles/r1_big_batch_decode.txt);
-    with S > 1 each GPU replays its micro-batches' graphs on S HIP streams;
+    projections run on the hand-written stream-K / split-K MFMA GEMM (csrc/kernels/gemm_sk.hip)
+    with its epilogue (RoPE + KV write, residual add, SwiGLU) fused, which beats the 128-row
+    GEMV kernels on S concurrent streams; with S > 1 each GPU replays its micro-batches'
+    graphs on S HIP streams;
   * one timed "step" = every in-flight sequence produces one new token (greedy, fused
     lm_head+argmax on device); hidden states move stage->stage with RCCL send/recv over
     xGMI, token ids return last->first the same way.
@@ -44,7 +45,7 @@ def parse():
     ap.add_argument("--model", default="llama2-7b")
     ap.add_argument("--batch", type=int, default=512,
                     help="sequences per micro-batch (per GPU, <= 1024); <= 128 decode on the fused GEMV "
-                         "kernels, more on the library GEMM + fused epilogue passes")
+                         "kernels, more on the stream-K MFMA GEMM (gemm_sk.hip) with fused epilogues")
     ap.add_argument("--prompt-len", type=int, default=128)
     ap.add_argument("--max-seq", type=int, default=0, help="0 = prompt + warmup + steps, rounded up to 64")
     ap.add_argument("--streams", type=int, default=1,
@@ -63,6 +64,8 @@ def parse():
     ap.add_argument("--latency-steps", type=int, default=32,
                     help="after the throughput pass, time this many batch-1 decode steps through the same "
                          "pipeline (b1_p50_tpot_ms / b1_tok_s in the JSON line); 0 = skip")
+    ap.add_argument("--stage-layers", type=int, default=0,
+                    help="profile one pipeline stage: the model cut to this many layers (NOT the headline metric)")
     ap.add_argument("--device", default="cuda", choices=("cuda", "cpu"),
                     help="cpu: the same schedule on gloo + the torch CPU path (multi-rank rehearsal)")
     return ap.parse_args()
@@ -125,11 +128,11 @@ def main():
                                batch=a.batch, prompt_len=a.prompt_len, max_seq=a.max_seq,
                                microbatches=a.microbatches, seed=a.seed, use_graph=not a.no_graph,
                                weight_dtype=a.weight_dtype, streams=a.streams, dp=a.dp,
-                               latency_steps=a.latency_steps, device=a.device)
+                               latency_steps=a.latency_steps, device=a.device, stage_layers=a.stage_layers)
     if res is None:  # non-zero ranks
         return
     line = {
-        "metric": "output_tokens_per_sec_whole_node",
+        "metric": "stage_profile_tokens_per_sec" if a.stage_layers else "output_tokens_per_sec_whole_node",
         "value": round(res["tok_s"], 2),
         "unit": "tokens/s",
         "n_gpus": a.gpus,
@@ -151,6 +154,7 @@ def main():
         "ttft_ms": round(res["ttft_ms"], 3),
         "b1_p50_tpot_ms": None if res["b1_p50_tpot_ms"] is None else round(res["b1_p50_tpot_ms"], 4),
         "b1_tok_s": None if res["b1_tok_s"] is None else round(res["b1_tok_s"], 2),
+        "mem_pred_gb": res["mem_pred_gb"], "mem_peak_gb": res["mem_peak_gb"],
         "reference_anecdote_tok_s": 4.3,
     }
     print(json.dumps(line), flush=True)

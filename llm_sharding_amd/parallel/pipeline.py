@@ -30,7 +30,7 @@ import torch
 from ..config import get_preset
 from ..runtime.engine import DecodeGraph, EagerDecode, RandomSource, StageEngine
 from ..utils import tracing
-from .scheduler import plan_stages
+from .scheduler import plan_stages, scratch_bytes, stage_memory
 
 
 class DistP2P:
@@ -548,7 +548,8 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
                          batch: int = 16, prompt_len: int = 128, max_seq: int = 0,
                          microbatches: int = 0, seed: int = 0, use_graph: bool = True,
                          verbose: bool = True, weight_dtype: str = "bf16", streams: int = 1,
-                         device: str = "cuda", dp: int = 1, latency_steps: int = 0) -> Optional[dict]:
+                         device: str = "cuda", dp: int = 1, latency_steps: int = 0,
+                         stage_layers: int = 0) -> Optional[dict]:
     """``microbatches`` 0 = ``streams`` x stages (every GPU holds ``streams`` micro-batches of
     ``batch`` sequences: weak scaling); ``max_seq`` 0 = what the run needs, rounded up to 64.
 
@@ -557,8 +558,15 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
     prompts; the numbers are whole-job aggregates (tokens of all replicas over the slowest
     rank's time). The pipelines share no communicator, so a replica's ring stays on its own
     xGMI links (adjacent ranks) and a 7B model fits one GPU many times over: dp8 trades the
-    pipeline's per-token latency for none of its bubbles."""
+    pipeline's per-token latency for none of its bubbles.
+
+    ``stage_layers`` > 0: a STAGE PROFILE, not the headline number - the model's architecture
+    cut to that many decoder layers (embedding and lm_head kept), e.g. one 10-layer stage of
+    Llama-2-70B's 8-stage plan on one GPU with ``microbatches=8`` to hold that stage's KV."""
     cfg = get_preset(model)
+    if stage_layers:
+        import dataclasses
+        cfg = dataclasses.replace(cfg, num_hidden_layers=stage_layers)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     if n_gpus != world:
@@ -594,8 +602,16 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
     M = microbatches or streams * pp
     need = prompt_len + max(warmup + steps, (LAT_WARMUP + latency_steps) if latency_steps else 0) + 1
     max_seq = max_seq or -(-need // 64) * 64
-    plan = plan_stages(cfg, pp, kv_tokens=max_seq * batch * M, head_split=pp > 1)
+    S_sets = max(1, min(streams, M))
+    plan = plan_stages(cfg, pp, kv_tokens=max_seq * batch * M, head_split=pp > 1,
+                       scratch=scratch_bytes(cfg, batch * prompt_len, S_sets, max_seq))
     st = plan.stages[srank]
+    # this stage's device bytes as the engine will allocate them (profiles/memory_table.md)
+    V = cfg.head_rows
+    v1 = (V // 2) // 128 * 128 if pp > 1 else V
+    head_rows = (v1 if st.has_head else 0) + (V - v1 if (pp > 1 and st.has_embed) else 0)
+    mem_pred = stage_memory(cfg, st.n_layers, slots=batch * M, max_seq=max_seq, prefill_rows=batch * prompt_len,
+                            has_embed=st.has_embed, head_rows=head_rows, scratch_sets=S_sets, io_rows=batch * M)
     if need > max_seq:
         raise ValueError(f"prompt+warmup+steps ({need}) exceeds max_seq {max_seq}")
     if verbose and rank == 0:
@@ -667,9 +683,10 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
     if latency_steps > 0:
         lat_p50, lat_el = _latency_pass(cfg, stage, srank, pp, st, dev, max_seq, prompts, prompt_len,
                                         latency_steps, dist, sync, p2p)
+    mem_peak = float(torch.cuda.max_memory_allocated(dev)) if gpu else 0.0
     stats = torch.tensor([elapsed, ttft_ms, _percentile(tpot, 0.5) if tpot else 0.0,
-                          _percentile(tpot, 0.9) if tpot else 0.0, load_s, lat_el, lat_p50],
-                         dtype=torch.float64, device=dev)
+                          _percentile(tpot, 0.9) if tpot else 0.0, load_s, lat_el, lat_p50,
+                          mem_pred["total"], mem_peak], dtype=torch.float64, device=dev)
     if not gpu and stage.last:  # no device events on CPU: wall-clock step time stands in for TPOT
         stats[2] = stats[3] = elapsed * 1e3 / steps
     if dist:
@@ -681,7 +698,9 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
         p50, p90 = float(allst[pp - 1, 2]), float(allst[pp - 1, 3])  # replica 0's last stage
         load_s = float(allst[:, 4].max())
         lat_el, lat_p50 = float(allst[:, 5].max()), float(allst[pp - 1, 6])
+        mem_pred_max, mem_peak_max = float(allst[:, 7].max()), float(allst[:, 8].max())
     else:
+        mem_pred_max, mem_peak_max = float(stats[7]), float(stats[8])
         p50, p90 = float(stats[2]), float(stats[3])
         lat_el, lat_p50 = float(stats[5]), float(stats[6])
     if latency_steps > 0 and not gpu:
@@ -699,12 +718,16 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
         "pp": pp,
         "streams": stage.S,
         "max_seq": max_seq,
-        "model_name": "Llama-2-7B" if model == "llama2-7b" else cfg.name,
+        "model_name": ("Llama-2-7B" if model == "llama2-7b" else cfg.name)
+        + (f" stage profile ({stage_layers} layers)" if stage_layers else ""),
         "load_s": load_s,
         "plan": plan.ranges(),
         "tokens_mb0": tokens_mb0,  # rank 0 only when it holds the history (1 stage or split head)
         "b1_p50_tpot_ms": lat_p50 if latency_steps > 0 else None,
         "b1_tok_s": (dp * latency_steps / lat_el) if latency_steps > 0 and lat_el > 0 else None,
+        # max over ranks: the memory model's stage bytes and torch's measured peak allocation
+        "mem_pred_gb": round(mem_pred_max / 1e9, 2),
+        "mem_peak_gb": round(mem_peak_max / 1e9, 2) if gpu else None,
     }
     trace = tracing.export_env(stage.tl)
     if trace and verbose:

@@ -77,10 +77,11 @@ def default_costs(cfg: LlamaConfig, elem_bytes: int = 2) -> tuple:
 def plan_stages(cfg: LlamaConfig, devices: Sequence[DeviceSpec] | int, *,
                 layer_costs: Optional[Sequence[float]] = None, embed_cost: Optional[float] = None,
                 head_cost: Optional[float] = None, kv_tokens: int = 0, elem_bytes: int = 2,
-                min_layers: int = 1, head_split: bool = False) -> Plan:
+                min_layers: int = 1, head_split: bool = False, scratch: float = 0.0) -> Plan:
     """Exact min-max contiguous partition. ``devices`` is a list (chain order) or a count.
     ``head_split``: the lm_head is shared by the last and the first stage (pipeline.py), so each
-    carries half of its cost and memory."""
+    carries half of its cost and memory. ``scratch``: per-stage engine scratch bytes
+    (:func:`scratch_bytes`), counted against every device's memory next to weights and KV."""
     if isinstance(devices, int):
         devices = [DeviceSpec() for _ in range(devices)]
     n, L = len(devices), cfg.num_hidden_layers
@@ -111,7 +112,7 @@ def plan_stages(cfg: LlamaConfig, devices: Sequence[DeviceSpec] | int, *,
         return t * devices[k].speed
 
     def stage_mem(k: int, a: int, b: int) -> float:
-        m = (b - a) * (lbytes + kv_per_layer)
+        m = (b - a) * (lbytes + kv_per_layer) + scratch
         if k == 0:
             m += emb_bytes + (emb_bytes * 0.5 if split else 0.0)
         if k == n - 1:
@@ -148,7 +149,8 @@ def plan_stages(cfg: LlamaConfig, devices: Sequence[DeviceSpec] | int, *,
     for k in range(n):
         a, b = cuts[k], cuts[k + 1]
         plan.stages.append(StagePlan(k, a, b, devices[k], k == 0, k == n - 1, stage_cost(k, a, b),
-                                     stage_mem(k, a, b) - (b - a) * kv_per_layer, (b - a) * kv_per_layer))
+                                     stage_mem(k, a, b) - (b - a) * kv_per_layer - scratch,
+                                     (b - a) * kv_per_layer))
     return plan
 
 
@@ -167,19 +169,48 @@ def kv_slots_for_memory(cfg: LlamaConfig, n_layers: int, max_seq: int, mem_bytes
     return int(min(max_per_microbatch, free // (per_slot * microbatches)))
 
 
-def scratch_bytes(cfg: LlamaConfig, rows: int, sets: int = 1) -> float:
+def scratch_bytes(cfg: LlamaConfig, rows: int, sets: int = 1, max_seq: int = 4096,
+                  head_rows: int = 0) -> float:
     """Device bytes a stage engine allocates besides weights and KV cache, per ``sets``
-    concurrently replayed scratch sets of ``rows`` rows (StageEngine._alloc_runtime /
-    decode_scratch): activations, attention split partials, the coop-GEMV and gemm_sk
-    workspaces."""
+    concurrently replayed scratch sets sized for ``rows`` rows - the same formulas as
+    StageEngine._alloc_runtime / decode_scratch: activations, attention split partials and
+    their tickets, the coop-GEMV workspace and the gemm_sk slabs (> 128 rows)."""
+    from ..ops import packing
     H, I, nh, hd = cfg.hidden_size, cfg.intermediate_size, cfg.num_attention_heads, cfg.head_dim
-    R = max(rows, 128)
-    act = R * (2 * H + 2 * cfg.q_size + I) * 2
-    ws_rows = max(128 * 16, 4 * R)
-    attn = ws_rows * nh * (hd + 1) * 4
-    coop = (1 << 24) * 4
-    sk = 2 * 256 * 256 * 256 * 4 if R > 128 else 0
+    dmr = packing.GEMV_MAX_ROWS
+    R = max(rows, dmr)
+    act = R * (2 * H + 2 * cfg.q_size + I) * 2 + R * (8 + 4)        # buffers + keys + tokens
+    nsplit = int(min(16, max(1, -(-max_seq // 256))))
+    ws_rows = max(dmr * nsplit, 4 * R)
+    attn = ws_rows * (nh * hd * 4 + nh * 4 + cfg.num_key_value_heads * 4)
+    shapes = [(cfg.qkv_size, H), (H, cfg.q_size), (cfg.mlp_in_size, H), (H, I)]
+    if head_rows:
+        shapes.append((head_rows, H))
+    even = () if cfg.is_gpt2 else ((2 * I, H),)
+    floats, groups = packing.coop_workspace_need(shapes, dmr, even_n=even)
+    coop = max(floats, 1 << 24) * 4 + max(groups, 4096) * 4
+    sk = (2 * 256 * 256 * 256 * 4 + 4 * 256 * 4) if R > dmr else 0
     return float(sets * (act + attn + coop + sk))
+
+
+def stage_memory(cfg: LlamaConfig, n_layers: int, *, slots: int, max_seq: int, prefill_rows: int,
+                 has_embed: bool = False, head_rows: int = 0, scratch_sets: int = 1,
+                 io_rows: int = 0, elem_bytes: int = 2) -> dict:
+    """Device bytes of one pipeline stage as the engine allocates them (weights, static KV cache,
+    scratch) - the memory table the bench's stage sizing relies on (profiles/memory_table.md).
+    ``head_rows``: lm_head rows held on this stage (split head: a part of the vocabulary);
+    ``io_rows``: per-micro-batch hidden/token hand-off buffers (PipelineStage.h_out/tok_out)."""
+    H = cfg.hidden_size
+    w = n_layers * cfg.layer_bytes(elem_bytes)
+    if has_embed:
+        w += cfg.vocab_size * H * elem_bytes
+    if head_rows:
+        w += head_rows * H * elem_bytes + H * elem_bytes          # lm_head part + final norm
+    kv = n_layers * cfg.kv_bytes_per_token_per_layer(elem_bytes) * slots * max_seq
+    scratch = scratch_bytes(cfg, prefill_rows, scratch_sets, max_seq, head_rows)
+    io = io_rows * (H * elem_bytes + 4 + 8)
+    return {"weights": float(w), "kv": float(kv), "scratch": float(scratch), "io": float(io),
+            "total": float(w + kv + scratch + io)}
 
 
 def even_split(n_layers: int, n_stages: int) -> list:

@@ -418,18 +418,23 @@ class StageEngine:
                 setattr(self, a, v)
 
     def memory_bytes(self) -> int:
-        n = 0
+        """Bytes of weights + KV cache (tensors that share storage are counted once)."""
+        ts = []
         for lw in self.layers:
-            for t in (lw.qkv, lw.o, lw.gate_up, lw.down, lw.ln_in, lw.ln_post, lw.qkv_s, lw.o_s, lw.gate_up_s,
-                      lw.down_s, lw.ln_in_b, lw.ln_post_b, lw.qkv_b, lw.o_b, lw.gate_up_b, lw.down_b):
-                if t is not None:
-                    n += t.numel() * t.element_size()
+            ts += [lw.qkv, lw.o, lw.gate_up, lw.down, lw.ln_in, lw.ln_post, lw.qkv_s, lw.o_s, lw.gate_up_s,
+                   lw.down_s, lw.ln_in_b, lw.ln_post_b, lw.qkv_b, lw.o_b, lw.gate_up_b, lw.down_b]
             if lw.raw is not None:
-                n += sum(t.numel() * t.element_size() for t in lw.raw.values())
-        for t in (self.embed_w, self.final_norm, self.lm_head, self.pos_emb, self.final_norm_b, self.lm_head_s):
-            if t is not None:
+                ts += list(lw.raw.values())
+        ts += [self.embed_w, self.final_norm, self.lm_head, self.pos_emb, self.final_norm_b, self.lm_head_s]
+        ts += self.k_cache + self.v_cache
+        seen, n = set(), 0
+        for t in ts:
+            if t is None:
+                continue
+            key = (t.untyped_storage().data_ptr(), t.storage_offset(), t.numel())
+            if key not in seen:
+                seen.add(key)
                 n += t.numel() * t.element_size()
-        n += sum(t.numel() * t.element_size() for t in self.k_cache + self.v_cache)
         return n
 
     # ------------------------------------------------------------------------- state
