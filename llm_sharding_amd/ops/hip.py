@@ -12,6 +12,7 @@ If the library is missing on a machine with a GPU we raise - there is no silent 
 from __future__ import annotations
 
 import ctypes
+import json
 import os
 from typing import Optional
 
@@ -343,14 +344,39 @@ def default_sk_workspace(device=None) -> SkWorkspace:
 N_CU = 256
 
 
-def gemm_sk_plan(M: int, N: int, K: int) -> tuple:
+SK_TUNING_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_sk_tuning.json")
+_SK_TUNED = None
+
+
+def _sk_tuned() -> dict:
+    """(N, K) -> [(M, (bn, grid, dp, split)), ...] from scripts/tune_gemm_sk.py's measurements."""
+    global _SK_TUNED
+    if _SK_TUNED is None:
+        _SK_TUNED = {}
+        if os.path.exists(SK_TUNING_FILE):
+            with open(SK_TUNING_FILE) as f:
+                for e in json.load(f).get("entries", []):
+                    _SK_TUNED.setdefault((e["N"], e["K"]), []).append((e["M"], tuple(e["cfg"])))
+    return _SK_TUNED
+
+
+def gemm_sk_plan(M: int, N: int, K: int, tuned: bool = True) -> tuple:
     """(bn, grid, dp, split) for ``gemm_sk``. Grid = one workgroup per CU (the kernel holds
     ~136-144 KiB of LDS). Whole tiles go out in data-parallel rounds; the remainder either as
     equal K splits (concurrent workgroups stream the same K offsets: L2 reuse) or by stream-K.
-    Costs per 64-deep K step measured on MI355X (scripts/bench_gemm_sk.py): ~1.5 us for a
-    256x256 tile, ~1.1 us for 256x128; stream-K's staggered K offsets lose ~2x of that to L2
-    misses; every extra partial costs one 256 x bn fp32 slab read (~100 GB/s per workgroup)."""
+
+    ``tuned``: a shape measured by scripts/tune_gemm_sk.py (same N, K and the same number of
+    256-row tiles, nearest M) takes its measured winner. Otherwise a cost model: per 64-deep K
+    step ~1.5 us for a 256x256 tile, ~1.1 us for 256x128 (scripts/bench_gemm_sk.py); stream-K's
+    staggered K offsets lose ~2x of that to L2 misses; every extra partial costs one 256 x bn
+    fp32 slab read (~100 GB/s per workgroup)."""
     mt = -(-M // SK_BM)
+    if tuned:
+        cands = [(abs(m - M), cfg) for m, cfg in _sk_tuned().get((N, K), ()) if -(-m // SK_BM) == mt]
+        if cands:
+            cfg = min(cands)[1]
+            if N % cfg[0] == 0:
+                return (cfg[0], N_CU, cfg[2], cfg[3])
     nkt = K // 64
     best = None
     for bn, c_it in ((256, 1.5), (128, 1.1)):

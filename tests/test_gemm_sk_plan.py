@@ -1,0 +1,28 @@
+"""gemm_sk's work-decomposition planner (ops/hip.py gemm_sk_plan): measured winners from
+ops/gemm_sk_tuning.json (scripts/tune_gemm_sk.py) for tuned shapes, the cost model elsewhere;
+every plan is one the kernel accepts (N % bn == 0, one workgroup per CU)."""
+from llm_sharding_amd.ops import hip
+
+
+def test_tuned_shapes_use_the_table():
+    tab = hip._sk_tuned()
+    assert tab, "ops/gemm_sk_tuning.json missing or empty"
+    for (N, K), rows in tab.items():
+        for M, cfg in rows:
+            assert hip.gemm_sk_plan(M, N, K) == (cfg[0], hip.N_CU, cfg[2], cfg[3])
+
+
+def test_nearest_measured_m_with_same_row_tiles():
+    tab = hip._sk_tuned()
+    rows = dict(tab[(4096, 4096)])
+    # 500 rows -> two 256-row tiles: the M=512 (or 384) entry, never the M=256 one
+    got = hip.gemm_sk_plan(500, 4096, 4096)
+    want = rows[512] if 512 in rows else rows[384]
+    assert got == (want[0], hip.N_CU, want[2], want[3])
+
+
+def test_cost_model_for_untuned_shapes():
+    for M, N, K in [(65536, 12288, 4096), (300, 5120, 3072), (4096, 128, 64)]:
+        bn, grid, dp, split = hip.gemm_sk_plan(M, N, K)
+        assert bn in (128, 256) and N % bn == 0 and grid == hip.N_CU and split >= 0
+        assert hip.gemm_sk_plan(M, N, K, tuned=False) == (bn, grid, dp, split) or (N, K) in hip._sk_tuned()
