@@ -27,8 +27,11 @@
 namespace {
 
 constexpr int BM = 256, BK = 64, NTHR = 512;
-constexpr int ELD = 68;  // fp32 row stride of the epilogue transpose image (2-way banked writes)
 
+// BN = 256: 2 x 4 waves of 128 x 64; BN = 192 / 128: 4 x 2 waves of 64 x 96 / 64 x 64.
+// BN = 192 exists for shapes where 256-wide tiles leave CUs idle or need split-K fixups
+// (Llama-2-7B qkv N=12288 at M=512: 2 x 64 = 128 tiles; gate_up N=22016: 230 tiles in one
+// round at full K); N need not be a multiple of 192 (the last column tile is partial).
 template <int BN, int NB>
 struct Geo {
   static constexpr int WM = BN == 256 ? 2 : 4;   // wave grid
@@ -39,11 +42,18 @@ struct Geo {
   static constexpr int BREG = (BN / 2) * BK * 2;    // bytes of one B region
   static constexpr int BUF = 2 * AREG + 2 * BREG;   // one K-tile
   static constexpr int AGL = AREG / 1024 / 8;       // DMA instructions per wave per A region
-  static constexpr int BGL = BREG / 1024 / 8;       // ... per B region
-  static constexpr int NPT = 2 * AGL + 2 * BGL;     // DMA instructions per wave per K-tile
-  static constexpr int EPI_BYTES = 8 * 64 * ELD * 4;
+  static constexpr int BBLK = BREG / 1024;          // 1 KiB blocks per B region (16 / 12 / 8)
+  // block b of a B region is issued by wave b % 8: with 12 blocks waves 0-3 issue 2 per
+  // region and waves 4-7 one, so the per-wave counts (and counted waits) depend on the wave
+  static constexpr int BGL = (BBLK + 7) / 8, BGL_LO = BBLK / 8, BHI_WAVES = BBLK % 8;
+  static constexpr int NPT = 2 * AGL + 2 * BGL;     // DMA instructions per K-tile, waves < BHI_WAVES
+  static constexpr int NPT_LO = 2 * AGL + 2 * BGL_LO;  // ... the other waves
+  static constexpr int EROWS = TN > 64 ? 32 : 64;   // rows per epilogue transpose pass
+  static constexpr int ELD = TN + 4;                // fp32 row stride of the transpose image
+  static constexpr int EPI_BYTES = 8 * EROWS * ELD * 4;
   static constexpr int SMEM = (NB * BUF > EPI_BYTES ? NB * BUF : EPI_BYTES) + 16;
   static_assert(SMEM <= 160 * 1024, "LDS budget");
+  static_assert(BHI_WAVES == 0 || BGL_LO == 0 || BHI_WAVES == 4, "B blocks per wave");
 };
 
 struct SkParams {
@@ -106,7 +116,8 @@ struct Kern {
   using G_ = Geo<BN, NB>;
   static constexpr int WM = G_::WM, WN = G_::WN, TM = G_::TM, TN = G_::TN, FM = G_::FM, FN = G_::FN;
   static constexpr int AREG = G_::AREG, BREG = G_::BREG, BUF = G_::BUF, AGL = G_::AGL, BGL = G_::BGL,
-                       NPT = G_::NPT;
+                       NPT = G_::NPT, NPT_LO = G_::NPT_LO, BGL_LO = G_::BGL_LO, BHI_WAVES = G_::BHI_WAVES,
+                       BBLK = G_::BBLK;
   static constexpr int HM = FM / 2, HN = FN / 2;  // quadrant size in 16x16 tiles
 
   unsigned char* smem;
@@ -131,7 +142,25 @@ struct Kern {
     unsigned char* dst = smem + buf * BUF + 2 * AREG + nh * BREG;
     const unsigned char* base = b_seg + (size_t)kt * 2048;
 #pragma unroll
-    for (int s = 0; s < BGL; ++s) glds16(base + boff[nh][s], dst + (w * BGL + s) * 1024);
+    for (int s = 0; s < BGL; ++s)
+      if (s < BGL_LO || w < BHI_WAVES) glds16(base + boff[nh][s], dst + (s * 8 + w) * 1024);
+  }
+  // counted wait keeping one K-tile of this wave's DMA in flight (+ EXTRA instructions)
+  template <int EXTRA = 0>
+  LSA_DEVICE void wait_tile() {
+    if constexpr (NPT == NPT_LO) {
+      vm_wait<NPT + EXTRA>();
+    } else {
+      if (w < BHI_WAVES) vm_wait<NPT + EXTRA>(); else vm_wait<NPT_LO + EXTRA>();
+    }
+  }
+  // counted wait leaving one A and one B region of this wave's DMA in flight
+  LSA_DEVICE void wait_ab() {
+    if constexpr (NPT == NPT_LO) {
+      vm_wait<AGL + BGL>();
+    } else {
+      if (w < BHI_WAVES) vm_wait<AGL + BGL>(); else vm_wait<AGL + BGL_LO>();
+    }
   }
 
   // ---- one segment: K-tiles [ka, kb) of output tile (mt, nt), accumulated into acc -------------
@@ -154,13 +183,14 @@ struct Kern {
         const int row = min(m0 + wr_ * TM + mh * (TM / 2) + i * 16 + (lane & 15), P.M - 1) - m0;
         aoff[mh][s] = (unsigned)((row * P.lda + kf * 32 + 8 * (lane >> 4)) * 2);
       }
+    const int nt16_last = (P.N >> 4) - 1 - (n0 >> 4);  // partial last column tile (BN = 192): clamp
 #pragma unroll
     for (int nh = 0; nh < 2; ++nh)
 #pragma unroll
       for (int s = 0; s < BGL; ++s) {
-        const int b = w * BGL + s, kf = b & 1, wj = b >> 1;
+        const int b = (s * 8 + w) % BBLK, kf = b & 1, wj = b >> 1;
         const int wc_ = wj / HN, j = wj % HN;
-        const int ntl = wc_ * FN + nh * HN + j;
+        const int ntl = min(wc_ * FN + nh * HN + j, nt16_last);
         boff[nh][s] = (unsigned)(((ntl * KT32 + kf) * 64 + lane) * 16);
       }
 
@@ -178,10 +208,10 @@ struct Kern {
         stage_a(1, 1, aoff, 1);
         vm_wait<BGL + AGL + NPT>();
       } else {
-        vm_wait<NPT>();
+        wait_tile();
       }
     } else {
-      vm_wait<AGL + BGL>();
+      wait_ab();
     }
     barrier();
     if (group) barrier();  // stagger: waves 4-7 run one barrier behind waves 0-3
@@ -224,21 +254,21 @@ struct Kern {
         const int cur = t & 1, nxt = cur ^ 1;
         rd_a(cur, 0);
         rd_b(cur, 0, b0);
-        if (t + 1 < n) { stage_b(nxt, 1, boff, t + 1); vm_wait<NPT>(); } else vm_wait<0>();
+        if (t + 1 < n) { stage_b(nxt, 1, boff, t + 1); wait_tile(); } else vm_wait<0>();
         barrier();
         mma(0, b0, 0);
         barrier();
         rd_b(cur, 1, b1);
-        if (t + 1 < n) { stage_a(nxt, 1, aoff, t + 1); vm_wait<NPT>(); } else vm_wait<0>();
+        if (t + 1 < n) { stage_a(nxt, 1, aoff, t + 1); wait_tile(); } else vm_wait<0>();
         barrier();
         mma(0, b1, 1);
         barrier();
         rd_a(cur, 1);
-        if (t + 2 < n) { stage_a(cur, 0, aoff, t + 2); vm_wait<NPT>(); } else vm_wait<0>();
+        if (t + 2 < n) { stage_a(cur, 0, aoff, t + 2); wait_tile(); } else vm_wait<0>();
         barrier();
         mma(1, b1, 1);
         barrier();
-        if (t + 2 < n) { stage_b(cur, 0, boff, t + 2); vm_wait<NPT>(); } else vm_wait<0>();
+        if (t + 2 < n) { stage_b(cur, 0, boff, t + 2); wait_tile(); } else vm_wait<0>();
         barrier();
         mma(1, b0, 0);
         barrier();
@@ -293,7 +323,7 @@ struct Kern {
   // read sc1: they bypass this CU's L1, which may hold stale copies). Caller: every wave, LDS
   // free (and a barrier before the LDS is reused by other waves).
   LSA_DEVICE void slab_add(const float* slab, size_t slot, f32x4_t (&acc)[FM][FN]) {
-    constexpr int RP = 2, NP = FM / RP, PB = RP * FN;  // tile rows per pass, passes, blocks per pass
+    constexpr int RP = FN > 4 ? 1 : 2, NP = FM / RP, PB = RP * FN;  // tile rows / pass, passes, blocks / pass
     const unsigned char* src = reinterpret_cast<const unsigned char*>(slab + slot * (size_t)(BM * BN)) +
                                (size_t)(w * FM * FN) * 1024 + lane * 16;
     unsigned char* ring = smem + w * (2 * PB * 1024);
@@ -325,28 +355,30 @@ struct Kern {
   // ---- fused epilogue through an LDS transpose -------------------------------------------------
   LSA_DEVICE void epilogue(const EpiArgs& ep, const f32x4_t (&acc)[FM][FN], int mt, int nt) {
     const SkParams& P = *p;
-    float* img = reinterpret_cast<float*>(smem) + w * (64 * ELD);
-    constexpr int PASSES = TM / 64;  // 64 rows of this wave's tile per pass
+    constexpr int EROWS = G_::EROWS, ELD = G_::ELD, FPP = EROWS / 16;  // rows / fragments per pass
+    float* img = reinterpret_cast<float*>(smem) + w * (EROWS * ELD);
+    constexpr int PASSES = TM / EROWS;
 #pragma unroll
     for (int ps = 0; ps < PASSES; ++ps) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < FPP; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            img[(i * 16 + 4 * (lane >> 4) + r) * ELD + j * 16 + (lane & 15)] = acc[ps * 4 + i][j][r];
+            img[(i * 16 + 4 * (lane >> 4) + r) * ELD + j * 16 + (lane & 15)] = acc[ps * FPP + i][j][r];
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      const int row_base = mt * BM + wr * TM + ps * 64;
+      const int row_base = mt * BM + wr * TM + ps * EROWS;
       const int col_base = nt * BN + wc * TN;
       if (EPI == EPI_SWIGLU) {
-        // units: 64 rows x FN/2 gate|up tile pairs
+        // units: EROWS rows x FN/2 gate|up tile pairs
+        constexpr int UNITS = EROWS * (FN / 2);
 #pragma unroll
-        for (int s = 0; s < (64 * (FN / 2)) / 64; ++s) {
+        for (int s = 0; s < (UNITS + 63) / 64; ++s) {
           const int u = lane + 64 * s, row = u / (FN / 2), pr = u % (FN / 2);
-          const int m = row_base + row;
+          const int m = (UNITS % 64 == 0 || u < UNITS) ? row_base + row : P.M;
           const float* src = img + row * ELD + pr * 32;
           float g[16], uu[16], v[16];
 #pragma unroll
@@ -355,7 +387,7 @@ struct Kern {
             *reinterpret_cast<f32x4_t*>(uu + 4 * q) = *reinterpret_cast<const f32x4_t*>(src + 16 + 4 * q);
           }
           const int c0 = col_base + pr * 32;
-          if (m < P.M) {
+          if (m < P.M && (BN != 192 || c0 < P.N)) {
             epi_bias16(ep, c0, g);
             epi_bias16(ep, c0 + 16, uu);
 #pragma unroll
@@ -368,14 +400,14 @@ struct Kern {
         }
       } else {
 #pragma unroll
-        for (int s = 0; s < (64 * FN) / 64; ++s) {
+        for (int s = 0; s < (EROWS * FN) / 64; ++s) {
           const int u = lane + 64 * s, row = u / FN, j = u % FN;
           const int m = row_base + row;
           const float* src = img + row * ELD + j * 16;
           float v[16];
 #pragma unroll
           for (int q = 0; q < 4; ++q) *reinterpret_cast<f32x4_t*>(v + 4 * q) = *reinterpret_cast<const f32x4_t*>(src + 4 * q);
-          if (m < P.M) epi_row16<EPI>(ep, m, col_base + j * 16, v);
+          if (m < P.M && (BN != 192 || col_base + j * 16 < P.N)) epi_row16<EPI>(ep, m, col_base + j * 16, v);
           __builtin_amdgcn_sched_barrier(0);
         }
       }
@@ -522,7 +554,8 @@ int launch(const bf16_raw* A, const bf16_raw* W, const SkParams& prm, const EpiA
 
 }  // namespace
 
-// bn: tile width 256 (2-buffer DMA ring) or 128 (nb = 2 or 3 buffers; 0 = 3); grid: workgroups
+// bn: tile width 256 / 192 (2-buffer DMA ring; 192: N % 16 == 0, partial last tile) or 128 (nb = 2
+// or 3 buffers; 0 = 3); grid: workgroups
 // (<= 1024); dp: 1 = whole tiles in data-parallel rounds first (0 = all tiles are remainder);
 // split: 0 = remainder by stream-K, S >= 1 = remainder tiles split into up to S K ranges
 // (clamped to NKT and to grid / remainder tiles; stream-K when the remainder exceeds the grid); slab: >= 2 * grid * 256 * bn floats and counters: >= remainder tiles (zeroed) when
@@ -531,10 +564,10 @@ extern "C" int lsa_gemm_sk(const void* a, int lda, const void* wp, int M, int N,
                            const EpiArgs* ep, int bn, int nb, int grid, int dp, int split, int group_m, float* slab,
                            unsigned* counters, long long slab_floats, int n_counters, hipStream_t stream) {
   if (M < 1 || K < BK || K % BK || lda < K || lda % 8 || !ep) return LSA_BAD_SHAPE;
-  if (bn != 256 && bn != 128) return LSA_UNSUPPORTED;
-  if (nb == 0) nb = bn == 256 ? 2 : 3;
+  if (bn != 256 && bn != 192 && bn != 128) return LSA_UNSUPPORTED;
+  if (nb == 0) nb = bn == 128 ? 3 : 2;
   if (nb != 2 && !(nb == 3 && bn == 128)) return LSA_UNSUPPORTED;
-  if (N % bn) return LSA_BAD_SHAPE;
+  if (bn == 192 ? (N % 16 || (epi == EPI_SWIGLU && N % 32)) : N % bn) return LSA_BAD_SHAPE;
   if (grid < 1 || grid > 1024 || group_m < 1) return LSA_BAD_SHAPE;
   if (epi == EPI_RESID && !ep->resid) return LSA_BAD_SHAPE;
   if (epi == EPI_QKV && (!ep->k_cache || !ep->v_cache || !ep->slot || !ep->pos)) return LSA_BAD_SHAPE;
@@ -545,7 +578,7 @@ extern "C" int lsa_gemm_sk(const void* a, int lda, const void* wp, int M, int N,
   prm.K = K;
   prm.lda = lda;
   prm.MT = (M + BM - 1) / BM;
-  prm.NT = N / bn;
+  prm.NT = (N + bn - 1) / bn;
   prm.NKT = K / BK;
   prm.group_m = group_m;
   const long long tiles = (long long)prm.MT * prm.NT;
@@ -572,6 +605,7 @@ extern "C" int lsa_gemm_sk(const void* a, int lda, const void* wp, int M, int N,
   const bf16_raw* A = static_cast<const bf16_raw*>(a);
   const bf16_raw* W = static_cast<const bf16_raw*>(wp);
 #define LSA_G(E) (bn == 256 ? launch<256, E, 2>(A, W, prm, *ep, slab, counters, stream)      \
+                 : bn == 192 ? launch<192, E, 2>(A, W, prm, *ep, slab, counters, stream)   \
                           : nb == 3 ? launch<128, E, 3>(A, W, prm, *ep, slab, counters, stream) \
                                     : launch<128, E, 2>(A, W, prm, *ep, slab, counters, stream))
   switch (epi) {

@@ -375,14 +375,14 @@ def gemm_sk_plan(M: int, N: int, K: int, tuned: bool = True) -> tuple:
         cands = [(abs(m - M), cfg) for m, cfg in _sk_tuned().get((N, K), ()) if -(-m // SK_BM) == mt]
         if cands:
             cfg = min(cands)[1]
-            if N % cfg[0] == 0:
+            if N % (16 if cfg[0] == 192 else cfg[0]) == 0:
                 return (cfg[0], N_CU, cfg[2], cfg[3])
     nkt = K // 64
     best = None
-    for bn, c_it in ((256, 1.5), (128, 1.1)):
-        if N % bn:
+    for bn, c_it in ((256, 1.5), (192, 1.2), (128, 1.1)):
+        if N % (16 if bn == 192 else bn):
             continue
-        tiles = mt * (N // bn)
+        tiles = mt * -(-N // bn)
         rounds, rem = divmod(tiles, N_CU)
         slab_us = SK_BM * bn * 4 / 100e3
         cands = [(rounds * nkt * c_it if rem == 0 else float("inf"), (bn, N_CU, 1, 0))]
@@ -402,7 +402,8 @@ def gemm_sk(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int,
             bn: int = 0, grid: int = 0, dp: int = 1, group_m: int = 8, nb: int = 0, split: int = -1,
             ws: Optional[SkWorkspace] = None) -> None:
     """Projection GEMM for any M (gemm_sk.hip): 256 x ``bn`` tiles, LDS-DMA staged, data-parallel
-    rounds + stream-K, fused epilogue. ``wp`` = pack_b(W[N, K]); N % bn == 0, K % 64 == 0."""
+    rounds + stream-K, fused epilogue. ``wp`` = pack_b(W[N, K]); K % 64 == 0; N % bn == 0 for
+    bn = 128 / 256, N % 16 == 0 for bn = 192 (partial last column tile)."""
     _req(_is_bf16_cuda(a, wp), "gemm_sk: bf16 cuda tensors required")
     _req(wp.numel() == N * K and K % 64 == 0 and K >= 64, "gemm_sk: packed weight shape")
     _req(a.dim() == 2 and a.shape[0] >= M >= 1 and a.shape[1] >= K and a.stride(1) == 1 and a.stride(0) % 8 == 0,
@@ -416,7 +417,8 @@ def gemm_sk(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int,
     grid = grid or pg
     if split < 0:
         split = 0
-    _req(bn in (128, 256) and N % bn == 0, f"gemm_sk: N={N} not a multiple of bn={bn}")
+    _req(bn in (128, 192, 256) and N % (16 if bn == 192 else bn) == 0 and (bn != 192 or epi != EPI_SWIGLU or N % 32 == 0),
+         f"gemm_sk: N={N} does not tile by bn={bn}")
     _req(1 <= grid <= 1024, "gemm_sk: grid")
     if ws is None:
         ws = default_sk_workspace(a.device)

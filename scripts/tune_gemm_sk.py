@@ -76,8 +76,8 @@ def main():
                     out = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
                     ep = hip.make_epi(out=out, resid=out, ldo=N, ldr=N)
                 res = []
-                for bn in (256, 128):
-                    if N % bn:
+                for bn in (256, 192, 128):
+                    if N % (16 if bn == 192 else bn):
                         continue
                     for sp in SPLITS:
                         try:

@@ -1,4 +1,4 @@
-"""gemm_sk.hip (LDS-DMA 256 x BN tiles, data-parallel rounds + stream-K, fused epilogues)
+"""gemm_sk.hip (LDS-DMA 256 x BN tiles, BN = 256 / 192 / 128, data-parallel rounds + stream-K, fused epilogues)
 against plain PyTorch fp32 references: every epilogue, both tile widths, grids that split tiles
 between workgroups (stream-K partial slabs + last-arriver combine) and grids that do not."""
 import pytest
@@ -33,8 +33,15 @@ def ws():
 
 # (bn, grid, dp, split): planner default, whole-tile rounds + stream-K, pure stream-K, odd grids
 # (bijective XCD remap), equal K splits of the remainder (2-, 3- and 8-way), 128-wide 2-buffer ring
+# and 192-wide tiles (4 x 2 waves, uneven B-DMA split over the waves, partial last column tile)
 CFGS = [(0, 0, 1, -1), (256, 256, 1, 0), (128, 256, 1, 0), (256, 37, 0, 0), (128, 13, 1, 0), (256, 1000, 0, 0),
-        (256, 256, 1, 2), (128, 256, 0, 3), (256, 512, 1, 8), (128, 96, 1, 1)]
+        (256, 256, 1, 2), (128, 256, 0, 3), (256, 512, 1, 8), (128, 96, 1, 1), (192, 256, 1, 0), (192, 256, 1, 2),
+        (192, 37, 0, 0)]
+
+
+def _skip(bn, N):
+    """bn = 192 takes any N % 16 == 0 (partial last tile); 128 / 256 need N % bn == 0."""
+    return bn and N % (16 if bn == 192 else bn)
 
 
 @pytest.mark.parametrize("M", [1, 129, 256, 300, 512, 777])
@@ -47,10 +54,10 @@ def test_gemm_sk_store_resid(M, N, K, ws):
     ref = a.float() @ w.float().T
     r = _rnd(M, N)
     for (bn, grid, dp, split) in CFGS:
-        if bn and N % bn:
+        if _skip(bn, N):
             continue
         nb = 2 if (bn, grid) == (128, 96) else 0
-        tiles = -(-M // 256) * (N // (bn or 256))
+        tiles = -(-M // 256) * -(-N // (bn or 256))
         if split > 0 and tiles * split > grid:
             continue
         out = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
@@ -86,7 +93,7 @@ def test_gemm_sk_swiglu(M, ws):
     wp = packing.pack_b(packing.fuse_gate_up(wg, wu))
     ref = F.silu(x.float() @ wg.float().T) * (x.float() @ wu.float().T)
     for (bn, grid, dp, split) in CFGS:
-        tiles = -(-M // 256) * (2 * I // (bn or 256))
+        tiles = -(-M // 256) * -(-2 * I // (bn or 256))
         if split > 0 and tiles * split > grid:
             continue
         out = torch.zeros(M, I, dtype=torch.bfloat16, device=DEV)
@@ -103,7 +110,7 @@ def _rope_ref(t, pos, cos, sin):
 
 
 @pytest.mark.parametrize("nh,nkv,hd", [(32, 32, 128), (8, 2, 64), (24, 8, 128)])
-@pytest.mark.parametrize("cfg", [(0, 0, 1, -1), (128, 29, 0, 0), (256, 256, 1, 3)])
+@pytest.mark.parametrize("cfg", [(0, 0, 1, -1), (128, 29, 0, 0), (256, 256, 1, 3), (192, 256, 1, 2)])
 def test_gemm_sk_qkv_rope_kv_append(nh, nkv, hd, cfg, ws):
     from llm_sharding_amd.config import tiny
     from llm_sharding_amd.models.rope import rope_table
@@ -122,7 +129,7 @@ def test_gemm_sk_qkv_rope_kv_append(nh, nkv, hd, cfg, ws):
     ep = h.make_epi(out=q, k_cache=kc, v_cache=vc, slot=slot, pos=pos, cos=cos, sin=sin, ldo=nh * hd,
                     n_heads=nh, n_kv=nkv, head_dim=hd, t_max=T)
     bn, grid, dp, split = cfg
-    if bn and N % bn:
+    if _skip(bn, N):
         pytest.skip("N not a multiple of bn")
     h.gemm_sk(x, wp, M, N, H, h.EPI_QKV, ep, bn=bn, grid=grid, dp=dp, split=split, ws=ws)
     xf, pl, sl = x.float(), pos.long(), slot.long()
