@@ -11,6 +11,7 @@
 //                     run in fp32 in the exp2 domain. Row m attends keys [0, kvlen(m)):
 //                     kvlen = pos+1 (causal; decode and prefill alike) unless an explicit
 //                     kv_len array is given (the reference's unmasked prefill, Q1).
+//                     K/V rows are read with non-temporal loads (streamed once per step).
 //                     The split count is fixed per launch (graph-capturable); the chunk is
 //                     derived on-device from the current length, so empty splits exit.
 //                     With nsplit > 1 every split publishes its (o, lse) partials with
@@ -28,7 +29,9 @@ constexpr int ATT_THR = ATT_WAVES * LSA_WAVE;
 constexpr float NEG_BIG = -1e30f;
 constexpr int ATT_MAX_SPLIT = 16;  // split-KV factor limit (the merge keeps one lse per split in VGPRs)
 
-template <int HD, int G>
+// U: key groups in flight per wave per iteration; PF: software-pipelined (the next iteration's
+// K/V loads issued before this one's math); NT: non-temporal K/V loads
+template <int HD, int G, int U = 4, int PF = 0, int NT = 0>
 __global__ __launch_bounds__(ATT_THR) void attn_split_kernel(
     const bf16_raw* __restrict__ q, int ldq, const bf16_raw* __restrict__ kc,
     const bf16_raw* __restrict__ vc, const int* __restrict__ slot, const int* __restrict__ pos,
@@ -38,7 +41,6 @@ __global__ __launch_bounds__(ATT_THR) void attn_split_kernel(
   constexpr int LPK = HD / 8;          // lanes per key row (8 bf16 = 16 B per lane)
   constexpr int KPW = LSA_WAVE / LPK;  // keys per wave-instruction
   constexpr int KPI = KPW * ATT_WAVES; // keys per workgroup iteration
-  constexpr int U = 4;                 // iterations in flight per wave
 
   __shared__ float s_m[ATT_WAVES][G];
   __shared__ float s_l[ATT_WAVES][G];
@@ -125,18 +127,33 @@ __global__ __launch_bounds__(ATT_THR) void attn_split_kernel(
     for (int j = 0; j < 8; ++j) o[r][j] = 0.f;
   }
 
-  // loop bound is wave-uniform (the 16-lane key groups of a wave shuffle only internally)
-  for (int base = k0 + w * KPW; base < k1; base += KPI * U) {
-    u32x4_t kr[U], vr[U];
-    bool valid[U];
+  auto load = [&](int base_, u32x4_t (&kr_)[U], u32x4_t (&vr_)[U]) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int key = base + grp + u * KPI;
-      valid[u] = key < k1;
-      const int kk = valid[u] ? key : k0;
-      kr[u] = ld16(kb + (size_t)kk * HD);
-      vr[u] = ld16(vb + (size_t)kk * HD);
+      const int key = base_ + grp + u * KPI;
+      const int kk = key < k1 ? key : k0;
+      if (NT) {
+        kr_[u] = ld16_nt(kb + (size_t)kk * HD);
+        vr_[u] = ld16_nt(vb + (size_t)kk * HD);
+      } else {
+        kr_[u] = ld16(kb + (size_t)kk * HD);
+        vr_[u] = ld16(vb + (size_t)kk * HD);
+      }
     }
+  };
+  u32x4_t kr[U], vr[U];
+  if (PF && k0 + w * KPW < k1) load(k0 + w * KPW, kr, vr);
+  // loop bound is wave-uniform (the 16-lane key groups of a wave shuffle only internally)
+  for (int base = k0 + w * KPW; base < k1; base += KPI * U) {
+    u32x4_t kn[U], vn[U];
+    if (PF) {
+      if (base + KPI * U < k1) load(base + KPI * U, kn, vn);
+    } else {
+      load(base, kr, vr);
+    }
+    bool valid[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) valid[u] = base + grp + u * KPI < k1;
     float s[G][U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -171,6 +188,13 @@ __global__ __launch_bounds__(ATT_THR) void attn_split_kernel(
         unpack8(vr[u], vf);
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[r][j] += p * vf[j];
+      }
+    }
+    if (PF) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        kr[u] = kn[u];
+        vr[u] = vn[u];
       }
     }
   }
@@ -225,16 +249,38 @@ __global__ __launch_bounds__(ATT_THR) void attn_split_kernel(
   if (nact > 1) arrive();
 }
 
+int g_attn_variant = 0;  // probe knob (scripts/attn_probe.py): 0 = default (U=4, NT), else U*100 + PF*10 + NT
+
+template <int HD, int G, int U, int PF, int NT>
+int launch_split_v(const bf16_raw* q, int ldq, const bf16_raw* kc, const bf16_raw* vc, const int* slot,
+                   const int* pos, const int* kv_len, int rows, int n_heads, int n_kv, int t_max,
+                   float scale_log2, int nsplit, int min_chunk, float* po, float* pl, bf16_raw* out,
+                   int ldo, unsigned* cnt, hipStream_t s) {
+  dim3 grid(nsplit, n_kv, rows);
+  attn_split_kernel<HD, G, U, PF, NT><<<grid, ATT_THR, 0, s>>>(q, ldq, kc, vc, slot, pos, kv_len, n_heads, n_kv,
+                                                               t_max, scale_log2, nsplit, min_chunk, po, pl, out, ldo, cnt);
+  LSA_CHECK_LAUNCH();
+  return LSA_OK;
+}
+
 template <int HD, int G>
 int launch_split(const bf16_raw* q, int ldq, const bf16_raw* kc, const bf16_raw* vc, const int* slot,
                  const int* pos, const int* kv_len, int rows, int n_heads, int n_kv, int t_max,
                  float scale_log2, int nsplit, int min_chunk, float* po, float* pl, bf16_raw* out,
                  int ldo, unsigned* cnt, hipStream_t s) {
-  dim3 grid(nsplit, n_kv, rows);
-  attn_split_kernel<HD, G><<<grid, ATT_THR, 0, s>>>(q, ldq, kc, vc, slot, pos, kv_len, n_heads, n_kv,
-                                                     t_max, scale_log2, nsplit, min_chunk, po, pl, out, ldo, cnt);
-  LSA_CHECK_LAUNCH();
-  return LSA_OK;
+  if (HD == 128 && G == 1 && g_attn_variant) {
+#define LSA_V(UU, P, N)                                                                                    \
+  if (g_attn_variant == UU * 100 + P * 10 + N)                                                           \
+    return launch_split_v<HD, G, UU, P, N>(q, ldq, kc, vc, slot, pos, kv_len, rows, n_heads, n_kv, t_max, \
+                                           scale_log2, nsplit, min_chunk, po, pl, out, ldo, cnt, s);
+    LSA_V(2, 0, 0) LSA_V(2, 1, 0) LSA_V(4, 0, 0) LSA_V(4, 1, 0) LSA_V(4, 1, 1) LSA_V(8, 0, 0) LSA_V(8, 0, 1)
+    LSA_V(8, 1, 0) LSA_V(6, 0, 0)
+#undef LSA_V
+  }
+  // default: U = 4 groups in flight, non-temporal K/V loads (each cache line is read once per
+  // step; 512 x 143-token 7B decode: 5.95 -> 6.79 TB/s, profiles/r2_attn_decode_variants.jsonl)
+  return launch_split_v<HD, G, 4, 0, 1>(q, ldq, kc, vc, slot, pos, kv_len, rows, n_heads, n_kv, t_max, scale_log2,
+                                        nsplit, min_chunk, po, pl, out, ldo, cnt, s);
 }
 
 template <int HD>
@@ -252,6 +298,11 @@ int dispatch_g(int g, const bf16_raw* q, int ldq, const bf16_raw* kc, const bf16
 }
 
 }  // namespace
+
+extern "C" int lsa_attn_set_variant(int v) {
+  g_attn_variant = v;
+  return LSA_OK;
+}
 
 extern "C" int lsa_attn_decode(const void* q, int ldq, const void* k_cache, const void* v_cache,
                                const int* slot, const int* pos, const int* kv_len, int rows,

@@ -2,6 +2,7 @@
 // (cdna_hip_programming.md Guideline 13):
 //   lsa_embed        nn.Embedding row gather (reference node_worker.py:215,302)
 //   lsa_rmsnorm      standalone RMSNorm (prefill path; decode fuses it into the GEMV)
+//   lsa_resid_rmsnorm_partials  residual add of split-K GEMM partials + the next RMSNorm
 //   lsa_layernorm    LayerNorm with bias (GPT-2 ln_1 / ln_2 / ln_f), optionally fused with the
 //                    learned absolute position embedding add (x += wpe[pos], written back)
 //   lsa_argmax_finalize  decode the fused-argmax keys -> token ids, reset the keys, append to
@@ -89,6 +90,78 @@ __global__ __launch_bounds__(256) void rmsnorm_reg_kernel(const bf16_raw* __rest
     float f[8], g[8] = {1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
     unpack8(v[j], f);
     if (w) unpack8(wv[j], g);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) f[k] = f[k] * rs * g[k];
+    st16(orow + (tid + j * 256) * 8, pack8(f));
+  }
+}
+
+// Residual add of split-K GEMM partials fused with the next RMSNorm (gemm_sk EPI_PARTIAL):
+//   h[row] = bf16(h[row] + (P[0][row] + ... + P[S-1][row]))   (fixed order: reproducible)
+//   out[row] = rmsnorm(h[row]) * w                              (skipped when out == nullptr)
+// The o / down projections of a >128-row forward end in a residual add that is always followed
+// by an RMSNorm (post-attention norm, next layer's input norm or the final norm): summing their
+// K-split partials here replaces the GEMM's slab + ticket + last-arriver fixup tail. H = 2048 * NC,
+// register-resident: every lane issues all its loads before the first use.
+template <int NC>
+__global__ __launch_bounds__(256) void resid_norm_partials_kernel(bf16_raw* __restrict__ h, int ldh,
+                                                                  const float* __restrict__ P, int S,
+                                                                  long long pstride, int ldp,
+                                                                  const bf16_raw* __restrict__ w, float eps,
+                                                                  bf16_raw* __restrict__ out, int ldo) {
+  constexpr int H = 2048 * NC;
+  __shared__ float s_part[4];
+  const int row = blockIdx.x, tid = threadIdx.x;
+  bf16_raw* hr = h + (size_t)row * ldh;
+  const float* pr = P + (size_t)row * ldp;
+  u32x4_t hv[NC];
+#pragma unroll
+  for (int j = 0; j < NC; ++j) hv[j] = ld16(hr + (tid + j * 256) * 8);
+  float acc[NC][8];
+#pragma unroll
+  for (int j = 0; j < NC; ++j)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[j][k] = 0.f;
+  for (int s = 0; s < S; ++s) {
+    const float* ps = pr + (size_t)s * pstride;
+    f32x4_t a[NC][2];
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      a[j][0] = *reinterpret_cast<const f32x4_t*>(ps + (tid + j * 256) * 8);
+      a[j][1] = *reinterpret_cast<const f32x4_t*>(ps + (tid + j * 256) * 8 + 4);
+    }
+#pragma unroll
+    for (int j = 0; j < NC; ++j)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        acc[j][k] += a[j][0][k];
+        acc[j][4 + k] += a[j][1][k];
+      }
+  }
+  float ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < NC; ++j) {
+    float f[8];
+    unpack8(hv[j], f);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) f[k] += acc[j][k];
+    hv[j] = pack8(f);
+    st16(hr + (tid + j * 256) * 8, hv[j]);
+    unpack8(hv[j], f);  // the norm sees the rounded residual, as after EPI_RESID
+#pragma unroll
+    for (int k = 0; k < 8; ++k) ss += f[k] * f[k];
+  }
+  if (!out) return;
+  ss = wave_sum(ss);
+  if ((tid & 63) == 0) s_part[tid >> 6] = ss;
+  __syncthreads();
+  const float rs = rsqrtf((s_part[0] + s_part[1] + s_part[2] + s_part[3]) / (float)H + eps);
+  bf16_raw* orow = out + (size_t)row * ldo;
+#pragma unroll
+  for (int j = 0; j < NC; ++j) {
+    float f[8], g[8] = {1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
+    unpack8(hv[j], f);
+    if (w) unpack8(ld16(w + (tid + j * 256) * 8), g);
 #pragma unroll
     for (int k = 0; k < 8; ++k) f[k] = f[k] * rs * g[k];
     st16(orow + (tid + j * 256) * 8, pack8(f));
@@ -196,6 +269,25 @@ extern "C" int lsa_rmsnorm(const void* x, int ldx, const void* w, int rows, int 
     case 8192: rmsnorm_reg_kernel<4><<<rows, 256, 0, stream>>>(xb, ldx, wb, eps, ob, ldo); break;
     default:
       rmsnorm_kernel<<<rows, 256, 0, stream>>>(xb, ldx, wb, H, eps, ob, ldo);
+  }
+  LSA_CHECK_LAUNCH();
+  return LSA_OK;
+}
+
+extern "C" int lsa_resid_rmsnorm_partials(void* h, int ldh, const float* partials, int S, long long pstride,
+                                          int ldp, const void* w, int rows, int H, float eps, void* out, int ldo,
+                                          hipStream_t stream) {
+  if (rows < 1 || S < 1 || ldh % 8 || ldp % 8 || (out && ldo % 8) || pstride < (long long)rows * ldp)
+    return LSA_BAD_SHAPE;
+  bf16_raw* hb = static_cast<bf16_raw*>(h);
+  const bf16_raw* wb = static_cast<const bf16_raw*>(w);
+  bf16_raw* ob = static_cast<bf16_raw*>(out);
+  switch (H) {
+    case 2048: resid_norm_partials_kernel<1><<<rows, 256, 0, stream>>>(hb, ldh, partials, S, pstride, ldp, wb, eps, ob, ldo); break;
+    case 4096: resid_norm_partials_kernel<2><<<rows, 256, 0, stream>>>(hb, ldh, partials, S, pstride, ldp, wb, eps, ob, ldo); break;
+    case 6144: resid_norm_partials_kernel<3><<<rows, 256, 0, stream>>>(hb, ldh, partials, S, pstride, ldp, wb, eps, ob, ldo); break;
+    case 8192: resid_norm_partials_kernel<4><<<rows, 256, 0, stream>>>(hb, ldh, partials, S, pstride, ldp, wb, eps, ob, ldo); break;
+    default: return LSA_UNSUPPORTED;
   }
   LSA_CHECK_LAUNCH();
   return LSA_OK;

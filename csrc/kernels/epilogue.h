@@ -15,7 +15,10 @@
 #pragma once
 #include "common.h"
 
-enum EpiMode { EPI_STORE = 0, EPI_RESID = 1, EPI_SWIGLU = 2, EPI_QKV = 3, EPI_ARGMAX = 4 };
+// EPI_PARTIAL (gemm_sk only): every K-split workgroup stores its fp32 partial tile to
+// ((float*)out)[split][M][ldo]; the following norm kernel adds the partials to the residual
+// stream (lsa_resid_rmsnorm_partials) instead of an in-GEMM fixup.
+enum EpiMode { EPI_STORE = 0, EPI_RESID = 1, EPI_SWIGLU = 2, EPI_QKV = 3, EPI_ARGMAX = 4, EPI_PARTIAL = 5 };
 
 // Mirrored by llm_sharding_amd/ops/hip.py::EpiArgs (ctypes) - keep field order in sync.
 struct EpiArgs {

@@ -353,7 +353,7 @@ struct Kern {
   }
 
   // ---- fused epilogue through an LDS transpose -------------------------------------------------
-  LSA_DEVICE void epilogue(const EpiArgs& ep, const f32x4_t (&acc)[FM][FN], int mt, int nt) {
+  LSA_DEVICE void epilogue(const EpiArgs& ep, const f32x4_t (&acc)[FM][FN], int mt, int nt, int sp) {
     const SkParams& P = *p;
     constexpr int EROWS = G_::EROWS, ELD = G_::ELD, FPP = EROWS / 16;  // rows / fragments per pass
     float* img = reinterpret_cast<float*>(smem) + w * (EROWS * ELD);
@@ -407,7 +407,16 @@ struct Kern {
           float v[16];
 #pragma unroll
           for (int q = 0; q < 4; ++q) *reinterpret_cast<f32x4_t*>(v + 4 * q) = *reinterpret_cast<const f32x4_t*>(src + 4 * q);
-          if (m < P.M && (BN != 192 || col_base + j * 16 < P.N)) epi_row16<EPI>(ep, m, col_base + j * 16, v);
+          if (m < P.M && (BN != 192 || col_base + j * 16 < P.N)) {
+            if (EPI == EPI_PARTIAL) {  // fp32 partial of K range sp: 4 x 16-B stores
+              float* o = reinterpret_cast<float*>(ep.out) + ((size_t)sp * P.M + m) * ep.ldo + col_base + j * 16;
+#pragma unroll
+              for (int q = 0; q < 4; ++q)
+                st16(reinterpret_cast<bf16_raw*>(o + 4 * q), __builtin_bit_cast(u32x4_t, *reinterpret_cast<const f32x4_t*>(v + 4 * q)));
+            } else {
+              epi_row16<EPI>(ep, m, col_base + j * 16, v);
+            }
+          }
           __builtin_amdgcn_sched_barrier(0);
         }
       }
@@ -468,7 +477,7 @@ __global__ __launch_bounds__(NTHR) void gemm_sk_kernel(const bf16_raw* __restric
     if (j < (x < rr ? q + 1 : q)) su = (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + j;
   }
   for (;;) {
-    int tile, ts = 0, ka = 0, kb = prm.NKT;
+    int tile, ts = 0, ka = 0, kb = prm.NKT, sp = 0;
     bool sk = false;
     if (r < prm.dp_rounds) {
       tile = r * G + g;
@@ -476,7 +485,7 @@ __global__ __launch_bounds__(NTHR) void gemm_sk_kernel(const bf16_raw* __restric
     } else if (prm.split) {
       if (split_done || su < 0) break;
       ts = su % prm.sk_tiles;
-      const int sp = su / prm.sk_tiles;
+      sp = su / prm.sk_tiles;
       ka = sp * prm.NKT / prm.split;
       kb = (sp + 1) * prm.NKT / prm.split;
       tile = prm.dp_rounds * G + ts;
@@ -498,7 +507,7 @@ __global__ __launch_bounds__(NTHR) void gemm_sk_kernel(const bf16_raw* __restric
     k.run_segment(acc, mt, nt, ka, kb);
     LSA_STAMP(k.stamp_base + 2);
     bool do_epi = true;
-    if (partial) {
+    if (partial && EPI != EPI_PARTIAL) {
       // contributors of this tile, in K order: split mode - workgroups ts + s * sk_tiles
       // (slot 0); stream-K - the workgroups whose iteration ranges intersect the tile's
       const long long t0 = (long long)ts * prm.NKT, t1 = t0 + prm.NKT;
@@ -536,7 +545,7 @@ __global__ __launch_bounds__(NTHR) void gemm_sk_kernel(const bf16_raw* __restric
       }
     }
     LSA_STAMP(k.stamp_base + 4);
-    if (do_epi) k.epilogue(ep, acc, mt, nt);
+    if (do_epi) k.epilogue(ep, acc, mt, nt, sp);
     LSA_STAMP(k.stamp_base + 5);
     k.stamp_base = k.stamp_base + 6 < 30 ? k.stamp_base + 6 : 24;
     __syncthreads();
@@ -557,6 +566,8 @@ int launch(const bf16_raw* A, const bf16_raw* W, const SkParams& prm, const EpiA
 // bn: tile width 256 / 192 (2-buffer DMA ring; 192: N % 16 == 0, partial last tile) or 128 (nb = 2
 // or 3 buffers; 0 = 3); grid: workgroups
 // (<= 1024); dp: 1 = whole tiles in data-parallel rounds first (0 = all tiles are remainder);
+// epi EPI_PARTIAL: every tile split into exactly `split` K ranges (tiles * split <= grid), fp32
+// partial k stored to ((float*)ep->out)[k][M][ldo], no slabs or tickets (lsa_resid_rmsnorm_partials sums them);
 // split: 0 = remainder by stream-K, S >= 1 = remainder tiles split into up to S K ranges
 // (clamped to NKT and to grid / remainder tiles; stream-K when the remainder exceeds the grid); slab: >= 2 * grid * 256 * bn floats and counters: >= remainder tiles (zeroed) when
 // any tile is split. Returns LSA_BAD_SHAPE on any shape the kernel's indexing cannot take.
@@ -572,6 +583,7 @@ extern "C" int lsa_gemm_sk(const void* a, int lda, const void* wp, int M, int N,
   if (epi == EPI_RESID && !ep->resid) return LSA_BAD_SHAPE;
   if (epi == EPI_QKV && (!ep->k_cache || !ep->v_cache || !ep->slot || !ep->pos)) return LSA_BAD_SHAPE;
   if (!ep->out) return LSA_BAD_SHAPE;
+  if (epi == EPI_PARTIAL && (split < 1 || ep->ldo < N || ep->ldo % 4)) return LSA_BAD_SHAPE;
   SkParams prm;
   prm.M = M;
   prm.N = N;
@@ -588,7 +600,15 @@ extern "C" int lsa_gemm_sk(const void* a, int lda, const void* wp, int M, int N,
   prm.dp_rounds = dp ? (int)(tiles / prm.G) : 0;
   prm.sk_tiles = (int)(tiles - (long long)prm.dp_rounds * prm.G);
   prm.split = 0;
-  if (split > 0 && prm.sk_tiles > 0 && prm.sk_tiles <= prm.G) {
+  if (epi == EPI_PARTIAL) {
+    // every tile split into exactly `split` K ranges, one workgroup each, partial k written to
+    // out[k]: the consumer sums exactly `split` partials, so nothing may be clamped here
+    if (split > prm.NKT || tiles * split > grid) return LSA_BAD_SHAPE;
+    prm.G = grid;
+    prm.dp_rounds = 0;
+    prm.sk_tiles = (int)tiles;
+    prm.split = split;
+  } else if (split > 0 && prm.sk_tiles > 0 && prm.sk_tiles <= prm.G) {
     // at most NKT ranges per tile and sk_tiles * split <= G workgroups
     prm.split = split < prm.NKT ? split : prm.NKT;
     if (prm.split > prm.G / prm.sk_tiles) prm.split = prm.G / prm.sk_tiles;
@@ -600,7 +620,8 @@ extern "C" int lsa_gemm_sk(const void* a, int lda, const void* wp, int M, int N,
       prm.G = prm.sk_tiles * prm.NKT;  // every workgroup gets >= 1 iteration
     }
   }
-  if (prm.sk_tiles > 0 && (!slab || !counters || slab_floats < 2LL * prm.G * BM * bn || n_counters < prm.sk_tiles))
+  if (epi != EPI_PARTIAL && prm.sk_tiles > 0 &&
+      (!slab || !counters || slab_floats < 2LL * prm.G * BM * bn || n_counters < prm.sk_tiles))
     return LSA_BAD_SHAPE;
   const bf16_raw* A = static_cast<const bf16_raw*>(a);
   const bf16_raw* W = static_cast<const bf16_raw*>(wp);
@@ -613,6 +634,7 @@ extern "C" int lsa_gemm_sk(const void* a, int lda, const void* wp, int M, int N,
     case EPI_RESID: return LSA_G(EPI_RESID);
     case EPI_QKV: return LSA_G(EPI_QKV);
     case EPI_SWIGLU: return LSA_G(EPI_SWIGLU);
+    case EPI_PARTIAL: return LSA_G(EPI_PARTIAL);
     default: return LSA_UNSUPPORTED;
   }
 #undef LSA_G

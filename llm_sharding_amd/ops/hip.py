@@ -14,6 +14,7 @@ from __future__ import annotations
 import ctypes
 import json
 import os
+from contextlib import contextmanager
 from typing import Optional
 
 import torch
@@ -21,7 +22,7 @@ import torch
 NATIVE_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_native")
 KERNELS_SO = os.path.join(NATIVE_DIR, "liblsa_kernels.so")
 
-EPI_STORE, EPI_RESID, EPI_SWIGLU, EPI_QKV, EPI_ARGMAX = range(5)
+EPI_STORE, EPI_RESID, EPI_SWIGLU, EPI_QKV, EPI_ARGMAX, EPI_PARTIAL = range(6)
 _STATUS = {0: "ok", 1: "bad shape", 2: "unsupported", 3: "launch failed"}
 
 
@@ -65,12 +66,14 @@ def lib() -> ctypes.CDLL:
     L.lsa_embed.argtypes = [vp, i, vp, i, vp, i, vp]
     L.lsa_rmsnorm.argtypes = [vp, i, vp, i, i, f, vp, i, vp]
     L.lsa_layernorm.argtypes = [vp, i, vp, vp, vp, vp, i, i, f, vp, i, vp]
+    L.lsa_resid_rmsnorm_partials.argtypes = [vp, i, vp, i, ctypes.c_longlong, i, vp, i, i, f, vp, i, vp]
     L.lsa_argmax_finalize.argtypes = [vp, i, vp, vp, i, vp, i, i, vp, vp]
     L.lsa_pos_advance.argtypes = [vp, i, i, vp]
     L.lsa_gemm_sk.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(EpiArgs), i, i, i, i, i, i, vp, vp, ctypes.c_longlong, i,
                               vp]
     for name in ("lsa_gemv", "lsa_gemv_coop", "lsa_gemv_fp8", "lsa_dequant_fp8_packed", "lsa_gemv_coop_fp8", "lsa_gemm",
                  "lsa_gemm_sk", "lsa_attn_decode", "lsa_attn_prefill", "lsa_embed", "lsa_rmsnorm", "lsa_layernorm",
+                 "lsa_resid_rmsnorm_partials",
                  "lsa_argmax_finalize", "lsa_pos_advance", "lsa_version"):
         getattr(L, name).restype = ctypes.c_int
     _lib = L
@@ -346,18 +349,32 @@ N_CU = 256
 
 SK_TUNING_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_sk_tuning.json")
 _SK_TUNED = None
+_SK_PARTIAL = None
+
+
+def _sk_load() -> None:
+    global _SK_TUNED, _SK_PARTIAL
+    _SK_TUNED, _SK_PARTIAL = {}, {}
+    if os.path.exists(SK_TUNING_FILE):
+        with open(SK_TUNING_FILE) as f:
+            for e in json.load(f).get("entries", []):
+                _SK_TUNED.setdefault((e["N"], e["K"]), []).append((e["M"], tuple(e["cfg"])))
+                if "partial" in e:  # measured on a residual projection: [bn, split] or null
+                    _SK_PARTIAL.setdefault((e["N"], e["K"]), []).append((e["M"], e["partial"]))
 
 
 def _sk_tuned() -> dict:
     """(N, K) -> [(M, (bn, grid, dp, split)), ...] from scripts/tune_gemm_sk.py's measurements."""
-    global _SK_TUNED
     if _SK_TUNED is None:
-        _SK_TUNED = {}
-        if os.path.exists(SK_TUNING_FILE):
-            with open(SK_TUNING_FILE) as f:
-                for e in json.load(f).get("entries", []):
-                    _SK_TUNED.setdefault((e["N"], e["K"]), []).append((e["M"], tuple(e["cfg"])))
+        _sk_load()
     return _SK_TUNED
+
+
+def _sk_partial() -> dict:
+    """(N, K) -> [(M, [bn, split] | None), ...]: residual projections measured both ways."""
+    if _SK_PARTIAL is None:
+        _sk_load()
+    return _SK_PARTIAL
 
 
 def gemm_sk_plan(M: int, N: int, K: int, tuned: bool = True) -> tuple:
@@ -410,7 +427,9 @@ def gemm_sk(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int,
          "gemm_sk: A must be [>=M, >=K] row-major with 16-B aligned rows")
     _req(a.data_ptr() % 16 == 0, "gemm_sk: A must be 16-byte aligned")
     _check_epi(epi, ep, N)
-    _req(epi in (EPI_STORE, EPI_RESID, EPI_SWIGLU, EPI_QKV), f"gemm_sk: epilogue {epi} not supported")
+    _req(epi in (EPI_STORE, EPI_RESID, EPI_SWIGLU, EPI_QKV, EPI_PARTIAL), f"gemm_sk: epilogue {epi} not supported")
+    if epi == EPI_PARTIAL:  # exactly `split` K ranges per tile, every tile in one round
+        _req(bn in (128, 192, 256) and split >= 1 and grid >= 1, "gemm_sk partial: explicit bn, grid and split required")
     pb, pg, pd, ps = gemm_sk_plan(M, N, K)
     if not bn:
         bn, grid, split = pb, grid or pg, ps if split < 0 else split
@@ -520,6 +539,54 @@ def embed(ids: torch.Tensor, table: torch.Tensor, out: torch.Tensor, rows: Optio
     _req(_is_bf16_cuda(table, out) and out.shape[1] >= table.shape[1], "embed: shapes")
     rc = lib().lsa_embed(_p(ids), rows, _p(table), table.shape[1], _p(out), out.stride(0), _stream())
     _check(rc, "lsa_embed")
+
+
+def resid_rmsnorm_partials(h: torch.Tensor, partials: torch.Tensor, S: int, rows: int, eps: float,
+                           out: Optional[torch.Tensor] = None, w: Optional[torch.Tensor] = None) -> None:
+    """h[:rows] = bf16(h + sum_s partials[s]) (fixed order), then ``out`` = rmsnorm(h) [* w]
+    (no norm when ``out`` is None). ``partials``: fp32 [S_alloc, >= rows, H] written by
+    ``gemm_sk(..., EPI_PARTIAL, split=S)`` with ldo = H (elementwise.hip)."""
+    H = h.shape[1]
+    _req(_is_bf16_cuda(h, w, out) and partials.dtype == torch.float32 and partials.is_cuda, "resid_rmsnorm_partials: dtypes")
+    _req(partials.dim() == 3 and partials.shape[0] >= S and partials.shape[2] == H and partials.is_contiguous()
+         and partials.shape[1] >= rows, "resid_rmsnorm_partials: partials must be [>=S, >=rows, H] contiguous")
+    # the GEMM wrote partial k at k * rows * H (its M = rows), not at the allocation's stride
+    rc = lib().lsa_resid_rmsnorm_partials(_p(h), h.stride(0), _p(partials), S, rows * H, H, _p(w), rows, H, float(eps),
+                                          _p(out), 0 if out is None else out.stride(0), _stream())
+    _check(rc, "lsa_resid_rmsnorm_partials")
+
+
+def gemm_sk_partial_plan(M: int, N: int, K: int) -> Optional[tuple]:
+    """(bn, split) for a residual projection run as EPI_PARTIAL + resid_rmsnorm_partials, or
+    None when the fused EPI_RESID plan is better. Tuned shapes carry a measured ``partial``
+    entry (scripts/tune_gemm_sk.py); otherwise None (no partials above PARTIAL_MAX_ROWS)."""
+    if M > PARTIAL_MAX_ROWS:
+        return None
+    if _PARTIAL_FORCE is not None:  # force_partial_plan(): tests pin the mode
+        return None if _PARTIAL_FORCE is False else _PARTIAL_FORCE
+    mt = -(-M // SK_BM)
+    cands = [(abs(m - M), pp) for m, pp in _sk_partial().get((N, K), ()) if -(-m // SK_BM) == mt]
+    if not cands:
+        return None
+    pp = min(cands)[1]
+    return None if pp is None else tuple(pp)
+
+
+PARTIAL_MAX_ROWS = 1024   # rows of the engine's split-K partial buffer
+PARTIAL_MAX_SPLIT = 8
+_PARTIAL_FORCE = None
+
+
+@contextmanager
+def force_partial_plan(plan):
+    """Within the block every residual projection of <= PARTIAL_MAX_ROWS rows uses ``plan``
+    ((bn, split), or False for the fused EPI_RESID path) instead of the tuning table."""
+    global _PARTIAL_FORCE
+    prev, _PARTIAL_FORCE = _PARTIAL_FORCE, plan
+    try:
+        yield
+    finally:
+        _PARTIAL_FORCE = prev
 
 
 def rmsnorm(x: torch.Tensor, w: Optional[torch.Tensor], out: torch.Tensor, rows: int, eps: float,

@@ -174,7 +174,7 @@ def scratch_bytes(cfg: LlamaConfig, rows: int, sets: int = 1, max_seq: int = 409
     """Device bytes a stage engine allocates besides weights and KV cache, per ``sets``
     concurrently replayed scratch sets sized for ``rows`` rows - the same formulas as
     StageEngine._alloc_runtime / decode_scratch: activations, attention split partials and
-    their tickets, the coop-GEMV workspace and the gemm_sk slabs (> 128 rows)."""
+    their tickets, the coop-GEMV workspace, the gemm_sk slabs and split-K partials (> 128 rows)."""
     from ..ops import packing
     H, I, nh, hd = cfg.hidden_size, cfg.intermediate_size, cfg.num_attention_heads, cfg.head_dim
     dmr = packing.GEMV_MAX_ROWS
@@ -190,7 +190,9 @@ def scratch_bytes(cfg: LlamaConfig, rows: int, sets: int = 1, max_seq: int = 409
     floats, groups = packing.coop_workspace_need(shapes, dmr, even_n=even)
     coop = max(floats, 1 << 24) * 4 + max(groups, 4096) * 4
     sk = (2 * 256 * 256 * 256 * 4 + 4 * 256 * 4) if R > dmr else 0
-    return float(sets * (act + attn + coop + sk))
+    # split-K partials of the residual projections (hip.PARTIAL_MAX_SPLIT x <= 1024 rows x H fp32)
+    part = 8 * min(R, 1024) * H * 4 if (R > dmr and not cfg.is_gpt2) else 0
+    return float(sets * (act + attn + coop + sk + part))
 
 
 def stage_memory(cfg: LlamaConfig, n_layers: int, *, slots: int, max_seq: int, prefill_rows: int,

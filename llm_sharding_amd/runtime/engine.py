@@ -362,13 +362,24 @@ class StageEngine:
             self.coop_ws = hip.CoopWorkspace(dev, slab_floats=max(floats, 1 << 24), groups=max(groups, 4096))
             # stream-K / split-K partial slabs + tickets of the > 128-row GEMM (gemm_sk.hip)
             self.sk_ws = hip.SkWorkspace(dev) if R > self.DECODE_MAX_ROWS else None
+            # split-K partials of the residual projections (gemm_sk EPI_PARTIAL), summed by the
+            # following norm kernel, for >128-row forwards of up to PARTIAL_MAX_ROWS rows
+            self.part_k = self._alloc_part_k(R)
             self.w_scratch = None
             if self.fp8:  # one projection's bf16 weights, for the >64-row paths
                 self.w_scratch = torch.empty(max(n * k for n, k in shapes), dtype=torch.bfloat16, device=dev)
 
+    def _alloc_part_k(self, R: int):
+        from ..ops import hip
+        if R <= self.DECODE_MAX_ROWS or self.cfg.is_gpt2:
+            return None
+        rows = min(R, hip.PARTIAL_MAX_ROWS)
+        return torch.empty((hip.PARTIAL_MAX_SPLIT, rows, self.cfg.hidden_size), dtype=torch.float32,
+                           device=self.device)
+
     # buffers a forward pass writes besides the KV cache: one set per concurrently running graph
     SCRATCH_ATTRS = ("buf_h", "buf_xn", "buf_q", "buf_attn", "buf_act", "part_o", "part_lse", "attn_cnt",
-                     "coop_ws", "sk_ws", "w_scratch", "keys", "tokens", "ws_rows")
+                     "coop_ws", "sk_ws", "part_k", "w_scratch", "keys", "tokens", "ws_rows")
 
     def decode_scratch(self, k: int, rows: Optional[int] = None) -> dict:
         """Scratch set ``k`` for forward passes that run CONCURRENTLY on different streams (a
@@ -398,6 +409,7 @@ class StageEngine:
                 "coop_ws": hip.CoopWorkspace(dev, slab_floats=self.coop_ws.slab.numel(),
                                              groups=self.coop_ws.counters.numel()),
                 "sk_ws": hip.SkWorkspace(dev) if R > self.DECODE_MAX_ROWS else None,
+                "part_k": self._alloc_part_k(R),
                 "w_scratch": None if self.w_scratch is None else torch.empty_like(self.w_scratch),
                 "keys": torch.zeros(R, dtype=torch.int64, device=dev),
                 "tokens": torch.zeros(R, dtype=torch.int32, device=dev),
@@ -628,6 +640,22 @@ class StageEngine:
         def pre(x, w, s, N, K, epi, ep):
             hip.gemm(x, wbf(w, s, N, K), rows, N, K, epi, ep, ws=ws, sk_ws=self.sk_ws)
 
+        # residual projections as split-K partials summed by the next norm kernel, where measured
+        # faster than the fused residual epilogue (ops/gemm_sk_tuning.json "partial" entries)
+        part_ok = not decode and self.part_k is not None and rows <= self.part_k.shape[1]
+
+        def resid_proj(x, w, s, N, K, ep):
+            # returns the split count of partials left in part_k (0: residual applied in-GEMM)
+            pp = hip.gemm_sk_partial_plan(rows, N, K) if part_ok else None
+            if pp is None:
+                pre(x, w, s, N, K, hip.EPI_RESID, ep)
+                return 0
+            bn, sp = pp
+            hip.gemm_sk(x, wbf(w, s, N, K), rows, N, K, hip.EPI_PARTIAL, hip.make_epi(out=self.part_k, ldo=N),
+                        bn=bn, grid=hip.N_CU, dp=0, split=sp, ws=self.sk_ws)
+            return sp
+
+        pending = 0  # down-projection partials not yet added to hbuf
         for li, lw in enumerate(self.layers):
             kc, vc = self.k_cache[li], self.v_cache[li]
             ep_qkv = hip.make_epi(out=q, k_cache=kc, v_cache=vc, slot=slot, pos=pos, cos=self.cos, sin=self.sin,
@@ -635,7 +663,11 @@ class StageEngine:
             if decode:
                 dec(hbuf, lw.qkv, lw.qkv_s, cfg.qkv_size, H, hip.EPI_QKV, ep_qkv, norm=True)
             else:
-                hip.rmsnorm(hbuf, None, xn, rows, eps, H)
+                if pending:
+                    hip.resid_rmsnorm_partials(hbuf, self.part_k, pending, rows, eps, out=xn)
+                    pending = 0
+                else:
+                    hip.rmsnorm(hbuf, None, xn, rows, eps, H)
                 pre(xn, lw.qkv, lw.qkv_s, cfg.qkv_size, H, hip.EPI_QKV, ep_qkv)
             if tiles is not None:
                 hip.attn_prefill(q, kc, vc, tiles[1], nh, nkv, hd, attn_o, causal=kv_len is None, tiles_host=tiles[0])
@@ -649,10 +681,15 @@ class StageEngine:
                 dec(hbuf, lw.gate_up, lw.gate_up_s, 2 * I, H, hip.EPI_SWIGLU, ep_gu, norm=True)
                 dec(act, lw.down, lw.down_s, H, I, hip.EPI_RESID, ep_o)
             else:
-                pre(attn_o, lw.o, lw.o_s, H, cfg.q_size, hip.EPI_RESID, ep_o)
-                hip.rmsnorm(hbuf, None, xn, rows, eps, H)
+                sp = resid_proj(attn_o, lw.o, lw.o_s, H, cfg.q_size, ep_o)
+                if sp:
+                    hip.resid_rmsnorm_partials(hbuf, self.part_k, sp, rows, eps, out=xn)
+                else:
+                    hip.rmsnorm(hbuf, None, xn, rows, eps, H)
                 pre(xn, lw.gate_up, lw.gate_up_s, 2 * I, H, hip.EPI_SWIGLU, ep_gu)
-                pre(act, lw.down, lw.down_s, H, I, hip.EPI_RESID, ep_o)
+                pending = resid_proj(act, lw.down, lw.down_s, H, I, ep_o)
+        if pending:  # the stage's output residual stream
+            hip.resid_rmsnorm_partials(hbuf, self.part_k, pending, rows, eps)
         return hbuf
 
     def _forward_hip_gpt2(self, hbuf, slot, pos, kv_len, rows, nsplit, tiles, decode, native_fp8) -> torch.Tensor:

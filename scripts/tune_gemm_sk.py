@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Autotune gemm_sk's work decomposition per projection shape, with the epilogue the engine
 runs (QKV: RoPE + KV append, o/down: residual add, gate_up: SwiGLU), weights rotated over
-> 600 MB of copies so they stream from HBM as in a decode step. Writes the winners to
+> 600 MB of copies so they stream from HBM as in a decode step. Residual projections are also
+timed as split-K partials summed by the following norm (EPI_PARTIAL + resid_rmsnorm_partials)
+against the fused EPI_RESID + rmsnorm pair; the winner goes in the entry's "partial" field. Writes the winners to
 llm_sharding_amd/ops/gemm_sk_tuning.json, which hip.gemm_sk_plan consults before its cost model.
 
 usage: tune_gemm_sk.py [--rows 256,512,...] [--models llama2-7b,...] [--out PATH] [--iters N]
@@ -88,16 +90,49 @@ def main():
                             continue
                         res.append((round(us, 2), bn, sp))
                 res.sort()
+                partial = None
+                if epi == hip.EPI_RESID and M <= hip.PARTIAL_MAX_ROWS:
+                    # the engine follows every residual projection with an RMSNorm: compare
+                    # fused (EPI_RESID + rmsnorm) against EPI_PARTIAL + resid_rmsnorm_partials
+                    xn = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
+                    pbuf = torch.zeros(hip.PARTIAL_MAX_SPLIT, M, N, dtype=torch.float32, device=DEV)
+                    bbn, bsp = res[0][1], res[0][2]
+
+                    def fused(i):
+                        hip.gemm_sk(x, ws[i % nbuf], M, N, K, epi, ep, bn=bbn, grid=hip.N_CU, dp=1, split=bsp, ws=sk_ws)
+                        hip.rmsnorm(out, None, xn, M, 1e-5, N)
+                    t_fused = timeit(fused, a.iters)
+                    pres = []
+                    for bn in (256, 192, 128):
+                        if N % (16 if bn == 192 else bn):
+                            continue
+                        tiles = -(-M // hip.SK_BM) * -(-N // bn)
+                        for sp in range(1, hip.PARTIAL_MAX_SPLIT + 1):
+                            if tiles * sp > hip.N_CU or sp > K // 64:
+                                continue
+                            epp = hip.make_epi(out=pbuf, ldo=N)
+
+                            def part(i):
+                                hip.gemm_sk(x, ws[i % nbuf], M, N, K, hip.EPI_PARTIAL, epp, bn=bn, grid=hip.N_CU, dp=0,
+                                            split=sp, ws=sk_ws)
+                                hip.resid_rmsnorm_partials(out, pbuf, sp, M, 1e-5, out=xn)
+                            pres.append((round(timeit(part, a.iters), 2), bn, sp))
+                    pres.sort()
+                    partial = {"fused_us": round(t_fused, 2), "best": pres[0] if pres else None, "all": pres}
                 plan = hip.gemm_sk_plan(M, N, K, tuned=False)
                 model_us = next((r[0] for r in res if (r[1], r[2]) == (plan[0], plan[3])), None)
                 fl = 2.0 * M * N * K
                 line = {"model": model, "shape": name, "N": N, "K": K, "M": M, "epi": epi,
                         "best_us": res[0][0], "best": [res[0][1], hip.N_CU, 1, res[0][2]],
                         "best_tflops": round(fl / res[0][0] / 1e6, 1), "cost_model_us": model_us,
-                        "all": res}
+                        "all": res, "partial": partial}
                 print(json.dumps(line), flush=True)
                 entries = [e for e in entries if (e["N"], e["K"], e["M"]) != (N, K, M)]
-                entries.append({"N": N, "K": K, "M": M, "cfg": line["best"], "us": res[0][0]})
+                ent = {"N": N, "K": K, "M": M, "cfg": line["best"], "us": res[0][0]}
+                if partial is not None:  # [bn, split] when partials + fused norm beat EPI_RESID + norm
+                    pb = partial["best"]
+                    ent["partial"] = [pb[1], pb[2]] if pb and pb[0] < partial["fused_us"] else None
+                entries.append(ent)
             del ws
             torch.cuda.empty_cache()
     entries.sort(key=lambda e: (e["N"], e["K"], e["M"]))

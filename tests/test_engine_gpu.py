@@ -91,12 +91,22 @@ def test_engine_prefill_then_decode_vs_golden(cfg_fn, S):
             assert got == int(lg.argmax(-1)[0])
 
 
-@pytest.mark.parametrize("rows", [160, 300])
-def test_big_batch_decode_graph_vs_golden(rows):
+@pytest.mark.parametrize("rows,partial", [(160, None), (300, None), (300, False), (300, (128, 2)), (160, (256, 3))])
+def test_big_batch_decode_graph_vs_golden(rows, partial):
     """A decode graph above the 128-row GEMV range (160 / 300 sequences: gemm_sk.hip's stream-K
     and split-K GEMM with fused epilogues, captured in the graph) against the fp32 golden model:
     prefill and decode-step hidden states, and the greedy tokens wherever the top-2 margin is
-    clear."""
+    clear. ``partial``: the residual projections' mode - tuning table (None), fused EPI_RESID
+    (False) or (bn, split) K-split partials summed by resid_rmsnorm_partials."""
+    from llm_sharding_amd.ops import hip
+    if partial is None:
+        _big_batch_vs_golden(rows)
+    else:
+        with hip.force_partial_plan(partial):
+            _big_batch_vs_golden(rows)
+
+
+def _big_batch_vs_golden(rows):
     cfg = _mid_cfg()
     seed, P = 13, 5
     eng = StageEngine(cfg, 0, cfg.num_hidden_layers, DEV, torch.bfloat16, has_embed=True, has_head=True,

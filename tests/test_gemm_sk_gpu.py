@@ -163,3 +163,30 @@ def test_gemm_sk_graph_replay(ws):
         torch.cuda.synchronize()
         assert rel_err(out, first) < 1e-6
     assert rel_err(first, a.float() @ w.float().T) < 8e-3
+
+
+@pytest.mark.parametrize("M,N,K,bn,S", [(512, 4096, 4096, 128, 4), (300, 4096, 1216, 256, 3), (777, 2048, 640, 192, 2),
+                                        (129, 8192, 512, 128, 1), (256, 4096, 11008, 128, 8)])
+def test_gemm_sk_partials_resid_rmsnorm(M, N, K, bn, S, ws):
+    """EPI_PARTIAL (each K range's fp32 partial stored, no in-GEMM fixup) + the fused residual
+    add / RMSNorm kernel that sums them, against fp32 torch."""
+    h = hip()
+    a = _rnd(M, K)
+    w = _rnd(N, K, scale=0.02)
+    r = _rnd(M, N)
+    ref = a.float() @ w.float().T
+    P = torch.full((h.PARTIAL_MAX_SPLIT, M, N), float("nan"), device=DEV)
+    h.gemm_sk(a, packing.pack_b(w), M, N, K, h.EPI_PARTIAL, h.make_epi(out=P, ldo=N), bn=bn, grid=256, dp=0, split=S,
+              ws=ws)
+    assert rel_err(P[:S].sum(0), ref) < 1e-5
+    assert bool(torch.isnan(P[S:]).all())  # nothing beyond the S partials is written
+    hb, xn = r.clone(), torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
+    h.resid_rmsnorm_partials(hb, P, S, M, 1e-5, out=xn)
+    want_h = r.float() + ref
+    assert rel_err(hb, want_h) < 8e-3
+    hf = hb.float()
+    want_xn = hf * torch.rsqrt(hf.pow(2).mean(-1, keepdim=True) + 1e-5)
+    assert rel_err(xn, want_xn) < 8e-3
+    h2 = r.clone()
+    h.resid_rmsnorm_partials(h2, P, S, M, 1e-5)  # residual only (stage output)
+    assert torch.equal(h2, hb)
