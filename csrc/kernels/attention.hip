@@ -83,7 +83,7 @@ __global__ __launch_bounds__(ATT_THR) void attn_split_kernel(
 #pragma unroll
       for (int sp = 0; sp < ATT_MAX_SPLIT; ++sp) {
         if (sp < nact) {
-          const float wgt = exp2f(lse[sp] - mm);
+          const float wgt = __builtin_amdgcn_exp2f(lse[sp] - mm);
           ws += wgt;
           acc += wgt * __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(por, ((hb + sp) * HD + d) * 4, 0, 16));
         }
@@ -175,14 +175,14 @@ __global__ __launch_bounds__(ATT_THR) void attn_split_kernel(
 #pragma unroll
       for (int u = 1; u < U; ++u) bm = fmaxf(bm, s[r][u]);
       const float mn = fmaxf(mx[r], bm);
-      const float alpha = exp2f(mx[r] - mn);
+      const float alpha = __builtin_amdgcn_exp2f(mx[r] - mn);
       mx[r] = mn;
       l[r] *= alpha;
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[r][j] *= alpha;
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const float p = valid[u] ? exp2f(s[r][u] - mn) : 0.f;
+        const float p = valid[u] ? __builtin_amdgcn_exp2f(s[r][u] - mn) : 0.f;
         l[r] += p;
         float vf[8];
         unpack8(vr[u], vf);
@@ -207,7 +207,7 @@ __global__ __launch_bounds__(ATT_THR) void attn_split_kernel(
       const float mo = __shfl_xor(mx[r], off, 64);
       const float lo = __shfl_xor(l[r], off, 64);
       const float mn = fmaxf(mx[r], mo);
-      const float a = exp2f(mx[r] - mn), b = exp2f(mo - mn);
+      const float a = __builtin_amdgcn_exp2f(mx[r] - mn), b = __builtin_amdgcn_exp2f(mo - mn);
       l[r] = l[r] * a + lo * b;
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[r][j] = o[r][j] * a + __shfl_xor(o[r][j], off, 64) * b;
@@ -234,7 +234,7 @@ __global__ __launch_bounds__(ATT_THR) void attn_split_kernel(
     float ls = 0.f, os = 0.f;
 #pragma unroll
     for (int i = 0; i < ATT_WAVES; ++i) {
-      const float a = exp2f(s_m[i][r] - mm);
+      const float a = __builtin_amdgcn_exp2f(s_m[i][r] - mm);
       ls += s_l[i][r] * a;
       os += s_o[i][r][d] * a;
     }

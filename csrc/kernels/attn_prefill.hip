@@ -4,61 +4,85 @@
 // fp32 softmax, GQA by repeat_kv; SURVEY.md §2.3 K7, reference shard_loader.py:57-74 via
 // HF LlamaDecoderLayer) with one kernel that never materialises the score matrix.
 //
-// Work unit: one query tile (<= 64 consecutive positions of ONE sequence, described by the
-// host-built tile table) x one query head; 4 waves, 16 query rows per wave. For every 64-key
-// block the K block is staged row-major (XOR-swizzled 16-B chunks) and the V block
-// transposed (swizzled 8-B key granules) in LDS, then, per wave:
-//   S^T[key][row] = K . Q^T     A = K from LDS, B = Q^T held in registers for the whole tile
-//   online softmax              the C layout gives each lane ONE query row (lane & 15), so the
-//                               running max / sum / rescale are per-lane scalars plus two
-//                               cross-lane max/sum steps (xor 16, xor 32)
-//   O^T[dim][row] += V^T . P^T  B = P^T straight from the S^T accumulators (bf16), using the
-//                               key order k(8g+j) = 16*(j>>2) + 4g + (j&3) inside each 32-key
-//                               fragment, which is exactly what lane group g holds; A = V^T
-//                               from LDS in the same key order (two 8-B reads per fragment).
+// Work unit: one query tile of ONE sequence (host-built tile table) x one KV head's group of
+// HPW query heads (HPW = G = n_heads / n_kv when it divides 8, else 1): 8 waves, each owning
+// 16 query rows of one head (positions (w / HPW) * 16 ..), so a tile holds 128 / HPW
+// positions and every staged K/V block serves the whole GQA group (no re-staging per head).
+// Per 64-key block:
+//   * K and V arrive by LDS-DMA (global_load_lds, 16 B/lane) into a double-buffered ring,
+//     block kb+1 in flight while block kb is computed; one barrier per block. The swizzle is
+//     applied on the SOURCE address, so each 1 KiB piece lands lane-linear.
+//   * S^T[key][row] = K . Q^T   A = K rows (ds_read_b128, XOR-swizzled rows: conflict-free),
+//                               B = Q^T held in registers for the whole tile
+//   * online softmax            each lane holds ONE query row's scores (lane & 15): running
+//                               max / sum are per-lane scalars + two cross-lane steps
+//   * O^T[dim][row] += V^T . P^T  B = P^T straight from the S^T accumulators (bf16) with the
+//                               key order k(8g+j) = 16*(j>>2) + 4g + (j&3) of each 32-key
+//                               fragment; A = V^T read with ds_read_b64_tr_b16 (hardware
+//                               transpose) from the row-major V image - no transposing stores.
 // Causal (row at position p sees keys <= p) or, for the reference's unmasked prefill
-// (SURVEY.md Q1), every key < kv_len.
+// (SURVEY.md Q1), every key < kv_len. Waves skip blocks wholly above their rows' diagonal.
 #include "common.h"
 
 namespace {
 
-constexpr int BK = 64, NTHR = 256;  // 64-row query tiles: 4 waves x 16 rows
+constexpr int BKV = 64, NWV = 8, NTHR = NWV * 64;  // 64-key blocks, 8 waves x 16 query rows
 
 struct PrefillTile {
   int row0, nrows, slot, pos0, kvlen, pad0, pad1, pad2;
 };
 
+typedef short v4s_t __attribute__((ext_vector_type(4)));
+
+// byte offset of 16-B chunk ch of row r in a [BKV][HD] bf16 image: rows XOR-swizzled so that
+// 16-lane ds_read_b128 row reads and 4-row ds_read_b64_tr_b16 reads are (near) conflict-free
 template <int HD>
-LSA_DEVICE int k_off(int key, int c16) {  // K block [BK][HD] bf16, 16-B chunks swizzled per key
-  constexpr int NC = HD / 8;  // 16 (256-B rows): key & 15; 8 (128-B rows): (key >> 1) & 7
-  const int sw = NC >= 16 ? (key & 15) : ((key >> 1) & (NC - 1));
-  return key * (HD * 2) + ((c16 ^ sw) << 4);
-}
-template <int HD>
-LSA_DEVICE int vt_off(int dim, int g8) {  // V^T block [HD][BK] bf16, 8-B (4-key) granules swizzled per dim
-  return dim * (BK * 2) + ((g8 ^ (dim & 15)) << 3);
+LSA_DEVICE int sw_off(int r, int ch) {
+  if constexpr (HD == 128) return r * 256 + ((ch ^ (((r & 3) << 2) | ((r >> 2) & 3))) << 4);
+  else return r * 128 + ((ch ^ ((r >> 1) & 7)) << 4);
 }
 
-template <int HD>
+LSA_DEVICE void glds16(const void* src, unsigned char* lds_base) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
+}
+
+template <int HD, int HPW>
 __global__ __launch_bounds__(NTHR) void flash_prefill_kernel(
     const bf16_raw* __restrict__ q, int ldq, const bf16_raw* __restrict__ kc, const bf16_raw* __restrict__ vc,
     const PrefillTile* __restrict__ tiles, int n_heads, int n_kv, int t_max, float scale_log2, int causal,
     bf16_raw* __restrict__ out, int ldo) {
-  constexpr int KF = HD / 32;     // 32-dim fragments of a query/key row
-  constexpr int DT = HD / 16;     // 16-dim output tiles
-  constexpr int NC = HD / 8;      // 16-B chunks per key row
-  constexpr int LPT = BK * NC / NTHR;  // 16-B loads per thread per operand per block
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * BK * HD * 2];
-  unsigned char* ks = smem;
-  unsigned char* vts = smem + BK * HD * 2;
+  constexpr int KF = HD / 32;                 // 32-dim fragments of a query/key row
+  constexpr int DT = HD / 16;                 // 16-dim output tiles
+  constexpr int NC = HD / 8;                  // 16-B chunks per row
+  constexpr int BLK = BKV * HD * 2;           // bytes of one K (or V) block
+  constexpr int PPW = BLK / 1024 / NWV;       // 1 KiB DMA pieces per wave per operand
+  constexpr int RPP = 1024 / (HD * 2);        // rows per piece
+  static_assert(PPW >= 1 && NWV % HPW == 0, "geometry");
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * 2 * BLK];  // [buffer][K | V]
 
-  const PrefillTile tile = tiles[blockIdx.x];
-  const int head = blockIdx.y;
-  const int kvh = head / (n_heads / n_kv);
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, l16 = lane & 15;
+  // work item -> (tile, head group). XCD-aware when the group count is a multiple of 8: XCD x
+  // (= blockIdx.x % 8 in dispatch order) owns groups x, x+8, ... so their K/V blocks stay in
+  // its L2, and walks its items tile-major (heaviest tiles of all its groups first)
+  const int n_groups = n_heads / HPW, n_tiles = gridDim.x / n_groups;
+  int tix, grp;
+  if (n_groups % 8 == 0) {
+    const int x = blockIdx.x % 8, j = blockIdx.x / 8, ngx = n_groups / 8;
+    tix = j / ngx;
+    grp = (j % ngx) * 8 + x;
+  } else {
+    tix = blockIdx.x % n_tiles;
+    grp = blockIdx.x / n_tiles;
+  }
+  const PrefillTile tile = tiles[tix];
+  const int G = n_heads / n_kv;
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, l16 = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int head = grp * HPW + w % HPW;
+  const int kvh = grp * HPW / G;
+  const int prow0 = (w / HPW) * 16;
 
   // ---- Q^T fragments for this wave's 16 rows (row = l16), kept for the whole tile
-  const int my_row = w * 16 + l16;
+  const int my_row = prow0 + l16;
   const bool row_ok = my_row < tile.nrows;
   const int my_pos = tile.pos0 + my_row;
   u32x4_t qf[KF];
@@ -69,37 +93,27 @@ __global__ __launch_bounds__(NTHR) void flash_prefill_kernel(
   }
   const int lim = causal ? min(tile.pos0 + tile.nrows, tile.kvlen) : tile.kvlen;  // keys any row needs
   const int my_lim = causal ? min(my_pos + 1, tile.kvlen) : tile.kvlen;         // keys this row sees
-  const int nkb = (lim + BK - 1) / BK;
+  const int wave_lim = causal ? min(tile.pos0 + min(prow0 + 16, tile.nrows), tile.kvlen) : tile.kvlen;
+  // blocks entirely below every row's limit need no mask (the wave's first row sees the fewest keys)
+  const int wave_min_lim = causal ? min(tile.pos0 + prow0 + 1, tile.kvlen) : tile.kvlen;
+  const int nkb = (lim + BKV - 1) / BKV;
 
   const size_t cache_base = ((size_t)tile.slot * n_kv + kvh) * (size_t)t_max * HD;
   const bf16_raw* kb_ptr = kc + cache_base;
   const bf16_raw* vb_ptr = vc + cache_base;
 
-  // staging map: thread -> (key = i*(NTHR/NC) + tid/NC, chunk = tid%NC)
-  const int s_key = tid / NC, s_c = tid % NC;
-  u32x4_t kr[LPT], vr[LPT];
-  auto load_block = [&](int kb) {
+  // DMA of block kb into buffer buf: piece pc covers rows pc*RPP ..; lane -> (row, dest chunk
+  // slot); the source chunk is the swizzle's preimage, so the image is sw_off-addressed
+  auto stage = [&](int kb, int buf) {
+    unsigned char* kd = smem + buf * (2 * BLK);
 #pragma unroll
-    for (int i = 0; i < LPT; ++i) {
-      int key = kb * BK + i * (NTHR / NC) + s_key;
-      key = key < lim ? key : lim - 1;  // clamp: masked anyway, stays inside the cache
-      kr[i] = ld16(kb_ptr + (size_t)key * HD + s_c * 8);
-      vr[i] = ld16(vb_ptr + (size_t)key * HD + s_c * 8);
-    }
-  };
-  auto store_block = [&]() {
-#pragma unroll
-    for (int i = 0; i < LPT; ++i) {
-      const int key = i * (NTHR / NC) + s_key;
-      *reinterpret_cast<u32x4_t*>(ks + k_off<HD>(key, s_c)) = kr[i];
-      // transpose V: 8 dims of one key -> 8 rows of V^T
-      const unsigned* vw = reinterpret_cast<const unsigned*>(&vr[i]);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int dim = s_c * 8 + j;
-        const bf16_raw v = (bf16_raw)((j & 1) ? (vw[j >> 1] >> 16) : (vw[j >> 1] & 0xffffu));
-        *reinterpret_cast<bf16_raw*>(vts + vt_off<HD>(dim, key >> 2) + (key & 3) * 2) = v;
-      }
+    for (int s = 0; s < PPW; ++s) {
+      const int pc = w * PPW + s;
+      const int r = pc * RPP + lane / NC, slot = lane % NC;
+      const int ch = HD == 128 ? (slot ^ (((r & 3) << 2) | ((r >> 2) & 3))) : (slot ^ ((r >> 1) & 7));
+      const int key = min(kb * BKV + r, lim - 1);  // clamped rows are masked in the softmax
+      glds16(kb_ptr + (size_t)key * HD + ch * 8, kd + pc * 1024);
+      glds16(vb_ptr + (size_t)key * HD + ch * 8, kd + BLK + pc * 1024);
     }
   };
 
@@ -108,77 +122,106 @@ __global__ __launch_bounds__(NTHR) void flash_prefill_kernel(
   for (int d = 0; d < DT; ++d) o[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   float m_run = -INFINITY, l_run = 0.f;
 
-  if (nkb > 0) load_block(0);
-  for (int kb = 0; kb < nkb; ++kb) {
-    __syncthreads();  // previous block's LDS reads are done
-    store_block();
-    __syncthreads();
-    if (kb + 1 < nkb) load_block(kb + 1);
+  // per-lane LDS offsets, hoisted out of the block loop (the swizzle term of a lane's reads is
+  // the same in every block; rows differ by compile-time multiples folded into the reads)
+  int k_off[KF], v_off[DT];
+#pragma unroll
+  for (int kf = 0; kf < KF; ++kf) k_off[kf] = sw_off<HD>(l16, kf * 4 + g);  // + kt * 16 rows
+  const int key_lo = 4 * g + (l16 >> 2);                                    // + f2 * 32 (+ 16) rows
+#pragma unroll
+  for (int d = 0; d < DT; ++d) v_off[d] = sw_off<HD>(key_lo, 2 * d + ((l16 & 3) >> 1)) + 8 * (l16 & 1);
 
-    // S^T = K . Q^T : 4 key tiles of 16
+  if (nkb > 0) stage(0, 0);
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int cur = kb & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of block kb landed
+    __syncthreads();                                    // ... every wave's; block kb-1 reads done
+    if (kb + 1 < nkb) stage(kb + 1, cur ^ 1);
+    if (kb * BKV >= wave_lim) continue;                 // wave-uniform: all keys above the diagonal
+    const unsigned char* ks = smem + cur * (2 * BLK);
+    const unsigned char* vs = ks + BLK;
+
+    // S^T = K . Q^T : 4 key tiles of 16 (row kt*16 + l16: the swizzle term depends on l16 only)
     f32x4_t s[4];
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
       s[kt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kf = 0; kf < KF; ++kf) {
-        const u32x4_t a = *reinterpret_cast<const u32x4_t*>(ks + k_off<HD>(kt * 16 + l16, kf * 4 + g));
+        const u32x4_t a = *reinterpret_cast<const u32x4_t*>(ks + kt * 16 * (HD * 2) + k_off[kf]);
         s[kt] = mfma16(a, qf[kf], s[kt]);
       }
     }
-    // scale, mask, block row max (this lane: row my_row, keys kb*64 + kt*16 + 4g + r)
+    // scale, mask (diagonal / tail blocks only), block row max (this lane: row my_row, keys
+    // kb*64 + kt*16 + 4g + r)
     float mx = -INFINITY;
+    if ((kb + 1) * BKV <= wave_min_lim) {
 #pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
+      for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = kb * BK + kt * 16 + g * 4 + r;
-        const float v = key < my_lim ? s[kt][r] * scale_log2 : -INFINITY;
-        s[kt][r] = v;
-        mx = fmaxf(mx, v);
-      }
+        for (int r = 0; r < 4; ++r) {
+          s[kt][r] *= scale_log2;
+          mx = fmaxf(mx, s[kt][r]);
+        }
+    } else {
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = kb * BKV + kt * 16 + g * 4 + r;
+          const float v = key < my_lim ? s[kt][r] * scale_log2 : -INFINITY;
+          s[kt][r] = v;
+          mx = fmaxf(mx, v);
+        }
+    }
     mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float m_new = fmaxf(m_run, mx);
     // fully-masked rows so far (m_new = -inf) keep alpha = 1 and p = 0
     const float m_use = m_new == -INFINITY ? 0.f : m_new;
-    const float alpha = exp2f(m_run - m_use);
+    // raw v_exp_f32 (arguments <= 0: no range reduction needed; -inf -> 0)
+    const float alpha = __builtin_amdgcn_exp2f(m_run - m_use);
     float psum = 0.f;
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float p = exp2f(s[kt][r] - m_use);
+        const float p = __builtin_amdgcn_exp2f(s[kt][r] - m_use);
         s[kt][r] = p;
         psum += p;
       }
     l_run = l_run * alpha + psum;  // per-lane partial (this lane's keys); reduced at the end
+    // rescale O only when some row's max moved (wave-uniform branch)
+    if (__builtin_amdgcn_ballot_w64(m_new != m_run)) {
+#pragma unroll
+      for (int d = 0; d < DT; ++d) o[d] *= alpha;
+    }
     m_run = m_new;
-#pragma unroll
-    for (int d = 0; d < DT; ++d) o[d] *= alpha;
 
-    // O^T += V^T . P^T over two 32-key fragments
+    // O^T += V^T . P^T over two 32-key fragments; V^T by hardware-transposed reads: in each
+    // 16-lane group, lane 4q+p addresses key (base + q), dims 4p..4p+3 of the 16-dim tile
 #pragma unroll
-    for (int kf2 = 0; kf2 < 2; ++kf2) {
+    for (int f2 = 0; f2 < 2; ++f2) {
       float pf[8];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        pf[r] = s[2 * kf2][r];
-        pf[4 + r] = s[2 * kf2 + 1][r];
+        pf[r] = s[2 * f2][r];
+        pf[4 + r] = s[2 * f2 + 1][r];
       }
       const u32x4_t b = pack8(pf);
 #pragma unroll
       for (int d = 0; d < DT; ++d) {
-        const int dim = d * 16 + l16;
-        const unsigned long long lo =
-            *reinterpret_cast<const unsigned long long*>(vts + vt_off<HD>(dim, kf2 * 8 + g));
-        const unsigned long long hi =
-            *reinterpret_cast<const unsigned long long*>(vts + vt_off<HD>(dim, kf2 * 8 + 4 + g));
+        // rows key_lo + f2*32 (+16): same swizzle term as key_lo (it depends on row & 15 only
+        // through row & 3 and (row >> 2) & 3, unchanged by multiples of 16)
+        const v4s_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) v4s_t*)(vs + f2 * 32 * (HD * 2) + v_off[d]));
+        const v4s_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) v4s_t*)(vs + (f2 * 32 + 16) * (HD * 2) + v_off[d]));
         u32x4_t a;
-        a[0] = (unsigned)lo;
-        a[1] = (unsigned)(lo >> 32);
-        a[2] = (unsigned)hi;
-        a[3] = (unsigned)(hi >> 32);
+        a[0] = __builtin_bit_cast(u32x2_t, lo)[0];
+        a[1] = __builtin_bit_cast(u32x2_t, lo)[1];
+        a[2] = __builtin_bit_cast(u32x2_t, hi)[0];
+        a[3] = __builtin_bit_cast(u32x2_t, hi)[1];
         o[d] = mfma16(a, b, o[d]);
       }
     }
@@ -198,26 +241,57 @@ __global__ __launch_bounds__(NTHR) void flash_prefill_kernel(
   }
 }
 
+template <int HD, int HPW>
+void launch_prefill(const bf16_raw* q, int ldq, const bf16_raw* k, const bf16_raw* v, const PrefillTile* t,
+                    int n_tiles, int n_heads, int n_kv, int t_max, float sl2, int causal, bf16_raw* o, int ldo,
+                    hipStream_t stream) {
+  dim3 grid(n_tiles * (n_heads / HPW)), block(NTHR);
+  flash_prefill_kernel<HD, HPW><<<grid, block, 0, stream>>>(q, ldq, k, v, t, n_heads, n_kv, t_max, sl2, causal, o, ldo);
+}
+
+template <int HD>
+int dispatch_hpw(int hpw, const bf16_raw* q, int ldq, const bf16_raw* k, const bf16_raw* v, const PrefillTile* t,
+                 int n_tiles, int n_heads, int n_kv, int t_max, float sl2, int causal, bf16_raw* o, int ldo,
+                 hipStream_t stream) {
+  switch (hpw) {
+    case 1: launch_prefill<HD, 1>(q, ldq, k, v, t, n_tiles, n_heads, n_kv, t_max, sl2, causal, o, ldo, stream); break;
+    case 2: launch_prefill<HD, 2>(q, ldq, k, v, t, n_tiles, n_heads, n_kv, t_max, sl2, causal, o, ldo, stream); break;
+    case 4: launch_prefill<HD, 4>(q, ldq, k, v, t, n_tiles, n_heads, n_kv, t_max, sl2, causal, o, ldo, stream); break;
+    case 8: launch_prefill<HD, 8>(q, ldq, k, v, t, n_tiles, n_heads, n_kv, t_max, sl2, causal, o, ldo, stream); break;
+    default: return LSA_UNSUPPORTED;
+  }
+  return LSA_OK;
+}
+
 }  // namespace
 
-// tiles: device array of n_tiles PrefillTile {row0, nrows<=64, slot, pos0, kvlen, pad x3}.
+// tiles: device array of n_tiles PrefillTile {row0, nrows, slot, pos0, kvlen, pad x3}; nrows <=
+// lsa_prefill_tile_rows(n_heads, n_kv) (128 / heads-per-workgroup).
+extern "C" int lsa_prefill_tile_rows(int n_heads, int n_kv) {
+  if (n_kv < 1 || n_heads % n_kv) return 0;
+  const int g = n_heads / n_kv;
+  return NTHR / 64 * 16 / ((NWV % g == 0) ? g : 1);
+}
+
 extern "C" int lsa_attn_prefill(const void* q, int ldq, const void* kc, const void* vc, const void* tiles, int n_tiles,
                                 int n_heads, int n_kv, int head_dim, int t_max, float scale, int causal, void* out,
                                 int ldo, hipStream_t stream) {
-  if (n_tiles < 1 || n_heads % n_kv || n_heads < 1) return LSA_BAD_SHAPE;
+  if (n_tiles < 1 || n_kv < 1 || n_heads % n_kv || n_heads < 1) return LSA_BAD_SHAPE;
   const float sl2 = scale * 1.4426950408889634f;
-  dim3 grid(n_tiles, n_heads), block(NTHR);
+  const int g = n_heads / n_kv, hpw = (NWV % g == 0) ? g : 1;
   const auto* t = static_cast<const PrefillTile*>(tiles);
   const auto* qq = static_cast<const bf16_raw*>(q);
   const auto* k = static_cast<const bf16_raw*>(kc);
   const auto* v = static_cast<const bf16_raw*>(vc);
   auto* o = static_cast<bf16_raw*>(out);
+  int rc;
   if (head_dim == 128)
-    flash_prefill_kernel<128><<<grid, block, 0, stream>>>(qq, ldq, k, v, t, n_heads, n_kv, t_max, sl2, causal, o, ldo);
+    rc = dispatch_hpw<128>(hpw, qq, ldq, k, v, t, n_tiles, n_heads, n_kv, t_max, sl2, causal, o, ldo, stream);
   else if (head_dim == 64)
-    flash_prefill_kernel<64><<<grid, block, 0, stream>>>(qq, ldq, k, v, t, n_heads, n_kv, t_max, sl2, causal, o, ldo);
+    rc = dispatch_hpw<64>(hpw, qq, ldq, k, v, t, n_tiles, n_heads, n_kv, t_max, sl2, causal, o, ldo, stream);
   else
     return LSA_UNSUPPORTED;
+  if (rc != LSA_OK) return rc;
   LSA_CHECK_LAUNCH();
   return LSA_OK;
 }

@@ -478,15 +478,23 @@ def attn(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, slot: to
     _check(rc, "lsa_attn_decode")
 
 
-PREFILL_TILE_ROWS = 64
+PREFILL_TILE_ROWS = 128  # positions per tile with one query head per workgroup
 
 
-def build_prefill_tiles(slot, pos, kv_len=None, device=None):
+def prefill_tile_rows(n_heads: int, n_kv: int) -> int:
+    """Positions per flash-prefill tile: 8 waves x 16 rows shared by the GQA group's heads
+    that one workgroup covers (all G of them when G divides 8; lsa_prefill_tile_rows)."""
+    g = n_heads // n_kv
+    return PREFILL_TILE_ROWS // (g if 8 % g == 0 else 1)
+
+
+def build_prefill_tiles(slot, pos, kv_len=None, device=None, tile_rows: int = PREFILL_TILE_ROWS):
     """Host-side tile table for :func:`attn_prefill`: rows are grouped into runs of one
-    sequence (same slot, consecutive positions) and each run is cut into <= 64-row tiles
-    ``[row0, nrows, slot, pos0, kvlen, 0, 0, 0]`` (int32). Causal tiles get
-    ``kvlen = last position + 1``; with an explicit per-row ``kv_len`` (the reference's
-    unmasked prefill) every row of a run must share it. Heaviest tiles first (balance)."""
+    sequence (same slot, consecutive positions) and each run is cut into <= ``tile_rows``-row
+    tiles ``[row0, nrows, slot, pos0, kvlen, 0, 0, 0]`` (int32; ``tile_rows`` =
+    :func:`prefill_tile_rows` of the model). Causal tiles get ``kvlen = last position + 1``;
+    with an explicit per-row ``kv_len`` (the reference's unmasked prefill) every row of a run
+    must share it. Heaviest tiles first (balance)."""
     slot = [int(x) for x in (slot.tolist() if torch.is_tensor(slot) else slot)]
     pos = [int(x) for x in (pos.tolist() if torch.is_tensor(pos) else pos)]
     kvl = None if kv_len is None else [int(x) for x in (kv_len.tolist() if torch.is_tensor(kv_len) else kv_len)]
@@ -494,7 +502,7 @@ def build_prefill_tiles(slot, pos, kv_len=None, device=None):
     r, n = 0, len(slot)
     while r < n:
         e = r + 1
-        while (e < n and slot[e] == slot[r] and pos[e] == pos[e - 1] + 1 and e - r < PREFILL_TILE_ROWS
+        while (e < n and slot[e] == slot[r] and pos[e] == pos[e - 1] + 1 and e - r < tile_rows
                and (kvl is None or kvl[e] == kvl[r])):
             e += 1
         kv = pos[e - 1] + 1 if kvl is None else kvl[r]
@@ -520,7 +528,7 @@ def attn_prefill(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, 
     slots, t_max = k_cache.shape[0], k_cache.shape[2]
     if th.numel():
         row0, nr, sl, p0, kv = (th[:, i] for i in range(5))
-        _req(bool((nr >= 1).all() and (nr <= PREFILL_TILE_ROWS).all()), "attn_prefill: tile rows")
+        _req(bool((nr >= 1).all() and (nr <= prefill_tile_rows(n_heads, n_kv)).all()), "attn_prefill: tile rows")
         _req(bool((row0 >= 0).all()) and int((row0 + nr).max()) <= min(q.shape[0], out.shape[0]),
              "attn_prefill: tile rows out of range")
         _req(bool((sl >= 0).all() and (sl < slots).all()), "attn_prefill: slot out of range")

@@ -403,13 +403,31 @@ def test_attention_prefill_flash(nh, nkv, hd, causal):
     rows = len(slot)
     q = _rnd(rows, nh * hd)
     out = torch.zeros(rows, nh * hd, dtype=torch.bfloat16, device=DEV)
-    tiles = h.build_prefill_tiles(slot, pos, kvl, device=DEV)
+    tiles = h.build_prefill_tiles(slot, pos, kvl, device=DEV, tile_rows=h.prefill_tile_rows(nh, nkv))
     h.attn_prefill(q, kc, vc, tiles, nh, nkv, hd, out, causal=causal)
     ref = _prefill_ref(q, kc, vc, slot, pos, nh, nkv, hd, kvl)
     assert rel_err(out, ref) < 1e-2
     # per-row check too: no row may be garbage even if the aggregate is fine
     per_row = ((out.float() - ref).norm(dim=1) / ref.norm(dim=1))
     assert float(per_row.max()) < 3e-2
+
+
+@pytest.mark.parametrize("nh,nkv", [(32, 32), (64, 8), (16, 4)])
+def test_attention_prefill_long_sequence(nh, nkv):
+    """One 1100-token causal prefill (many 64-key blocks, partial last block, GQA groups
+    sharing each staged K/V block) against fp32 torch, checked on a row sample."""
+    h = hip()
+    hd, T, S = 128, 1152, 1100
+    kc, vc = _rnd(1, nkv, T, hd), _rnd(1, nkv, T, hd)
+    q = _rnd(S, nh * hd)
+    out = torch.zeros(S, nh * hd, dtype=torch.bfloat16, device=DEV)
+    slot, pos = [0] * S, list(range(S))
+    h.attn_prefill(q, kc, vc, h.build_prefill_tiles(slot, pos, device=DEV, tile_rows=h.prefill_tile_rows(nh, nkv)),
+                   nh, nkv, hd, out)
+    idx = torch.tensor([0, 1, 63, 64, 127, 128, 500, 777, 1023, 1024, 1099])
+    ref = _prefill_ref(q[idx], kc, vc, [0] * len(idx), idx.tolist(), nh, nkv, hd, None)
+    per_row = ((out[idx].float() - ref).norm(dim=1) / ref.norm(dim=1))
+    assert float(per_row.max()) < 2e-2, per_row
 
 
 @pytest.mark.parametrize("cfg", packing.FP8_CONFIGS)

@@ -102,7 +102,7 @@ def test_flash_prefill_random(segs, heads, causal):
     rows = len(slot)
     q = torch.randn(rows, nh * hd, device=DEV).to(torch.bfloat16)
     out = torch.zeros(rows, nh * hd, dtype=torch.bfloat16, device=DEV)
-    h.attn_prefill(q, kc, vc, h.build_prefill_tiles(slot, pos, kvl, device=DEV), nh, nkv, hd, out, causal=causal)
+    h.attn_prefill(q, kc, vc, h.build_prefill_tiles(slot, pos, kvl, device=DEV, tile_rows=h.prefill_tile_rows(nh, nkv)), nh, nkv, hd, out, causal=causal)
     g = nh // nkv
     ref = torch.zeros(rows, nh * hd, device=DEV)
     for r in range(rows):
