@@ -141,7 +141,8 @@ class PipelineStage:
                  microbatches: int, max_seq: int, source, use_graph: bool = True,
                  max_prefill_rows: int = 2048, dtype=torch.bfloat16, p2p=None,
                  split_head: Optional[bool] = None, weight_dtype: str = "bf16", streams: int = 1,
-                 pp_streams: Optional[bool] = None, engine: Optional[StageEngine] = None):
+                 pp_streams: Optional[bool] = None, engine: Optional[StageEngine] = None,
+                 persistent: bool = False):
         """``engine``: reuse a loaded StageEngine (its weights, KV cache and scratch) instead of
         building one - e.g. a batch-1 latency pass after a throughput pass; it must cover this
         stage's layers and hold >= batch x microbatches KV slots."""
@@ -186,6 +187,7 @@ class PipelineStage:
             self.seed = [None] * microbatches   # stage 0: (h_fin, keys) of each micro-batch's prefill
             self.final_tokens = [None] * microbatches
         self.graphs: list = []
+        self.persistent = persistent  # batch-1 decode graphs run decode_persistent.hip where eligible
         self.send_works: dict = {}
         self.tokens_ready = [True] * microbatches  # stage 0: next-step token ids are in place
         self.tl = tracing.from_env(rank, self.device if self.gpu else "cpu")  # LSA_TRACE=dir
@@ -297,7 +299,7 @@ class PipelineStage:
         self.graphs = []
         for mb in range(self.M):
             # micro-batches that share a stream replay one after another: one scratch set each
-            extra = {"scratch": mb % self.S} if self.gpu else {}
+            extra = {"scratch": mb % self.S, "persistent": self.persistent} if self.gpu else {}
             cls = DecodeGraph if self.gpu else EagerDecode
             if self.split and mode in ("first", "last"):
                 # stage 0 re-derives token s at step s: one more history row than the last stage keeps
@@ -518,7 +520,8 @@ def _latency_pass(cfg, stage: "PipelineStage", srank: int, pp: int, st, dev, max
     eng = stage.eng
     eng.reset([0])
     b1 = PipelineStage(cfg, srank, pp, st.start, st.end, dev, 1, 1, max_seq, None,
-                       use_graph=stage.use_graph, dtype=stage.dtype, p2p=p2p, engine=eng)
+                       use_graph=stage.use_graph, dtype=stage.dtype, p2p=p2p, engine=eng,
+                       persistent=os.environ.get("LSA_PERSISTENT", "0") == "1")
     b1.tl = stage.tl
     p1 = prompts[:1, :1].contiguous() if prompts is not None else None
     firsts = b1.prefill(p1, prompt_len)
