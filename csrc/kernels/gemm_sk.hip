@@ -407,7 +407,22 @@ struct Kern {
           float v[16];
 #pragma unroll
           for (int q = 0; q < 4; ++q) *reinterpret_cast<f32x4_t*>(v + 4 * q) = *reinterpret_cast<const f32x4_t*>(src + 4 * q);
-          if (m < P.M && (BN != 192 || col_base + j * 16 < P.N)) {
+          if (EPI == EPI_ARGMAX) {
+            // largest key of the unit, then of the FN lanes of this row (consecutive lanes; FN
+            // is a power of two for bn 128 / 256), one 64-bit atomic per row and wave
+            const int c0 = col_base + j * 16;
+            unsigned long long k = 0ull;
+            if (m < P.M) {
+              epi_bias16(ep, c0, v);
+              k = argmax_key16(v, (unsigned)(c0 + ep.col_offset));
+            }
+#pragma unroll
+            for (int o = 1; o < FN; o <<= 1) {
+              const unsigned long long ko = __shfl_xor(k, o, 64);
+              k = ko > k ? ko : k;
+            }
+            if (m < P.M && (lane % FN) == 0) atomicMax(&ep.keys[m], k);
+          } else if (m < P.M && (BN != 192 || col_base + j * 16 < P.N)) {
             if (EPI == EPI_PARTIAL) {  // fp32 partial of K range sp: 4 x 16-B stores
               float* o = reinterpret_cast<float*>(ep.out) + ((size_t)sp * P.M + m) * ep.ldo + col_base + j * 16;
 #pragma unroll
@@ -582,7 +597,7 @@ extern "C" int lsa_gemm_sk(const void* a, int lda, const void* wp, int M, int N,
   if (grid < 1 || grid > 1024 || group_m < 1) return LSA_BAD_SHAPE;
   if (epi == EPI_RESID && !ep->resid) return LSA_BAD_SHAPE;
   if (epi == EPI_QKV && (!ep->k_cache || !ep->v_cache || !ep->slot || !ep->pos)) return LSA_BAD_SHAPE;
-  if (!ep->out) return LSA_BAD_SHAPE;
+  if (epi == EPI_ARGMAX ? (!ep->keys || bn == 192) : !ep->out) return LSA_BAD_SHAPE;
   if (epi == EPI_PARTIAL && (split < 1 || ep->ldo < N || ep->ldo % 4)) return LSA_BAD_SHAPE;
   SkParams prm;
   prm.M = M;
@@ -635,6 +650,7 @@ extern "C" int lsa_gemm_sk(const void* a, int lda, const void* wp, int M, int N,
     case EPI_QKV: return LSA_G(EPI_QKV);
     case EPI_SWIGLU: return LSA_G(EPI_SWIGLU);
     case EPI_PARTIAL: return LSA_G(EPI_PARTIAL);
+    case EPI_ARGMAX: return LSA_G(EPI_ARGMAX);
     default: return LSA_UNSUPPORTED;
   }
 #undef LSA_G

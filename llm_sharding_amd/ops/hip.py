@@ -429,10 +429,16 @@ def gemm_sk(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int,
          "gemm_sk: A must be [>=M, >=K] row-major with 16-B aligned rows")
     _req(a.data_ptr() % 16 == 0, "gemm_sk: A must be 16-byte aligned")
     _check_epi(epi, ep, N)
-    _req(epi in (EPI_STORE, EPI_RESID, EPI_SWIGLU, EPI_QKV, EPI_PARTIAL), f"gemm_sk: epilogue {epi} not supported")
+    _req(epi in (EPI_STORE, EPI_RESID, EPI_SWIGLU, EPI_QKV, EPI_PARTIAL, EPI_ARGMAX), f"gemm_sk: epilogue {epi} not supported")
     if epi == EPI_PARTIAL:  # exactly `split` K ranges per tile, every tile in one round
         _req(bn in (128, 192, 256) and split >= 1 and grid >= 1, "gemm_sk partial: explicit bn, grid and split required")
     pb, pg, pd, ps = gemm_sk_plan(M, N, K)
+    if epi == EPI_ARGMAX:
+        # the argmax epilogue reduces over power-of-two lane groups; whole-K tiles only, so every
+        # logit is summed in the same order whatever N range (split lm_head) it is computed in
+        if pb == 192:
+            pb = 256 if N % 256 == 0 else 128
+        ps = split = 1
     if not bn:
         bn, grid, split = pb, grid or pg, ps if split < 0 else split
     grid = grid or pg

@@ -549,16 +549,26 @@ class StageEngine:
         n = idx.numel()
         if keys is None:
             keys = torch.zeros(n, dtype=torch.int64, device=self.device)
-        step = self.DECODE_MAX_ROWS
-        for c0 in range(0, n, step):
-            c = min(step, n - c0)
-            self.head_gemv(h, c, keys[c0:c0 + c], a_rows=idx[c0:c0 + c])
+        # one call: head_gemv picks the same kernel path (and numerics) for n rows as a decode
+        # graph of n rows does, so a split head's re-derived first token matches the prefill's
+        self.head_gemv(h, n, keys, a_rows=idx)
         return keys
 
     def head_gemv(self, h: torch.Tensor, rows: int, keys: torch.Tensor, a_rows=None) -> None:
         """Fused final RMSNorm + lm_head slice + argmax keys (atomicMax into ``keys``).
         GPT-2: ln_f (LayerNorm kernel, rows gathered first) then the plain GEMV + argmax."""
         from ..ops import hip
+        N0 = self.head_v1 - self.head_v0
+        if (rows > self.DECODE_MAX_ROWS and not self.cfg.is_gpt2 and self.lm_head_s is None and self.sk_ws is not None
+                and N0 % 128 == 0 and rows <= self.buf_xn.shape[0]):
+            # big batches: RMSNorm kernel (final norm folded into lm_head) -> gemm_sk with the
+            # fused argmax epilogue (one launch instead of 128-row GEMV chunks)
+            xn = self.buf_xn[:rows]
+            src = h[:rows] if a_rows is None else h.index_select(0, a_rows.long())
+            hip.rmsnorm(src, None, xn, rows, self.cfg.rms_norm_eps, self.cfg.hidden_size)
+            ep = hip.make_epi(keys=keys, col_offset=self.head_v0, bias=self.head_bias)
+            hip.gemm_sk(xn, self.lm_head, rows, N0, self.cfg.hidden_size, hip.EPI_ARGMAX, ep, ws=self.sk_ws)
+            return
         if rows > self.DECODE_MAX_ROWS:  # the fused head kernels take <= 128 rows per launch
             for c0 in range(0, rows, self.DECODE_MAX_ROWS):
                 c = min(self.DECODE_MAX_ROWS, rows - c0)

@@ -1,6 +1,11 @@
+#!/bin/bash
+# full GPU test suite + smoke + driver-style bench
 set -o pipefail
-cd $GRAFT_REPO_ROOT
+cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/full_pytest.log 2>&1 && \
-timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > gpurun_out/full_bench.log 2>&1
-echo rc=$?
+mkdir -p gpurun_out/full
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+    > gpurun_out/full/pytest.log 2>&1 &&
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/full/smoke.log 2>&1 &&
+timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > gpurun_out/full/bench.log 2>&1
+echo "rc=$?"

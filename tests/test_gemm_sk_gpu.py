@@ -190,3 +190,23 @@ def test_gemm_sk_partials_resid_rmsnorm(M, N, K, bn, S, ws):
     h2 = r.clone()
     h.resid_rmsnorm_partials(h2, P, S, M, 1e-5)  # residual only (stage output)
     assert torch.equal(h2, hb)
+
+
+@pytest.mark.parametrize("M,N,bn", [(300, 4096, 256), (512, 32000 // 128 * 128, 0), (777, 2048, 128)])
+def test_gemm_sk_argmax(M, N, bn, ws):
+    """EPI_ARGMAX (lm_head + greedy argmax keys, 64-bit atomics) against torch.argmax of the fp32
+    logits, with a column offset and a -huge bias column, wherever the top-2 margin is clear."""
+    h = hip()
+    K = 1024
+    a = _rnd(M, K)
+    w = _rnd(N, K, scale=0.05)
+    bias = torch.zeros(N, device=DEV)
+    bias[7] = -3.0e38
+    keys = torch.zeros(M, dtype=torch.int64, device=DEV)
+    h.gemm_sk(a, packing.pack_b(w), M, N, K, h.EPI_ARGMAX, h.make_epi(keys=keys, col_offset=100, bias=bias), bn=bn,
+              grid=256 if bn else 0, ws=ws)
+    lg = a.float() @ w.float().T + bias
+    top = lg.topk(2, dim=-1)
+    clear = (top.values[:, 0] - top.values[:, 1]) > 1e-3 * top.values[:, 0].abs()
+    got = 0xFFFFFFFF - (keys & 0xFFFFFFFF)
+    assert bool((got[clear] == top.indices[clear, 0] + 100).all())
