@@ -274,7 +274,7 @@ int launch_split(const bf16_raw* q, int ldq, const bf16_raw* kc, const bf16_raw*
     return launch_split_v<HD, G, UU, P, N>(q, ldq, kc, vc, slot, pos, kv_len, rows, n_heads, n_kv, t_max, \
                                            scale_log2, nsplit, min_chunk, po, pl, out, ldo, cnt, s);
     LSA_V(2, 0, 0) LSA_V(2, 1, 0) LSA_V(4, 0, 0) LSA_V(4, 1, 0) LSA_V(4, 1, 1) LSA_V(8, 0, 0) LSA_V(8, 0, 1)
-    LSA_V(8, 1, 0) LSA_V(6, 0, 0)
+    LSA_V(8, 1, 0) LSA_V(6, 0, 0) LSA_V(8, 1, 1) LSA_V(2, 1, 1) LSA_V(2, 0, 1)
 #undef LSA_V
   }
   // default: U = 4 groups in flight, non-temporal K/V loads (each cache line is read once per

@@ -74,6 +74,16 @@ LSA_DEVICE T wave_max(T v) {
   return v;
 }
 
+// Sum of squares of 16 values (x0 = columns 0..7, x1 = 8..15) in one fixed rounding order
+// (no contraction): the fused RMSNorm's per-64-column partials must be bitwise identical
+// whether a residual GEMM's epilogue (gemm_sk) or lsa_row_ss produced them.
+LSA_DEVICE float ss16(const float* x0, const float* x1) {
+  float s = 0.f;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) s = __fadd_rn(s, __fadd_rn(__fmul_rn(x0[q], x0[q]), __fmul_rn(x1[q], x1[q])));
+  return s;
+}
+
 // Orderable 64-bit key for a fused argmax: larger logit wins, ties -> smaller index
 // (torch.argmax returns the first maximal index; reference node_worker.py:264).
 LSA_DEVICE unsigned long long argmax_key(float v, unsigned idx) {

@@ -168,6 +168,27 @@ __global__ __launch_bounds__(256) void resid_norm_partials_kernel(bf16_raw* __re
   }
 }
 
+// Row sums of squares per 64-column block (the layout gemm_sk's fused norm reads, see
+// EpiArgs::ss_in): the stage input / embedding of a >128-row forward, whose producer is not a
+// residual GEMM. One 64-lane group per row, each lane one block (8 x 16-B loads).
+__global__ __launch_bounds__(256) void row_ss_kernel(const bf16_raw* __restrict__ h, int ldh, int rows, int nb,
+                                                     float* __restrict__ ss) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), b = threadIdx.x & 63;
+  if (row >= rows) return;
+  for (int blk = b; blk < nb; blk += 64) {
+    const bf16_raw* p = h + (size_t)row * ldh + blk * 64;
+    float s4[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // 16-column units, summed as gemm_sk's residual epilogue does
+      float x0[8], x1[8];
+      unpack8(ld16(p + j * 16), x0);
+      unpack8(ld16(p + j * 16 + 8), x1);
+      s4[j] = ss16(x0, x1);
+    }
+    ss[(size_t)row * nb + blk] = __fadd_rn(__fadd_rn(s4[0], s4[1]), __fadd_rn(s4[2], s4[3]));
+  }
+}
+
 // Two-pass (mean, then centred variance) over the row held in L2; the optional position add
 // rounds to bf16 first, as HF's ``inputs_embeds + position_embeds`` in the model dtype does.
 __global__ __launch_bounds__(256) void layernorm_kernel(bf16_raw* __restrict__ x, int ldx,
@@ -289,6 +310,13 @@ extern "C" int lsa_resid_rmsnorm_partials(void* h, int ldh, const float* partial
     case 8192: resid_norm_partials_kernel<4><<<rows, 256, 0, stream>>>(hb, ldh, partials, S, pstride, ldp, wb, eps, ob, ldo); break;
     default: return LSA_UNSUPPORTED;
   }
+  LSA_CHECK_LAUNCH();
+  return LSA_OK;
+}
+
+extern "C" int lsa_row_ss(const void* h, int ldh, int rows, int H, float* ss, hipStream_t stream) {
+  if (rows < 1 || H % 64 || ldh % 8) return LSA_BAD_SHAPE;
+  row_ss_kernel<<<(rows + 3) / 4, 256, 0, stream>>>(static_cast<const bf16_raw*>(h), ldh, rows, H / 64, ss);
   LSA_CHECK_LAUNCH();
   return LSA_OK;
 }

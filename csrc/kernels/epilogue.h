@@ -40,6 +40,13 @@ struct EpiArgs {
   int t_max;
   int col_offset;           // ARGMAX: vocabulary index of column 0 (vocab-parallel chunks)
   int act;                  // STORE: 0 identity, 1 gelu (tanh form, GPT-2 "gelu_new")
+  // fused RMSNorm across GEMMs (gemm_sk only; layout [M][ss_n] fp32, one partial sum of squares
+  // per 64 columns of the residual stream): RESID writes the partials of its rounded outputs to
+  // ss_out; QKV / SWIGLU scale row m by rsqrt(sum(ss_in[m][:]) / (64 ss_n) + ss_eps) first
+  float* ss_out;
+  const float* ss_in;
+  int ss_n;
+  float ss_eps;
 };
 
 LSA_DEVICE float silu(float g) { return g / (1.0f + __expf(-g)); }

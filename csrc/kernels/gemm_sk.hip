@@ -51,7 +51,8 @@ struct Geo {
   static constexpr int EROWS = TN > 64 ? 32 : 64;   // rows per epilogue transpose pass
   static constexpr int ELD = TN + 4;                // fp32 row stride of the transpose image
   static constexpr int EPI_BYTES = 8 * EROWS * ELD * 4;
-  static constexpr int SMEM = (NB * BUF > EPI_BYTES ? NB * BUF : EPI_BYTES) + 16;
+  static constexpr int RS_OFF = (NB * BUF > EPI_BYTES ? NB * BUF : EPI_BYTES);  // per-wave row rstd [8][EROWS]
+  static constexpr int SMEM = RS_OFF + 8 * EROWS * 4 + 16;
   static_assert(SMEM <= 160 * 1024, "LDS budget");
   static_assert(BHI_WAVES == 0 || BGL_LO == 0 || BHI_WAVES == 4, "B blocks per wave");
 };
@@ -357,9 +358,24 @@ struct Kern {
     const SkParams& P = *p;
     constexpr int EROWS = G_::EROWS, ELD = G_::ELD, FPP = EROWS / 16;  // rows / fragments per pass
     float* img = reinterpret_cast<float*>(smem) + w * (EROWS * ELD);
+    float* s_rs = reinterpret_cast<float*>(smem + G_::RS_OFF) + w * EROWS;
+    constexpr bool SS_IN = EPI == EPI_QKV || EPI == EPI_SWIGLU;
     constexpr int PASSES = TM / EROWS;
 #pragma unroll
     for (int ps = 0; ps < PASSES; ++ps) {
+      if (SS_IN && ep.ss_in) {
+        // fused RMSNorm: rstd of this pass's rows from the producer's 64-column partials
+        if (lane < EROWS) {
+          const int m = min(mt * BM + wr * TM + ps * EROWS + lane, P.M - 1);
+          const float* sp = ep.ss_in + (size_t)m * ep.ss_n;
+          float t = 0.f;
+          for (int i = 0; i < ep.ss_n; i += 4) {
+            const f32x4_t q4 = *reinterpret_cast<const f32x4_t*>(sp + i);
+            t += (q4[0] + q4[1]) + (q4[2] + q4[3]);
+          }
+          s_rs[lane] = rsqrtf(t / (float)(64 * ep.ss_n) + ep.ss_eps);
+        }
+      }
 #pragma unroll
       for (int i = 0; i < FPP; ++i)
 #pragma unroll
@@ -388,6 +404,14 @@ struct Kern {
           }
           const int c0 = col_base + pr * 32;
           if (m < P.M && (BN != 192 || c0 < P.N)) {
+            if (ep.ss_in) {
+              const float r = s_rs[row];
+#pragma unroll
+              for (int q = 0; q < 16; ++q) {
+                g[q] *= r;
+                uu[q] *= r;
+              }
+            }
             epi_bias16(ep, c0, g);
             epi_bias16(ep, c0 + 16, uu);
 #pragma unroll
@@ -422,7 +446,40 @@ struct Kern {
               k = ko > k ? ko : k;
             }
             if (m < P.M && (lane % FN) == 0) atomicMax(&ep.keys[m], k);
+          } else if (EPI == EPI_RESID && ep.ss_out) {
+            // residual add + the row's sum of squares of the ROUNDED outputs over this wave's
+            // 64 columns (FN = 4 consecutive lanes per row: bn 128 / 256), one float per block
+            float ssq = 0.f;
+            const int c0 = col_base + j * 16;
+            if (m < P.M) {
+              epi_bias16(ep, c0, v);
+              const bf16_raw* rr = ep.resid + (size_t)m * ep.ldr + c0;
+              float x0[8], x1[8];
+              unpack8(ld16(rr), x0);
+              unpack8(ld16(rr + 8), x1);
+#pragma unroll
+              for (int q = 0; q < 8; ++q) {
+                x0[q] += v[q];
+                x1[q] += v[q + 8];
+              }
+              const u32x4_t p0 = pack8(x0), p1 = pack8(x1);
+              bf16_raw* o = ep.out + (size_t)m * ep.ldo + c0;
+              st16(o, p0);
+              st16(o + 8, p1);
+              unpack8(p0, x0);
+              unpack8(p1, x1);
+              ssq = ss16(x0, x1);
+            }
+            // (s0 + s1) + (s2 + s3) over the FN = 4 units of the 64-column block (lsa_row_ss order)
+#pragma unroll
+            for (int o = 1; o < FN; o <<= 1) ssq = __fadd_rn(ssq, __shfl_xor(ssq, o, 64));
+            if (m < P.M && (lane % FN) == 0) ep.ss_out[(size_t)m * ep.ss_n + (col_base >> 6)] = ssq;
           } else if (m < P.M && (BN != 192 || col_base + j * 16 < P.N)) {
+            if (EPI == EPI_QKV && ep.ss_in) {
+              const float r = s_rs[row];
+#pragma unroll
+              for (int q = 0; q < 16; ++q) v[q] *= r;
+            }
             if (EPI == EPI_PARTIAL) {  // fp32 partial of K range sp: 4 x 16-B stores
               float* o = reinterpret_cast<float*>(ep.out) + ((size_t)sp * P.M + m) * ep.ldo + col_base + j * 16;
 #pragma unroll
@@ -598,6 +655,9 @@ extern "C" int lsa_gemm_sk(const void* a, int lda, const void* wp, int M, int N,
   if (epi == EPI_RESID && !ep->resid) return LSA_BAD_SHAPE;
   if (epi == EPI_QKV && (!ep->k_cache || !ep->v_cache || !ep->slot || !ep->pos)) return LSA_BAD_SHAPE;
   if (epi == EPI_ARGMAX ? (!ep->keys || bn == 192) : !ep->out) return LSA_BAD_SHAPE;
+  if (ep->ss_out && (epi != EPI_RESID || bn == 192 || N % 64 || ep->ss_n != N / 64)) return LSA_BAD_SHAPE;
+  if (ep->ss_in && ((epi != EPI_QKV && epi != EPI_SWIGLU) || ep->ss_n < 4 || ep->ss_n % 4 || K != 64 * ep->ss_n))
+    return LSA_BAD_SHAPE;
   if (epi == EPI_PARTIAL && (split < 1 || ep->ldo < N || ep->ldo % 4)) return LSA_BAD_SHAPE;
   SkParams prm;
   prm.M = M;

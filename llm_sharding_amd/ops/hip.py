@@ -35,6 +35,7 @@ class EpiArgs(ctypes.Structure):
         ("ldo", ctypes.c_int), ("ldr", ctypes.c_int), ("n_heads", ctypes.c_int),
         ("n_kv", ctypes.c_int), ("head_dim", ctypes.c_int), ("t_max", ctypes.c_int),
         ("col_offset", ctypes.c_int), ("act", ctypes.c_int),
+        ("ss_out", ctypes.c_void_p), ("ss_in", ctypes.c_void_p), ("ss_n", ctypes.c_int), ("ss_eps", ctypes.c_float),
     ]
 
 
@@ -67,6 +68,7 @@ def lib() -> ctypes.CDLL:
     L.lsa_rmsnorm.argtypes = [vp, i, vp, i, i, f, vp, i, vp]
     L.lsa_layernorm.argtypes = [vp, i, vp, vp, vp, vp, i, i, f, vp, i, vp]
     L.lsa_resid_rmsnorm_partials.argtypes = [vp, i, vp, i, ctypes.c_longlong, i, vp, i, i, f, vp, i, vp]
+    L.lsa_row_ss.argtypes = [vp, i, i, i, vp, vp]
     L.lsa_decode_persistent.argtypes = [vp, i, i, i, i, i, i, i, i, f, f, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i,
                                         vp, vp, i, i, vp, i, vp, vp, i, vp]
     L.lsa_argmax_finalize.argtypes = [vp, i, vp, vp, i, vp, i, i, vp, vp]
@@ -75,7 +77,7 @@ def lib() -> ctypes.CDLL:
                               vp]
     for name in ("lsa_gemv", "lsa_gemv_coop", "lsa_gemv_fp8", "lsa_dequant_fp8_packed", "lsa_gemv_coop_fp8", "lsa_gemm",
                  "lsa_gemm_sk", "lsa_attn_decode", "lsa_attn_prefill", "lsa_embed", "lsa_rmsnorm", "lsa_layernorm",
-                 "lsa_resid_rmsnorm_partials", "lsa_decode_persistent",
+                 "lsa_resid_rmsnorm_partials", "lsa_decode_persistent", "lsa_row_ss",
                  "lsa_argmax_finalize", "lsa_pos_advance", "lsa_version"):
         getattr(L, name).restype = ctypes.c_int
     _lib = L
@@ -109,9 +111,12 @@ ACT_NONE, ACT_GELU = 0, 1  # EpiArgs.act (EPI_STORE): identity / tanh-GELU (GPT-
 
 def make_epi(out=None, resid=None, k_cache=None, v_cache=None, slot=None, pos=None, cos=None,
              sin=None, keys=None, ldo=0, ldr=0, n_heads=0, n_kv=0, head_dim=0, t_max=0,
-             col_offset=0, bias=None, act=ACT_NONE) -> EpiArgs:
+             col_offset=0, bias=None, act=ACT_NONE, ss_out=None, ss_in=None, ss_eps=0.0) -> EpiArgs:
     """Epilogue arguments. ``bias``: optional fp32 [N] added to every output column (in packed
-    column order); ``cos=None`` with EPI_QKV: no RoPE, natural q|k|v column order."""
+    column order); ``cos=None`` with EPI_QKV: no RoPE, natural q|k|v column order.
+    ``ss_out`` / ``ss_in`` (gemm_sk): fp32 [>= M, H/64] row partial sums of squares - a RESID
+    GEMM writes them for its outputs, a QKV / SWIGLU GEMM reading the raw residual stream as A
+    applies the RMSNorm scale from them (the norm weight is folded into its W)."""
     if bias is not None:
         _req(bias.dtype == torch.float32 and bias.is_contiguous(), "epilogue bias: contiguous fp32")
     # vectorised epilogues store 16-B runs: rows must start 16-B aligned
@@ -119,8 +124,12 @@ def make_epi(out=None, resid=None, k_cache=None, v_cache=None, slot=None, pos=No
     for t in (out, resid, bias):
         _req(t is None or t.data_ptr() % 16 == 0, "epilogue: out/resid/bias must be 16-byte aligned")
     _req(head_dim == 0 or (head_dim & (head_dim - 1)) == 0, f"epilogue: head_dim {head_dim} not a power of two")
+    ssb = ss_in if ss_in is not None else ss_out
+    for t in (ss_out, ss_in):
+        _req(t is None or (t.dtype == torch.float32 and t.dim() == 2 and t.is_contiguous()), "epilogue: ss fp32 [M, H/64]")
     return EpiArgs(_p(out), _p(resid), _p(k_cache), _p(v_cache), _p(slot), _p(pos), _p(cos), _p(sin),
-                   _p(keys), _p(bias), ldo, ldr, n_heads, n_kv, head_dim, t_max, col_offset, int(act))
+                   _p(keys), _p(bias), ldo, ldr, n_heads, n_kv, head_dim, t_max, col_offset, int(act),
+                   _p(ss_out), _p(ss_in), 0 if ssb is None else ssb.shape[1], float(ss_eps))
 
 
 # ------------------------------------------------------------------------------ projections
@@ -295,6 +304,7 @@ def gemm(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep
             and a.data_ptr() % 16 == 0:
         gemm_sk(a, wp, M, N, K, epi, ep, ws=sk_ws)
         return
+    _req(not (ep.ss_out or ep.ss_in), "gemm: the fused-norm epilogue fields need the gemm_sk path")
     _req(_is_bf16_cuda(a, wp), "gemm: bf16 cuda tensors required")
     _req(wp.numel() == N * K and K % 64 == 0, "gemm: packed weight shape")
     _req(a.dim() == 2 and a.shape[0] >= M and a.shape[1] >= K and a.stride(1) == 1, "gemm: A shape")
@@ -433,6 +443,8 @@ def gemm_sk(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int,
     if epi == EPI_PARTIAL:  # exactly `split` K ranges per tile, every tile in one round
         _req(bn in (128, 192, 256) and split >= 1 and grid >= 1, "gemm_sk partial: explicit bn, grid and split required")
     pb, pg, pd, ps = gemm_sk_plan(M, N, K)
+    if ep.ss_out and pb == 192:  # the fused-norm partials are per 64 columns of one wave (TN = 64)
+        pb = 256 if N % 256 == 0 else 128
     if epi == EPI_ARGMAX:
         # the argmax epilogue reduces over power-of-two lane groups; whole-K tiles only, so every
         # logit is summed in the same order whatever N range (split lm_head) it is computed in
@@ -555,6 +567,13 @@ def embed(ids: torch.Tensor, table: torch.Tensor, out: torch.Tensor, rows: Optio
     _req(_is_bf16_cuda(table, out) and out.shape[1] >= table.shape[1], "embed: shapes")
     rc = lib().lsa_embed(_p(ids), rows, _p(table), table.shape[1], _p(out), out.stride(0), _stream())
     _check(rc, "lsa_embed")
+
+
+def row_ss(h: torch.Tensor, rows: int, ss: torch.Tensor) -> None:
+    """ss[r][b] = sum of squares of h[r, 64b:64b+64] (fp32) for the fused RMSNorm of gemm_sk."""
+    _req(_is_bf16_cuda(h) and ss.dtype == torch.float32 and ss.shape[1] * 64 == h.shape[1], "row_ss: shapes")
+    rc = lib().lsa_row_ss(_p(h), h.stride(0), rows, h.shape[1], _p(ss), _stream())
+    _check(rc, "lsa_row_ss")
 
 
 def resid_rmsnorm_partials(h: torch.Tensor, partials: torch.Tensor, S: int, rows: int, eps: float,

@@ -192,7 +192,8 @@ def scratch_bytes(cfg: LlamaConfig, rows: int, sets: int = 1, max_seq: int = 409
     sk = (2 * 256 * 256 * 256 * 4 + 4 * 256 * 4) if R > dmr else 0
     # split-K partials of the residual projections (hip.PARTIAL_MAX_SPLIT x <= 1024 rows x H fp32)
     part = 8 * min(R, 1024) * H * 4 if (R > dmr and not cfg.is_gpt2) else 0
-    return float(sets * (act + attn + coop + sk + part))
+    ssb = R * (H // 64) * 4 if (R > dmr and not cfg.is_gpt2 and H % 256 == 0) else 0  # fused-norm sums
+    return float(sets * (act + attn + coop + sk + part + ssb))
 
 
 def stage_memory(cfg: LlamaConfig, n_layers: int, *, slots: int, max_seq: int, prefill_rows: int,

@@ -177,7 +177,7 @@ class StageEngine:
     DECODE_MAX_ROWS = packing.GEMV_MAX_ROWS  # rows handled by the weight-streaming GEMV paths (128)
     # split-KV chunks never shorter than this many keys: below ~256 keys per split the merge
     # costs more than the extra parallelism buys (profiles/r1_bench_kernels_sweep.jsonl, attn)
-    ATTN_MIN_CHUNK = 256
+    ATTN_MIN_CHUNK = int(os.environ.get("LSA_ATTN_MIN_CHUNK", "256"))  # keys per decode split, at least
 
     def __init__(self, cfg: LlamaConfig, start: int, end: int, device="cpu",
                  dtype=torch.bfloat16, *, has_embed: bool = False, has_head: bool = False,
@@ -341,7 +341,7 @@ class StageEngine:
             self.buf_q = torch.zeros((R, cfg.q_size), dtype=bf, device=dev)
             self.buf_attn = torch.zeros((R, cfg.q_size), dtype=bf, device=dev)
             self.buf_act = torch.zeros((R, I), dtype=bf, device=dev)
-            self.max_decode_nsplit = int(min(16, max(1, ceil_div(self.max_seq, 256))))
+            self.max_decode_nsplit = int(min(16, max(1, ceil_div(self.max_seq, self.ATTN_MIN_CHUNK))))
             ws_rows = max(self.DECODE_MAX_ROWS * self.max_decode_nsplit, R * 4)
             self.part_o = torch.zeros(ws_rows * cfg.num_attention_heads * hd, dtype=torch.float32, device=dev)
             self.part_lse = torch.zeros(ws_rows * cfg.num_attention_heads, dtype=torch.float32, device=dev)
@@ -365,9 +365,16 @@ class StageEngine:
             # split-K partials of the residual projections (gemm_sk EPI_PARTIAL), summed by the
             # following norm kernel, for >128-row forwards of up to PARTIAL_MAX_ROWS rows
             self.part_k = self._alloc_part_k(R)
+            # row sums of squares per 64 columns of h: RMSNorm fused across the >128-row GEMMs
+            self.ss_buf = self._alloc_ss(R)
             self.w_scratch = None
             if self.fp8:  # one projection's bf16 weights, for the >64-row paths
                 self.w_scratch = torch.empty(max(n * k for n, k in shapes), dtype=torch.bfloat16, device=dev)
+
+    def _alloc_ss(self, R: int):
+        if R <= self.DECODE_MAX_ROWS or self.cfg.is_gpt2 or self.cfg.hidden_size % 256:
+            return None
+        return torch.zeros((R, self.cfg.hidden_size // 64), dtype=torch.float32, device=self.device)
 
     def _alloc_part_k(self, R: int):
         from ..ops import hip
@@ -396,7 +403,7 @@ class StageEngine:
 
     # buffers a forward pass writes besides the KV cache: one set per concurrently running graph
     SCRATCH_ATTRS = ("buf_h", "buf_xn", "buf_q", "buf_attn", "buf_act", "part_o", "part_lse", "attn_cnt",
-                     "coop_ws", "sk_ws", "part_k", "w_scratch", "keys", "tokens", "ws_rows")
+                     "coop_ws", "sk_ws", "part_k", "ss_buf", "w_scratch", "keys", "tokens", "ws_rows")
 
     def decode_scratch(self, k: int, rows: Optional[int] = None) -> dict:
         """Scratch set ``k`` for forward passes that run CONCURRENTLY on different streams (a
@@ -427,6 +434,7 @@ class StageEngine:
                                              groups=self.coop_ws.counters.numel()),
                 "sk_ws": hip.SkWorkspace(dev) if R > self.DECODE_MAX_ROWS else None,
                 "part_k": self._alloc_part_k(R),
+                "ss_buf": self._alloc_ss(R),
                 "w_scratch": None if self.w_scratch is None else torch.empty_like(self.w_scratch),
                 "keys": torch.zeros(R, dtype=torch.int64, device=dev),
                 "tokens": torch.zeros(R, dtype=torch.int32, device=dev),
@@ -683,6 +691,12 @@ class StageEngine:
                         bn=bn, grid=hip.N_CU, dp=0, split=sp, ws=self.sk_ws)
             return sp
 
+        # RMSNorm fused across the GEMMs: residual GEMMs write per-64-column sums of squares of
+        # their outputs (ss), the qkv / gate_up GEMMs read the raw residual stream and scale each
+        # row by its rstd in the epilogue - no standalone norm kernel between projections
+        fuse = not decode and self.ss_buf is not None and rows <= self.ss_buf.shape[0]
+        ss = self.ss_buf[:rows] if fuse else None
+        ss_valid = False  # ss holds the partials of hbuf's current values
         pending = 0  # down-projection partials not yet added to hbuf
         for li, lw in enumerate(self.layers):
             kc, vc = self.k_cache[li], self.v_cache[li]
@@ -691,12 +705,26 @@ class StageEngine:
             if decode:
                 dec(hbuf, lw.qkv, lw.qkv_s, cfg.qkv_size, H, hip.EPI_QKV, ep_qkv, norm=True)
             else:
-                if pending:
+                if pending and not fuse:
                     hip.resid_rmsnorm_partials(hbuf, self.part_k, pending, rows, eps, out=xn)
                     pending = 0
+                    pre(xn, lw.qkv, lw.qkv_s, cfg.qkv_size, H, hip.EPI_QKV, ep_qkv)
+                elif fuse:
+                    if pending:  # the previous down projection left K-split partials: add them
+                        hip.resid_rmsnorm_partials(hbuf, self.part_k, pending, rows, eps)
+                        pending = 0
+                    if not ss_valid:
+                        # (also at a stage's first layer: the same partials, in the same order, as
+                        # a residual GEMM epilogue writes - a layer range computes the same bits
+                        # whichever stage it starts)
+                        hip.row_ss(hbuf, rows, ss)
+                    ep_qkv = hip.make_epi(out=q, k_cache=kc, v_cache=vc, slot=slot, pos=pos, cos=self.cos,
+                                          sin=self.sin, ldo=q.stride(0), n_heads=nh, n_kv=nkv, head_dim=hd,
+                                          t_max=self.max_seq, ss_in=ss, ss_eps=eps)
+                    pre(hbuf, lw.qkv, lw.qkv_s, cfg.qkv_size, H, hip.EPI_QKV, ep_qkv)
                 else:
                     hip.rmsnorm(hbuf, None, xn, rows, eps, H)
-                pre(xn, lw.qkv, lw.qkv_s, cfg.qkv_size, H, hip.EPI_QKV, ep_qkv)
+                    pre(xn, lw.qkv, lw.qkv_s, cfg.qkv_size, H, hip.EPI_QKV, ep_qkv)
             if tiles is not None:
                 hip.attn_prefill(q, kc, vc, tiles[1], nh, nkv, hd, attn_o, causal=kv_len is None, tiles_host=tiles[0])
             else:
@@ -709,13 +737,20 @@ class StageEngine:
                 dec(hbuf, lw.gate_up, lw.gate_up_s, 2 * I, H, hip.EPI_SWIGLU, ep_gu, norm=True)
                 dec(act, lw.down, lw.down_s, H, I, hip.EPI_RESID, ep_o)
             else:
-                sp = resid_proj(attn_o, lw.o, lw.o_s, H, cfg.q_size, ep_o)
+                ep_r = hip.make_epi(out=hbuf, resid=hbuf, ldo=hbuf.stride(0), ldr=hbuf.stride(0), ss_out=ss) \
+                    if fuse else ep_o
+                sp = resid_proj(attn_o, lw.o, lw.o_s, H, cfg.q_size, ep_r)
                 if sp:
                     hip.resid_rmsnorm_partials(hbuf, self.part_k, sp, rows, eps, out=xn)
+                    pre(xn, lw.gate_up, lw.gate_up_s, 2 * I, H, hip.EPI_SWIGLU, ep_gu)
+                elif fuse:
+                    pre(hbuf, lw.gate_up, lw.gate_up_s, 2 * I, H, hip.EPI_SWIGLU,
+                        hip.make_epi(out=act, ldo=act.stride(0), ss_in=ss, ss_eps=eps))
                 else:
                     hip.rmsnorm(hbuf, None, xn, rows, eps, H)
-                pre(xn, lw.gate_up, lw.gate_up_s, 2 * I, H, hip.EPI_SWIGLU, ep_gu)
-                pending = resid_proj(act, lw.down, lw.down_s, H, I, ep_o)
+                    pre(xn, lw.gate_up, lw.gate_up_s, 2 * I, H, hip.EPI_SWIGLU, ep_gu)
+                pending = resid_proj(act, lw.down, lw.down_s, H, I, ep_r)
+                ss_valid = fuse and not pending
         if pending:  # the stage's output residual stream
             hip.resid_rmsnorm_partials(hbuf, self.part_k, pending, rows, eps)
         return hbuf

@@ -210,3 +210,45 @@ def test_gemm_sk_argmax(M, N, bn, ws):
     clear = (top.values[:, 0] - top.values[:, 1]) > 1e-3 * top.values[:, 0].abs()
     got = 0xFFFFFFFF - (keys & 0xFFFFFFFF)
     assert bool((got[clear] == top.indices[clear, 0] + 100).all())
+
+
+@pytest.mark.parametrize("M,bn", [(300, 128), (512, 256), (129, 0)])
+def test_gemm_sk_fused_rmsnorm_across_gemms(M, bn, ws):
+    """RMSNorm fused across GEMMs: a residual GEMM writes per-64-column sums of squares of its
+    rounded outputs (ss_out); a SwiGLU / QKV GEMM reading that raw residual stream as A scales
+    each row by rsqrt(mean + eps) from them (ss_in) - against fp32 torch RMSNorm + projection."""
+    from llm_sharding_amd.config import tiny
+    from llm_sharding_amd.models.rope import rope_table
+    h = hip()
+    H, K0, I, eps = 1024, 512, 768, 1e-5
+    x, r = _rnd(M, K0), _rnd(M, H)
+    wo = _rnd(H, K0, scale=0.03)
+    hb = r.clone()
+    ss = torch.full((M, H // 64), float("nan"), device=DEV)
+    h.gemm_sk(x, packing.pack_b(wo), M, H, K0, h.EPI_RESID, h.make_epi(out=hb, resid=hb, ldo=H, ldr=H, ss_out=ss),
+              bn=bn, grid=256 if bn else 0, ws=ws)
+    assert rel_err(hb, r.float() + x.float() @ wo.float().T) < 8e-3
+    assert rel_err(ss, hb.float().pow(2).view(M, H // 64, 64).sum(-1)) < 1e-5
+    hf = hb.float()
+    xn = hf * torch.rsqrt(hf.pow(2).mean(-1, keepdim=True) + eps)
+    # SwiGLU consumer
+    wg, wu = _rnd(I, H, scale=0.03), _rnd(I, H, scale=0.03)
+    out = torch.zeros(M, I, dtype=torch.bfloat16, device=DEV)
+    h.gemm_sk(hb, packing.pack_b(packing.fuse_gate_up(wg, wu)), M, 2 * I, H, h.EPI_SWIGLU,
+              h.make_epi(out=out, ldo=I, ss_in=ss, ss_eps=eps), ws=ws)
+    assert rel_err(out, F.silu(xn @ wg.float().T) * (xn @ wu.float().T)) < 1e-2
+    # QKV consumer (RoPE + KV append after the norm scale)
+    nh, nkv, hd, T = 8, 2, 128, 512
+    wq, wk, wv = _rnd(nh * hd, H, scale=0.03), _rnd(nkv * hd, H, scale=0.03), _rnd(nkv * hd, H, scale=0.03)
+    cos, sin = rope_table(tiny(head_dim=hd), T, DEV)
+    slot = torch.zeros(M, dtype=torch.int32, device=DEV)
+    pos = torch.randperm(T, device=DEV)[:M].to(torch.int32)
+    q = torch.zeros(M, nh * hd, dtype=torch.bfloat16, device=DEV)
+    kc = torch.zeros(1, nkv, T, hd, dtype=torch.bfloat16, device=DEV)
+    vc = torch.zeros_like(kc)
+    h.gemm_sk(hb, packing.pack_b(packing.fuse_qkv(wq, wk, wv, nh, nkv, hd)), M, (nh + 2 * nkv) * hd, H, h.EPI_QKV,
+              h.make_epi(out=q, k_cache=kc, v_cache=vc, slot=slot, pos=pos, cos=cos, sin=sin, ldo=nh * hd, n_heads=nh,
+                         n_kv=nkv, head_dim=hd, t_max=T, ss_in=ss, ss_eps=eps), ws=ws)
+    pl = pos.long()
+    assert rel_err(q, _rope_ref((xn @ wq.float().T).view(M, nh, hd), pl, cos, sin).reshape(M, -1)) < 1e-2
+    assert rel_err(vc[0, :, pl].transpose(0, 1), (xn @ wv.float().T).view(M, nkv, hd)) < 1e-2
