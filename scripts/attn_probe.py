@@ -16,10 +16,11 @@ DEV = "cuda"
 
 
 def main():
-    rows, nh, nkv, hd, tmax = 512, 32, 32, 128, 192
+    rows_list = [int(r) for r in (sys.argv[1].split(",") if len(sys.argv) > 1 else ["512"])]
+    nh, nkv, hd, tmax = 32, 32, 128, 192
     L = hip.lib()
     L.lsa_attn_set_variant.argtypes = [ctypes.c_int]
-    for T in (143, 180):
+    for rows, T in [(r, t) for r in rows_list for t in (143, 180)]:
         kcs = [torch.randn(rows, nkv, tmax, hd, device=DEV).to(torch.bfloat16) for _ in range(3)]
         vcs = [torch.randn_like(k) for k in kcs]
         q = torch.randn(rows, nh * hd, device=DEV).to(torch.bfloat16)
@@ -31,9 +32,9 @@ def main():
         cnt = torch.zeros(rows * nkv, dtype=torch.int32, device=DEV)
         nbytes = rows * nkv * T * hd * 2 * 2
         ref = None
-        for var in (0, 200, 210, 400, 410, 411, 600, 800, 801, 810):
+        for var in (0, 200, 201, 210, 211, 400, 410, 411, 800, 801, 810, 811):
             L.lsa_attn_set_variant(var)
-            for ns in (1, 2):
+            for ns in (1, 2, 4):
                 def run(i):
                     hip.attn(q, kcs[i % 3], vcs[i % 3], slot, pos, rows, nh, nkv, hd, ns, po, pl, out, counters=cnt)
                 run(0)
@@ -52,14 +53,14 @@ def main():
                 e.record()
                 torch.cuda.synchronize()
                 us = s.elapsed_time(e) * 1e3 / n
-                print(json.dumps({"T": T, "variant": var, "nsplit": ns, "us": round(us, 2),
+                print(json.dumps({"rows": rows, "T": T, "variant": var, "nsplit": ns, "us": round(us, 2),
                                   "TBps": round(nbytes / us / 1e6, 3), "relerr_vs_default": float(f"{err:.2e}")}),
                       flush=True)
         L.lsa_attn_set_variant(0)
         del kcs, vcs
         torch.cuda.empty_cache()
     # streaming-read reference: one pass over the same bytes (torch sum of a bf16 buffer)
-    buf = torch.randn(rows * nkv * 143 * hd * 2, device=DEV).to(torch.bfloat16)
+    buf = torch.randn(512 * nkv * 143 * hd * 2, device=DEV).to(torch.bfloat16)
     for _ in range(3):
         buf.sum()
     torch.cuda.synchronize()
