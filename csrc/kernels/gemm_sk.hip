@@ -8,8 +8,10 @@
 //    K step 64, one workgroup per CU, all LDS in ONE __shared__ array.
 //  * Both operands reach LDS by LDS-DMA (global_load_lds_dwordx4): the packed-16x32 weights
 //    (common.h) are already one lane-linear 1 KiB block per (16 cols, 32 k) fragment; the A
-//    tile is gathered in the same fragment order (per-lane source address), so every MFMA
-//    operand read is a conflict-free lane-linear ds_read_b128.
+//    tile is fetched as whole 128-B rows (full cache lines: 5-12 % faster than gathering
+//    fragment-order half lines, scripts/sk_ablate.py) into a row-major image whose 16-B chunks
+//    are XOR-swizzled by row (per-lane source address), so every MFMA operand read is a
+//    conflict-free ds_read_b128.
 //  * Each K-tile runs as 4 phases (one output quadrant of 16 or 8 MFMAs each). The two wave
 //    groups (waves 0-3 / 4-7, i.e. the two waves of every SIMD) run one raw s_barrier apart, so
 //    one wave of a SIMD issues MFMAs while its partner issues LDS reads and DMA.
@@ -70,10 +72,19 @@ struct SkParams {
   int group_m;           // grouped tile order: this many row tiles share a column sweep
 };
 
+// Diagnostic ablation builds only (-DLSA_SK_ABLATE=n, scripts/sk_ablate.py; results are garbage,
+// timings tell what bounds the main loop): 1 = no counted DMA waits in the loop, 2 = no DMA,
+// 5 = A gathered as half-line fragment blocks (the pre-swizzle layout; reads then mismatch),
+// 6 = no A DMA, 7 = no weight DMA,
+// 3 = no MFMA, 4 = no barriers in the loop. The production library never defines it.
+#ifndef LSA_SK_ABLATE
+#define LSA_SK_ABLATE 0
+#endif
+
 // counted wait on the DMA queue (no other vector-memory op is in flight in the main loop)
 template <int N>
 LSA_DEVICE void vm_wait() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+  if constexpr (LSA_SK_ABLATE != 1 || N == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
 }
 
 // Diagnostic build only (-DLSA_GEMM_STAMPS, scripts/gemm_stamps.py): per-workgroup
@@ -97,8 +108,13 @@ LSA_DEVICE void barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+LSA_DEVICE void loop_barrier() {
+  if constexpr (LSA_SK_ABLATE != 4) barrier();
+}
+
 LSA_DEVICE void glds16(const void* src, unsigned char* lds_base) {
-  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
+  if constexpr (LSA_SK_ABLATE != 2)
+    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
 }
 
 // tile id -> (row tile, col tile): group_m row tiles sweep the column tiles together so the
@@ -128,7 +144,8 @@ struct Kern {
   const SkParams* p;
 
   // ---- DMA staging of one LDS region of local K-tile t ------------------------------------------
-  // A region mh: blocks (wr', i, kf) = rows wr'*TM + mh*TM/2 + i*16 + (lane&15), k kt*64+kf*32+8*(lane>>4)
+  // A region mh: the 128 rows wr'*TM + mh*TM/2 + i*16 + r16 (ordered (wr', i, r16)), 128 B each,
+  // 16-B chunks XOR-swizzled by row%8; each DMA instruction fetches 8 whole rows (full lines)
   // Sources = wave-uniform segment base (SGPRs) + 32-bit per-lane offset (one VGPR per block
   // instead of a 64-bit pointer: the 256-wide tile needs every register it can keep).
   const unsigned char* a_seg;
@@ -136,12 +153,14 @@ struct Kern {
   LSA_DEVICE void stage_a(int buf, int mh, const unsigned (&aoff)[2][AGL], int kt) {
     unsigned char* dst = smem + buf * BUF + mh * AREG;
     const unsigned char* base = a_seg + (size_t)kt * (BK * 2);
+    if constexpr (LSA_SK_ABLATE == 6) return;
 #pragma unroll
     for (int s = 0; s < AGL; ++s) glds16(base + aoff[mh][s], dst + (w * AGL + s) * 1024);
   }
   LSA_DEVICE void stage_b(int buf, int nh, const unsigned (&boff)[2][BGL], int kt) {
     unsigned char* dst = smem + buf * BUF + 2 * AREG + nh * BREG;
     const unsigned char* base = b_seg + (size_t)kt * 2048;
+    if constexpr (LSA_SK_ABLATE == 7) return;
 #pragma unroll
     for (int s = 0; s < BGL; ++s)
       if (s < BGL_LO || w < BHI_WAVES) glds16(base + boff[nh][s], dst + (s * 8 + w) * 1024);
@@ -179,10 +198,18 @@ struct Kern {
     for (int mh = 0; mh < 2; ++mh)
 #pragma unroll
       for (int s = 0; s < AGL; ++s) {
-        const int b = w * AGL + s, kf = b & 1, wi = b >> 1;
-        const int wr_ = wi / HM, i = wi % HM;
-        const int row = min(m0 + wr_ * TM + mh * (TM / 2) + i * 16 + (lane & 15), P.M - 1) - m0;
-        aoff[mh][s] = (unsigned)((row * P.lda + kf * 32 + 8 * (lane >> 4)) * 2);
+        // block b = 8 whole 128-B rows (full cache lines) of the region's row-major image, rows
+        // ordered (wr', i, r16); lane -> row b*8 + lane/8, physical 16-B chunk lane%8 holding
+        // logical chunk (lane%8) ^ (row%8) (XOR swizzle: conflict-free fragment reads in rd_a)
+        const int b = w * AGL + s, wi = b >> 1, r16 = (b & 1) * 8 + (lane >> 3);
+        const int wr_ = wi / HM, i = wi % HM, ch = (lane & 7) ^ ((lane >> 3) & 7);
+        if constexpr (LSA_SK_ABLATE == 5) {  // (pre-swizzle fragment-order gather, half lines)
+          const int row = min(m0 + wr_ * TM + mh * (TM / 2) + i * 16 + (lane & 15), P.M - 1) - m0;
+          aoff[mh][s] = (unsigned)((row * P.lda + (b & 1) * 32 + 8 * (lane >> 4)) * 2);
+          continue;
+        }
+        const int row = min(m0 + wr_ * TM + mh * (TM / 2) + i * 16 + r16, P.M - 1) - m0;
+        aoff[mh][s] = (unsigned)((row * P.lda + ch * 8) * 2);
       }
     const int nt16_last = (P.N >> 4) - 1 - (n0 >> 4);  // partial last column tile (BN = 192): clamp
 #pragma unroll
@@ -219,12 +246,16 @@ struct Kern {
     LSA_STAMP(stamp_base + 1);
 
     u32x4_t a[HM][2], b0[HN][2], b1[HN][2];
+    // A fragment (row lane%16, k kf*32 + 8*(lane/16)) in the swizzled row-major image
+    const unsigned roff0 = (lane & 15) * 128 + (((lane >> 4) ^ (lane & 7)) * 16);
+    const unsigned roff1 = (lane & 15) * 128 + (((4 + (lane >> 4)) ^ (lane & 7)) * 16);
     auto rd_a = [&](int buf, int mh) {
-      const unsigned char* src = smem + buf * BUF + mh * AREG + lane * 16;
+      const unsigned char* src = smem + buf * BUF + mh * AREG;
 #pragma unroll
-      for (int i = 0; i < HM; ++i)
-#pragma unroll
-        for (int kf = 0; kf < 2; ++kf) a[i][kf] = ld16(src + ((wr * HM + i) * 2 + kf) * 1024);
+      for (int i = 0; i < HM; ++i) {
+        a[i][0] = ld16(src + (wr * HM + i) * 2048 + roff0);
+        a[i][1] = ld16(src + (wr * HM + i) * 2048 + roff1);
+      }
     };
     auto rd_b = [&](int buf, int nh, u32x4_t (&bb)[HN][2]) {
       const unsigned char* src = smem + buf * BUF + 2 * AREG + nh * BREG + lane * 16;
@@ -237,13 +268,23 @@ struct Kern {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_setprio(1);
+      if constexpr (LSA_SK_ABLATE == 3) {
 #pragma unroll
-      for (int kf = 0; kf < 2; ++kf)
+        for (int kf = 0; kf < 2; ++kf) {
 #pragma unroll
-        for (int i = 0; i < HM; ++i)
+          for (int i = 0; i < HM; ++i) asm volatile("" ::"v"(a[i][kf]));
 #pragma unroll
-          for (int j = 0; j < HN; ++j)
-            acc[mh * HM + i][nh * HN + j] = mfma16(a[i][kf], bb[j][kf], acc[mh * HM + i][nh * HN + j]);
+          for (int j = 0; j < HN; ++j) asm volatile("" ::"v"(bb[j][kf]));
+        }
+      } else {
+#pragma unroll
+        for (int kf = 0; kf < 2; ++kf)
+#pragma unroll
+          for (int i = 0; i < HM; ++i)
+#pragma unroll
+            for (int j = 0; j < HN; ++j)
+              acc[mh * HM + i][nh * HN + j] = mfma16(a[i][kf], bb[j][kf], acc[mh * HM + i][nh * HN + j]);
+      }
       __builtin_amdgcn_s_setprio(0);
     };
 
@@ -256,23 +297,23 @@ struct Kern {
         rd_a(cur, 0);
         rd_b(cur, 0, b0);
         if (t + 1 < n) { stage_b(nxt, 1, boff, t + 1); wait_tile(); } else vm_wait<0>();
-        barrier();
+        loop_barrier();
         mma(0, b0, 0);
-        barrier();
+        loop_barrier();
         rd_b(cur, 1, b1);
         if (t + 1 < n) { stage_a(nxt, 1, aoff, t + 1); wait_tile(); } else vm_wait<0>();
-        barrier();
+        loop_barrier();
         mma(0, b1, 1);
-        barrier();
+        loop_barrier();
         rd_a(cur, 1);
         if (t + 2 < n) { stage_a(cur, 0, aoff, t + 2); wait_tile(); } else vm_wait<0>();
-        barrier();
+        loop_barrier();
         mma(1, b1, 1);
-        barrier();
+        loop_barrier();
         if (t + 2 < n) { stage_b(cur, 0, boff, t + 2); wait_tile(); } else vm_wait<0>();
-        barrier();
+        loop_barrier();
         mma(1, b0, 0);
-        barrier();
+        loop_barrier();
       }
     } else {
       // 3 buffers: tile t+2 is staged during tile t into the buffer tile t-1 used, in read
@@ -283,23 +324,23 @@ struct Kern {
         rd_a(cur, 0);
         rd_b(cur, 0, b0);
         if (st) { stage_a(nx2, 0, aoff, t + 2); vm_wait<NPT + 2 * AGL>(); } else vm_wait<0>();
-        barrier();
+        loop_barrier();
         mma(0, b0, 0);
-        barrier();
+        loop_barrier();
         rd_b(cur, 1, b1);
         if (st) { stage_b(nx2, 0, boff, t + 2); vm_wait<NPT + AGL + BGL>(); } else vm_wait<0>();
-        barrier();
+        loop_barrier();
         mma(0, b1, 1);
-        barrier();
+        loop_barrier();
         rd_a(cur, 1);
         if (st) { stage_b(nx2, 1, boff, t + 2); vm_wait<NPT + 2 * BGL>(); } else vm_wait<0>();
-        barrier();
+        loop_barrier();
         mma(1, b1, 1);
-        barrier();
+        loop_barrier();
         if (st) { stage_a(nx2, 1, aoff, t + 2); vm_wait<NPT + AGL + BGL>(); } else vm_wait<0>();
-        barrier();
+        loop_barrier();
         mma(1, b0, 0);
-        barrier();
+        loop_barrier();
         cur = cur == 2 ? 0 : cur + 1;
         nx2 = nx2 == 2 ? 0 : nx2 + 1;
       }
