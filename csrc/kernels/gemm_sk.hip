@@ -28,19 +28,21 @@
 
 namespace {
 
-constexpr int BM = 256, BK = 64, NTHR = 512;
+constexpr int BK = 64, NTHR = 512;
 
-// BN = 256: 2 x 4 waves of 128 x 64; BN = 192 / 128: 4 x 2 waves of 64 x 96 / 64 x 64.
+// BM x BN tile, BM = 256 or 128 (decode batches of <= 128 rows and M = 384 / 640 ...: no
+// MFMA or A traffic on rows past M). BN = 256: 2 x 4 waves of BM/2 x 64; BN = 192 / 128: 4 x 2
+// waves of BM/4 x 96 / BM/4 x 64.
 // BN = 192 exists for shapes where 256-wide tiles leave CUs idle or need split-K fixups
 // (Llama-2-7B qkv N=12288 at M=512: 2 x 64 = 128 tiles; gate_up N=22016: 230 tiles in one
 // round at full K); N need not be a multiple of 192 (the last column tile is partial).
-template <int BN, int NB>
+template <int BM, int BN, int NB>
 struct Geo {
   static constexpr int WM = BN == 256 ? 2 : 4;   // wave grid
   static constexpr int WN = 8 / WM;
   static constexpr int TM = BM / WM, TN = BN / WN;  // per-wave output tile
   static constexpr int FM = TM / 16, FN = TN / 16;  // 16x16 MFMA tiles per wave
-  static constexpr int AREG = (BM / 2) * BK * 2;    // bytes of one A region (16 KiB)
+  static constexpr int AREG = (BM / 2) * BK * 2;    // bytes of one A region (16 / 8 KiB)
   static constexpr int BREG = (BN / 2) * BK * 2;    // bytes of one B region
   static constexpr int BUF = 2 * AREG + 2 * BREG;   // one K-tile
   static constexpr int AGL = AREG / 1024 / 8;       // DMA instructions per wave per A region
@@ -50,18 +52,20 @@ struct Geo {
   static constexpr int BGL = (BBLK + 7) / 8, BGL_LO = BBLK / 8, BHI_WAVES = BBLK % 8;
   static constexpr int NPT = 2 * AGL + 2 * BGL;     // DMA instructions per K-tile, waves < BHI_WAVES
   static constexpr int NPT_LO = 2 * AGL + 2 * BGL_LO;  // ... the other waves
-  static constexpr int EROWS = TN > 64 ? 32 : 64;   // rows per epilogue transpose pass
+  static constexpr int EROWS = (TN > 64 || TM < 64) ? 32 : 64;  // rows per epilogue transpose pass
   static constexpr int ELD = TN + 4;                // fp32 row stride of the transpose image
   static constexpr int EPI_BYTES = 8 * EROWS * ELD * 4;
   static constexpr int RS_OFF = (NB * BUF > EPI_BYTES ? NB * BUF : EPI_BYTES);  // per-wave row rstd [8][EROWS]
   static constexpr int SMEM = RS_OFF + 8 * EROWS * 4 + 16;
   static_assert(SMEM <= 160 * 1024, "LDS budget");
   static_assert(BHI_WAVES == 0 || BGL_LO == 0 || BHI_WAVES == 4, "B blocks per wave");
+  static_assert(AGL >= 1 && TM % EROWS == 0 && FM % 2 == 0, "tile geometry");
+  static_assert(NB == 2 || BHI_WAVES == 0, "3-buffer ring needs the same DMA count in every wave");
 };
 
 struct SkParams {
   int M, N, K, lda;
-  int MT, NT, NKT;       // 256-row tiles, BN-col tiles, 64-deep K tiles
+  int MT, NT, NKT;       // BM-row tiles, BN-col tiles, 64-deep K tiles
   int G;                 // workgroups
   int dp_rounds;         // full rounds of whole tiles (tile r*G + g)
   int sk_tiles;          // tiles after the data-parallel rounds (the remainder)
@@ -75,7 +79,8 @@ struct SkParams {
 // Diagnostic ablation builds only (-DLSA_SK_ABLATE=n, scripts/sk_ablate.py; results are garbage,
 // timings tell what bounds the main loop): 1 = no counted DMA waits in the loop, 2 = no DMA,
 // 5 = A gathered as half-line fragment blocks (the pre-swizzle layout; reads then mismatch),
-// 6 = no A DMA, 7 = no weight DMA,
+// 6 = no A DMA, 7 = no weight DMA, 8 = DMA only (no LDS reads, no MFMA), 9 = non-temporal
+// weight DMA,
 // 3 = no MFMA, 4 = no barriers in the loop. The production library never defines it.
 #ifndef LSA_SK_ABLATE
 #define LSA_SK_ABLATE 0
@@ -116,6 +121,12 @@ LSA_DEVICE void glds16(const void* src, unsigned char* lds_base) {
   if constexpr (LSA_SK_ABLATE != 2)
     __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
 }
+LSA_DEVICE void glds16_w(const void* src, unsigned char* lds_base) {  // weight stream
+  if constexpr (LSA_SK_ABLATE == 9)
+    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_base, 16, 0, 2 /* nt */);
+  else
+    glds16(src, lds_base);
+}
 
 // tile id -> (row tile, col tile): group_m row tiles sweep the column tiles together so the
 // A panels and the weight panels of a round of 256 tiles both stay in L2 / the Infinity Cache
@@ -128,9 +139,9 @@ LSA_DEVICE void tile_coords(const SkParams& p, int tile, int& mt, int& nt) {
   nt = r / gm;
 }
 
-template <int BN, int EPI, int NB>
+template <int BM, int BN, int EPI, int NB>
 struct Kern {
-  using G_ = Geo<BN, NB>;
+  using G_ = Geo<BM, BN, NB>;
   static constexpr int WM = G_::WM, WN = G_::WN, TM = G_::TM, TN = G_::TN, FM = G_::FM, FN = G_::FN;
   static constexpr int AREG = G_::AREG, BREG = G_::BREG, BUF = G_::BUF, AGL = G_::AGL, BGL = G_::BGL,
                        NPT = G_::NPT, NPT_LO = G_::NPT_LO, BGL_LO = G_::BGL_LO, BHI_WAVES = G_::BHI_WAVES,
@@ -163,7 +174,7 @@ struct Kern {
     if constexpr (LSA_SK_ABLATE == 7) return;
 #pragma unroll
     for (int s = 0; s < BGL; ++s)
-      if (s < BGL_LO || w < BHI_WAVES) glds16(base + boff[nh][s], dst + (s * 8 + w) * 1024);
+      if (s < BGL_LO || w < BHI_WAVES) glds16_w(base + boff[nh][s], dst + (s * 8 + w) * 1024);
   }
   // counted wait keeping one K-tile of this wave's DMA in flight (+ EXTRA instructions)
   template <int EXTRA = 0>
@@ -250,6 +261,7 @@ struct Kern {
     const unsigned roff0 = (lane & 15) * 128 + (((lane >> 4) ^ (lane & 7)) * 16);
     const unsigned roff1 = (lane & 15) * 128 + (((4 + (lane >> 4)) ^ (lane & 7)) * 16);
     auto rd_a = [&](int buf, int mh) {
+      if constexpr (LSA_SK_ABLATE == 8) return;
       const unsigned char* src = smem + buf * BUF + mh * AREG;
 #pragma unroll
       for (int i = 0; i < HM; ++i) {
@@ -258,6 +270,7 @@ struct Kern {
       }
     };
     auto rd_b = [&](int buf, int nh, u32x4_t (&bb)[HN][2]) {
+      if constexpr (LSA_SK_ABLATE == 8) return;
       const unsigned char* src = smem + buf * BUF + 2 * AREG + nh * BREG + lane * 16;
 #pragma unroll
       for (int j = 0; j < HN; ++j)
@@ -268,7 +281,7 @@ struct Kern {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_setprio(1);
-      if constexpr (LSA_SK_ABLATE == 3) {
+      if constexpr (LSA_SK_ABLATE == 3 || LSA_SK_ABLATE == 8) {
 #pragma unroll
         for (int kf = 0; kf < 2; ++kf) {
 #pragma unroll
@@ -365,32 +378,39 @@ struct Kern {
   // read sc1: they bypass this CU's L1, which may hold stale copies). Caller: every wave, LDS
   // free (and a barrier before the LDS is reused by other waves).
   LSA_DEVICE void slab_add(const float* slab, size_t slot, f32x4_t (&acc)[FM][FN]) {
-    constexpr int RP = FN > 4 ? 1 : 2, NP = FM / RP, PB = RP * FN;  // tile rows / pass, passes, blocks / pass
+    // RP tile rows (PB blocks) per pass, NP passes, DB ring buffers per wave: as much in flight
+    // as this geometry's LDS allows (the ring must stay below the flag word at SMEM - 16)
+    constexpr int AVAIL = G_::SMEM - 16;
+    constexpr int RP = (FN <= 4 && FM % 2 == 0 && 8 * 2 * 2 * FN * 1024 <= AVAIL) ? 2 : 1;
+    constexpr int NP = FM / RP, PB = RP * FN;
+    constexpr int DB = (NP > 1 && 8 * 2 * PB * 1024 <= AVAIL) ? 2 : 1;
+    static_assert(8 * DB * PB * 1024 <= AVAIL, "slab ring exceeds the LDS allocation");
     const unsigned char* src = reinterpret_cast<const unsigned char*>(slab + slot * (size_t)(BM * BN)) +
                                (size_t)(w * FM * FN) * 1024 + lane * 16;
-    unsigned char* ring = smem + w * (2 * PB * 1024);
+    unsigned char* ring = smem + w * (DB * PB * 1024);
     auto issue = [&](int pass) {
 #pragma unroll
       for (int q = 0; q < PB; ++q)
         __builtin_amdgcn_global_load_lds(src + ((pass * RP + q / FN) * FN + q % FN) * 1024,
-                                         (__attribute__((address_space(3))) void*)(ring + ((pass & 1) * PB + q) * 1024),
+                                         (__attribute__((address_space(3))) void*)(ring + ((pass % DB) * PB + q) * 1024),
                                          16, 0, 16 /* sc1 */);
     };
     issue(0);
 #pragma unroll
     for (int pass = 0; pass < NP; ++pass) {
-      if (pass + 1 < NP) {
+      if (DB == 2 && pass + 1 < NP) {
         issue(pass + 1);
         vm_wait<PB>();
       } else {
         vm_wait<0>();
       }
-      const unsigned char* rb = ring + (pass & 1) * PB * 1024 + lane * 16;
+      const unsigned char* rb = ring + (pass % DB) * PB * 1024 + lane * 16;
 #pragma unroll
       for (int q = 0; q < PB; ++q)
         acc[pass * RP + q / FN][q % FN] += __builtin_bit_cast(f32x4_t, ld16(rb + q * 1024));
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads retired before the buffer is refilled
       __builtin_amdgcn_sched_barrier(0);
+      if (DB == 1 && pass + 1 < NP) issue(pass + 1);
     }
   }
 
@@ -540,12 +560,12 @@ struct Kern {
   }
 };
 
-template <int BN, int EPI, int NB>
+template <int BM, int BN, int EPI, int NB>
 __global__ __launch_bounds__(NTHR) void gemm_sk_kernel(const bf16_raw* __restrict__ A, const bf16_raw* __restrict__ W,
                                                         SkParams prm, EpiArgs ep, float* __restrict__ slab,
                                                         unsigned* __restrict__ counters) {
-  using K_ = Kern<BN, EPI, NB>;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[Geo<BN, NB>::SMEM];
+  using K_ = Kern<BM, BN, EPI, NB>;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[Geo<BM, BN, NB>::SMEM];
   K_ k;
   k.smem = smem;
   k.A = A;
@@ -578,7 +598,7 @@ __global__ __launch_bounds__(NTHR) void gemm_sk_kernel(const bf16_raw* __restric
   // this workgroup's stream-K iterations [lo, hi) of the remaining tiles' K loops.
   const long long S = (long long)prm.sk_tiles * prm.NKT;
   const long long lo = prm.sk_tiles ? (long long)g * S / G : 0, hi = prm.sk_tiles ? (long long)(g + 1) * S / G : 0;
-  int* flag = reinterpret_cast<int*>(smem + Geo<BN, NB>::SMEM - 16);
+  int* flag = reinterpret_cast<int*>(smem + Geo<BM, BN, NB>::SMEM - 16);
   int r = 0;
   long long it = lo;
   bool split_done = false;
@@ -666,31 +686,48 @@ __global__ __launch_bounds__(NTHR) void gemm_sk_kernel(const bf16_raw* __restric
   }
 }
 
-template <int BN, int EPI, int NB>
+template <int BM, int BN, int EPI, int NB>
 int launch(const bf16_raw* A, const bf16_raw* W, const SkParams& prm, const EpiArgs& ep, float* slab,
            unsigned* cnt, hipStream_t s) {
-  gemm_sk_kernel<BN, EPI, NB><<<prm.G, NTHR, 0, s>>>(A, W, prm, ep, slab, cnt);
+  gemm_sk_kernel<BM, BN, EPI, NB><<<prm.G, NTHR, 0, s>>>(A, W, prm, ep, slab, cnt);
   LSA_CHECK_LAUNCH();
   return LSA_OK;
 }
 
+template <int BM, int EPI>
+int dispatch(const bf16_raw* A, const bf16_raw* W, const SkParams& prm, const EpiArgs& ep, float* slab,
+             unsigned* cnt, int bn, int nb, hipStream_t s) {
+  if (bn == 256) {
+    if constexpr (BM == 128) {
+      if (nb == 3) return launch<BM, 256, EPI, 3>(A, W, prm, ep, slab, cnt, s);
+    }
+    return launch<BM, 256, EPI, 2>(A, W, prm, ep, slab, cnt, s);
+  }
+  if (bn == 192) return launch<BM, 192, EPI, 2>(A, W, prm, ep, slab, cnt, s);
+  return nb == 3 ? launch<BM, 128, EPI, 3>(A, W, prm, ep, slab, cnt, s) : launch<BM, 128, EPI, 2>(A, W, prm, ep, slab, cnt, s);
+}
+
 }  // namespace
 
-// bn: tile width 256 / 192 (2-buffer DMA ring; 192: N % 16 == 0, partial last tile) or 128 (nb = 2
-// or 3 buffers; 0 = 3); grid: workgroups
-// (<= 1024); dp: 1 = whole tiles in data-parallel rounds first (0 = all tiles are remainder);
+// bm: tile height 256 or 128. bn: tile width 256 / 192 (192: N % 16 == 0, partial last tile) / 128.
+// nb: DMA ring buffers, 2 or 3 (3 for bn 128, and bn 256 at bm 128; 0 = the default: 3 where
+// allowed). grid: workgroups (<= 1024); dp: 1 = whole tiles in data-parallel rounds first (0 =
+// all tiles are remainder).
 // epi EPI_PARTIAL: every tile split into exactly `split` K ranges (tiles * split <= grid), fp32
-// partial k stored to ((float*)ep->out)[k][M][ldo], no slabs or tickets (lsa_resid_rmsnorm_partials sums them);
+// partial k stored to ((float*)ep->out)[k][M][ldo], no slabs or tickets (lsa_resid_rmsnorm_partials sums them).
 // split: 0 = remainder by stream-K, S >= 1 = remainder tiles split into up to S K ranges
-// (clamped to NKT and to grid / remainder tiles; stream-K when the remainder exceeds the grid); slab: >= 2 * grid * 256 * bn floats and counters: >= remainder tiles (zeroed) when
-// any tile is split. Returns LSA_BAD_SHAPE on any shape the kernel's indexing cannot take.
+// (clamped to NKT and to grid / remainder tiles; stream-K when the remainder exceeds the grid).
+// slab: >= 2 * grid * bm * bn floats and counters: >= remainder tiles (zeroed) when any tile is
+// split. Returns LSA_BAD_SHAPE on any shape the kernel's indexing cannot take.
 extern "C" int lsa_gemm_sk(const void* a, int lda, const void* wp, int M, int N, int K, int epi,
-                           const EpiArgs* ep, int bn, int nb, int grid, int dp, int split, int group_m, float* slab,
+                           const EpiArgs* ep, int bm, int bn, int nb, int grid, int dp, int split, int group_m, float* slab,
                            unsigned* counters, long long slab_floats, int n_counters, hipStream_t stream) {
   if (M < 1 || K < BK || K % BK || lda < K || lda % 8 || !ep) return LSA_BAD_SHAPE;
   if (bn != 256 && bn != 192 && bn != 128) return LSA_UNSUPPORTED;
-  if (nb == 0) nb = bn == 128 ? 3 : 2;
-  if (nb != 2 && !(nb == 3 && bn == 128)) return LSA_UNSUPPORTED;
+  if (bm != 256 && bm != 128) return LSA_UNSUPPORTED;
+  const int BM = bm;
+  if (nb == 0) nb = (bn == 128 || (bm == 128 && bn == 256)) ? 3 : 2;
+  if (nb != 2 && !(nb == 3 && (bn == 128 || (bm == 128 && bn == 256)))) return LSA_UNSUPPORTED;
   if (bn == 192 ? (N % 16 || (epi == EPI_SWIGLU && N % 32)) : N % bn) return LSA_BAD_SHAPE;
   if (grid < 1 || grid > 1024 || group_m < 1) return LSA_BAD_SHAPE;
   if (epi == EPI_RESID && !ep->resid) return LSA_BAD_SHAPE;
@@ -741,10 +778,8 @@ extern "C" int lsa_gemm_sk(const void* a, int lda, const void* wp, int M, int N,
     return LSA_BAD_SHAPE;
   const bf16_raw* A = static_cast<const bf16_raw*>(a);
   const bf16_raw* W = static_cast<const bf16_raw*>(wp);
-#define LSA_G(E) (bn == 256 ? launch<256, E, 2>(A, W, prm, *ep, slab, counters, stream)      \
-                 : bn == 192 ? launch<192, E, 2>(A, W, prm, *ep, slab, counters, stream)   \
-                          : nb == 3 ? launch<128, E, 3>(A, W, prm, *ep, slab, counters, stream) \
-                                    : launch<128, E, 2>(A, W, prm, *ep, slab, counters, stream))
+#define LSA_G(E) (bm == 256 ? dispatch<256, E>(A, W, prm, *ep, slab, counters, bn, nb, stream) \
+                    : dispatch<128, E>(A, W, prm, *ep, slab, counters, bn, nb, stream))
   switch (epi) {
     case EPI_STORE: return LSA_G(EPI_STORE);
     case EPI_RESID: return LSA_G(EPI_RESID);

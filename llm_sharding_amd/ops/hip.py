@@ -73,7 +73,7 @@ def lib() -> ctypes.CDLL:
                                         vp, vp, i, i, vp, i, vp, vp, i, vp]
     L.lsa_argmax_finalize.argtypes = [vp, i, vp, vp, i, vp, i, i, vp, vp]
     L.lsa_pos_advance.argtypes = [vp, i, i, vp]
-    L.lsa_gemm_sk.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(EpiArgs), i, i, i, i, i, i, vp, vp, ctypes.c_longlong, i,
+    L.lsa_gemm_sk.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(EpiArgs), i, i, i, i, i, i, i, vp, vp, ctypes.c_longlong, i,
                               vp]
     for name in ("lsa_gemv", "lsa_gemv_coop", "lsa_gemv_fp8", "lsa_dequant_fp8_packed", "lsa_gemv_coop_fp8", "lsa_gemm",
                  "lsa_gemm_sk", "lsa_attn_decode", "lsa_attn_prefill", "lsa_embed", "lsa_rmsnorm", "lsa_layernorm",
@@ -331,7 +331,7 @@ def gemm(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep
     _check(rc, "lsa_gemm")
 
 
-SK_BM = 256  # gemm_sk.hip row tile
+SK_BM = 256  # gemm_sk.hip row tile (default; 128-row tiles for small / odd M: plan field bm)
 
 
 class SkWorkspace:
@@ -390,49 +390,53 @@ def _sk_partial() -> dict:
 
 
 def gemm_sk_plan(M: int, N: int, K: int, tuned: bool = True) -> tuple:
-    """(bn, grid, dp, split) for ``gemm_sk``. Grid = one workgroup per CU (the kernel holds
+    """(bn, grid, dp, split, bm) for ``gemm_sk``. Grid = one workgroup per CU (the kernel holds
     ~136-144 KiB of LDS). Whole tiles go out in data-parallel rounds; the remainder either as
     equal K splits (concurrent workgroups stream the same K offsets: L2 reuse) or by stream-K.
 
     ``tuned``: a shape measured by scripts/tune_gemm_sk.py (same N, K and the same number of
-    256-row tiles, nearest M) takes its measured winner. Otherwise a cost model: per 64-deep K
+    128-row tiles, nearest M) takes its measured winner (bm = 256 unless the entry says 128). Otherwise a cost model: per 64-deep K
     step ~1.5 us for a 256x256 tile, ~1.1 us for 256x128 (scripts/bench_gemm_sk.py); stream-K's
     staggered K offsets lose ~2x of that to L2 misses; every extra partial costs one 256 x bn
     fp32 slab read (~100 GB/s per workgroup)."""
-    mt = -(-M // SK_BM)
     if tuned:
-        cands = [(abs(m - M), cfg) for m, cfg in _sk_tuned().get((N, K), ()) if -(-m // SK_BM) == mt]
+        m128 = -(-M // 128)
+        cands = [(abs(m - M), cfg) for m, cfg in _sk_tuned().get((N, K), ()) if -(-m // 128) == m128]
         if cands:
             cfg = min(cands)[1]
             if N % (16 if cfg[0] == 192 else cfg[0]) == 0:
-                return (cfg[0], N_CU, cfg[2], cfg[3])
+                return (cfg[0], N_CU, cfg[2], cfg[3], cfg[4] if len(cfg) > 4 else SK_BM)
     nkt = K // 64
     best = None
-    for bn, c_it in ((256, 1.5), (192, 1.2), (128, 1.1)):
-        if N % (16 if bn == 192 else bn):
-            continue
-        tiles = mt * -(-N // bn)
-        rounds, rem = divmod(tiles, N_CU)
-        slab_us = SK_BM * bn * 4 / 100e3
-        cands = [(rounds * nkt * c_it if rem == 0 else float("inf"), (bn, N_CU, 1, 0))]
-        if rem:
-            for sp in range(1, min(8, nkt, N_CU // rem) + 1):
-                t = (rounds * nkt + -(-nkt // sp)) * c_it + (sp - 1) * slab_us
-                cands.append((t, (bn, N_CU, 1, sp)))
-            per = rem * nkt / N_CU
-            cands.append(((rounds * nkt + per) * c_it + per * c_it + 2 * slab_us, (bn, N_CU, 1, 0)))
-        for c in cands:
-            if best is None or c[0] < best[0]:
-                best = c
+    # per 64-deep K step: 256 x bn tiles ~1.5 / 1.2 / 1.1 us, 128 x bn ~0.55x that
+    for bm, f in ((256, 1.0), (128, 0.55)):
+        mt = -(-M // bm)
+        for bn, c_it in ((256, 1.5 * f), (192, 1.2 * f), (128, 1.1 * f)):
+            if N % (16 if bn == 192 else bn):
+                continue
+            tiles = mt * -(-N // bn)
+            rounds, rem = divmod(tiles, N_CU)
+            slab_us = bm * bn * 4 / 100e3
+            cands = [(rounds * nkt * c_it if rem == 0 else float("inf"), (bn, N_CU, 1, 0, bm))]
+            if rem:
+                for sp in range(1, min(8, nkt, N_CU // rem) + 1):
+                    t = (rounds * nkt + -(-nkt // sp)) * c_it + (sp - 1) * slab_us
+                    cands.append((t, (bn, N_CU, 1, sp, bm)))
+                per = rem * nkt / N_CU
+                cands.append(((rounds * nkt + per) * c_it + per * c_it + 2 * slab_us, (bn, N_CU, 1, 0, bm)))
+            for c in cands:
+                if best is None or c[0] < best[0] - 1e-9:
+                    best = c
     return best[1]
 
 
 def gemm_sk(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep: EpiArgs,
             bn: int = 0, grid: int = 0, dp: int = 1, group_m: int = 8, nb: int = 0, split: int = -1,
-            ws: Optional[SkWorkspace] = None) -> None:
-    """Projection GEMM for any M (gemm_sk.hip): 256 x ``bn`` tiles, LDS-DMA staged, data-parallel
-    rounds + stream-K, fused epilogue. ``wp`` = pack_b(W[N, K]); K % 64 == 0; N % bn == 0 for
-    bn = 128 / 256, N % 16 == 0 for bn = 192 (partial last column tile)."""
+            ws: Optional[SkWorkspace] = None, bm: int = 0) -> None:
+    """Projection GEMM for any M (gemm_sk.hip): ``bm`` x ``bn`` tiles (bm 256 / 128), LDS-DMA
+    staged, data-parallel rounds + stream-K, fused epilogue. ``wp`` = pack_b(W[N, K]); K % 64
+    == 0; N % bn == 0 for bn = 128 / 256, N % 16 == 0 for bn = 192 (partial last column tile).
+    bn = bm = 0: the plan's (gemm_sk_plan)."""
     _req(_is_bf16_cuda(a, wp), "gemm_sk: bf16 cuda tensors required")
     _req(wp.numel() == N * K and K % 64 == 0 and K >= 64, "gemm_sk: packed weight shape")
     _req(a.dim() == 2 and a.shape[0] >= M >= 1 and a.shape[1] >= K and a.stride(1) == 1 and a.stride(0) % 8 == 0,
@@ -442,7 +446,7 @@ def gemm_sk(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int,
     _req(epi in (EPI_STORE, EPI_RESID, EPI_SWIGLU, EPI_QKV, EPI_PARTIAL, EPI_ARGMAX), f"gemm_sk: epilogue {epi} not supported")
     if epi == EPI_PARTIAL:  # exactly `split` K ranges per tile, every tile in one round
         _req(bn in (128, 192, 256) and split >= 1 and grid >= 1, "gemm_sk partial: explicit bn, grid and split required")
-    pb, pg, pd, ps = gemm_sk_plan(M, N, K)
+    pb, pg, pd, ps, pm = gemm_sk_plan(M, N, K)
     if ep.ss_out and pb == 192:  # the fused-norm partials are per 64 columns of one wave (TN = 64)
         pb = 256 if N % 256 == 0 else 128
     if epi == EPI_ARGMAX:
@@ -453,6 +457,8 @@ def gemm_sk(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int,
         ps = split = 1
     if not bn:
         bn, grid, split = pb, grid or pg, ps if split < 0 else split
+        bm = bm or pm
+    bm = bm or SK_BM
     grid = grid or pg
     if split < 0:
         split = 0
@@ -461,9 +467,10 @@ def gemm_sk(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int,
     _req(1 <= grid <= 1024, "gemm_sk: grid")
     if ws is None:
         ws = default_sk_workspace(a.device)
-    _req(ws.slab.numel() >= 2 * grid * SK_BM * bn and ws.counters.numel() >= 2 * grid,
+    _req(bm in (128, 256), "gemm_sk: bm")
+    _req(ws.slab.numel() >= 2 * grid * bm * bn and ws.counters.numel() >= 2 * grid,
          f"gemm_sk: workspace too small for grid={grid} bn={bn}")
-    rc = lib().lsa_gemm_sk(_p(a), a.stride(0), _p(wp), M, N, K, epi, ctypes.byref(ep), bn, nb, grid, dp, split, group_m,
+    rc = lib().lsa_gemm_sk(_p(a), a.stride(0), _p(wp), M, N, K, epi, ctypes.byref(ep), bm, bn, nb, grid, dp, split, group_m,
                            _p(ws.slab), _p(ws.counters), ws.slab.numel(), ws.counters.numel(), _stream())
     _check(rc, "lsa_gemm_sk")
 

@@ -3,7 +3,7 @@
 engine's fused-RMSNorm epilogues: ss_in on qkv / gate_up, ss_out on the residual projections)
 against the cooperative GEMV (gemv_coop.hip, norm folded in), on Llama-2-7B / 70B shapes with
 the real epilogues. Weights rotated beyond the Infinity Cache (bench_kernels.timeit). One JSON
-line per (model, shape, M): coop time, best gemm_sk (bn, split) and every candidate, and the
+line per (model, shape, M): coop time, best gemm_sk (bn, split, bm) and every candidate, and the
 weight-stream rate of each.
 
 usage: gemm_vs_coop.py [models] [rows]      e.g. gemm_vs_coop.py llama2-7b 32,64,96,128"""
@@ -62,16 +62,14 @@ def main():
                     ep_sk = hip.make_epi(out=out, resid=out, ldo=N, ldr=N, ss_out=sso)
                 coop_us = timeit(lambda i: hip.gemv(x, wts[i % nbuf], M, N, K, epi, ep, norm=norm, ws=ws))
                 res = []
-                for bn in (256, 192, 128):
-                    if N % (16 if bn == 192 else bn) or (bn == 192 and epi == hip.EPI_RESID):
-                        continue
-                    for sp in (0, 1, 2, 3, 4, 6, 8):
-                        try:
-                            t = timeit(lambda i: hip.gemm_sk(x, wts[i % nbuf], M, N, K, epi, ep_sk, bn=bn, grid=hip.N_CU,
-                                                              dp=1, split=sp, ws=sk_ws))
-                        except (RuntimeError, ValueError):
+                for bm in (128, 256):
+                    for bn in (256, 192, 128):
+                        if N % (16 if bn == 192 else bn) or (bn == 192 and epi == hip.EPI_RESID):
                             continue
-                        res.append((round(t, 2), bn, sp))
+                        for sp in (0, 1, 2, 3, 4, 6, 8):
+                            t = timeit(lambda i: hip.gemm_sk(x, wts[i % nbuf], M, N, K, epi, ep_sk, bn=bn, grid=hip.N_CU,
+                                                              dp=1, split=sp, ws=sk_ws, bm=bm))
+                            res.append((round(t, 2), bn, sp, bm))
                 res.sort()
                 wb = N * K * 2
                 print(json.dumps({"model": model, "shape": name, "N": N, "K": K, "M": M,

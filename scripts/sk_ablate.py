@@ -2,9 +2,10 @@
 """What bounds gemm_sk's main loop: the same configuration timed (hipGraph, cold weights) on
 ablation builds of gemm_sk.hip (-DLSA_SK_ABLATE=n; outputs are garbage, only the time matters):
 0 = production code, 1 = no counted DMA waits, 2 = no DMA, 3 = no MFMA, 4 = no loop barriers,
-5 = A fetched as whole 128-B rows (wrong layout, same bytes), 6 = no A DMA, 7 = no weight DMA.
+5 = A gathered as half-line fragment blocks (pre-swizzle layout), 6 = no A DMA, 7 = no weight DMA,
+8 = DMA only (no LDS reads, no MFMA), 9 = non-temporal weight DMA.
 
-    python scripts/sk_ablate.py --build                 (CPU host: hipcc the five variants)
+    python scripts/sk_ablate.py --build                 (CPU host: hipcc every variant)
     python scripts/sk_ablate.py M N K bn split [...]    (GPU: one JSON line per config)"""
 import ctypes
 import json
@@ -13,10 +14,10 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7)
+VARIANTS = tuple(range(10))
 
 
-NAMES = ["prod", "no_wait", "no_dma", "no_mfma", "no_barrier", "a_full_lines", "no_a_dma", "no_w_dma"]
+NAMES = ["prod", "no_wait", "no_dma", "no_mfma", "no_barrier", "a_full_lines", "no_a_dma", "no_w_dma", "dma_only", "w_nt"]
 
 
 def so(v):
@@ -44,7 +45,7 @@ def main():
     libs = {}
     for v in VARIANTS:
         L = ctypes.CDLL(so(v))
-        L.lsa_gemm_sk.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(hip.EpiArgs), i, i, i, i, i, i, vp, vp,
+        L.lsa_gemm_sk.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(hip.EpiArgs), i, i, i, i, i, i, i, vp, vp,
                                   ctypes.c_longlong, i, vp]
         libs[v] = L
     ws = hip.SkWorkspace("cuda")
@@ -59,7 +60,7 @@ def main():
         for v, L in libs.items():
             def run(it, L=L):
                 rc = L.lsa_gemm_sk(x.data_ptr(), x.stride(0), wps[it % nbuf].data_ptr(), M, N, K, hip.EPI_STORE,
-                                   ctypes.byref(ep), bn, 0, hip.N_CU, 1, split, 8, ws.slab.data_ptr(),
+                                   ctypes.byref(ep), 256, bn, 0, hip.N_CU, 1, split, 8, ws.slab.data_ptr(),
                                    ws.counters.data_ptr(), ws.slab.numel(), ws.counters.numel(),
                                    torch.cuda.current_stream().cuda_stream)
                 assert rc == 0, rc

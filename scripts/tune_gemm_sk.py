@@ -3,7 +3,8 @@
 runs (QKV: RoPE + KV append, o/down: residual add, gate_up: SwiGLU), weights rotated over
 > 600 MB of copies so they stream from HBM as in a decode step. Residual projections are also
 timed as split-K partials summed by the following norm (EPI_PARTIAL + resid_rmsnorm_partials)
-against the fused EPI_RESID + rmsnorm pair; the winner goes in the entry's "partial" field. Writes the winners to
+against the fused EPI_RESID + rmsnorm pair; the winner goes in the entry's "partial" field. Both row-tile
+heights (bm 256 / 128) are swept. Writes the winners to
 llm_sharding_amd/ops/gemm_sk_tuning.json, which hip.gemm_sk_plan consults before its cost model.
 
 usage: tune_gemm_sk.py [--rows 256,512,...] [--models llama2-7b,...] [--out PATH] [--iters N]
@@ -43,6 +44,7 @@ def main():
     ap.add_argument("--models", default="llama2-7b")
     ap.add_argument("--out", default=os.path.join(ROOT, "llm_sharding_amd", "ops", "gemm_sk_tuning.json"))
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--no-partial", action="store_true", help="skip the EPI_PARTIAL comparison")
     a = ap.parse_args()
     from llm_sharding_amd.config import llama2_7b
     from llm_sharding_amd.models.rope import rope_table
@@ -78,28 +80,30 @@ def main():
                     out = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
                     ep = hip.make_epi(out=out, resid=out, ldo=N, ldr=N)
                 res = []
-                for bn in (256, 192, 128):
-                    if N % (16 if bn == 192 else bn):
-                        continue
-                    for sp in SPLITS:
-                        try:
-                            us = timeit(lambda i: hip.gemm_sk(x, ws[i % nbuf], M, N, K, epi, ep, bn=bn, grid=hip.N_CU,
-                                                              dp=1, split=sp, ws=sk_ws), a.iters)
-                        except (RuntimeError, ValueError) as e:  # a config the host rejects for this shape
-                            print(f"# skip bn={bn} split={sp}: {e}", file=sys.stderr)
+                for bm in (256, 128):
+                    for bn in (256, 192, 128):
+                        if N % (16 if bn == 192 else bn):
                             continue
-                        res.append((round(us, 2), bn, sp))
+                        for sp in SPLITS:
+                            try:
+                                us = timeit(lambda i: hip.gemm_sk(x, ws[i % nbuf], M, N, K, epi, ep, bn=bn, grid=hip.N_CU,
+                                                                  dp=1, split=sp, ws=sk_ws, bm=bm), a.iters)
+                            except (RuntimeError, ValueError) as e:  # a config the host rejects for this shape
+                                print(f"# skip bm={bm} bn={bn} split={sp}: {e}", file=sys.stderr)
+                                continue
+                            res.append((round(us, 2), bn, sp, bm))
                 res.sort()
                 partial = None
-                if epi == hip.EPI_RESID and M <= hip.PARTIAL_MAX_ROWS:
+                if epi == hip.EPI_RESID and 128 < M <= hip.PARTIAL_MAX_ROWS and not a.no_partial:
                     # the engine follows every residual projection with an RMSNorm: compare
                     # fused (EPI_RESID + rmsnorm) against EPI_PARTIAL + resid_rmsnorm_partials
                     xn = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
                     pbuf = torch.zeros(hip.PARTIAL_MAX_SPLIT, M, N, dtype=torch.float32, device=DEV)
-                    bbn, bsp = res[0][1], res[0][2]
+                    bbn, bsp, bbm = res[0][1], res[0][2], res[0][3]
 
                     def fused(i):
-                        hip.gemm_sk(x, ws[i % nbuf], M, N, K, epi, ep, bn=bbn, grid=hip.N_CU, dp=1, split=bsp, ws=sk_ws)
+                        hip.gemm_sk(x, ws[i % nbuf], M, N, K, epi, ep, bn=bbn, grid=hip.N_CU, dp=1, split=bsp, ws=sk_ws,
+                                    bm=bbm)
                         hip.rmsnorm(out, None, xn, M, 1e-5, N)
                     t_fused = timeit(fused, a.iters)
                     pres = []
@@ -120,10 +124,10 @@ def main():
                     pres.sort()
                     partial = {"fused_us": round(t_fused, 2), "best": pres[0] if pres else None, "all": pres}
                 plan = hip.gemm_sk_plan(M, N, K, tuned=False)
-                model_us = next((r[0] for r in res if (r[1], r[2]) == (plan[0], plan[3])), None)
+                model_us = next((r[0] for r in res if (r[1], r[2], r[3]) == (plan[0], plan[3], plan[4])), None)
                 fl = 2.0 * M * N * K
                 line = {"model": model, "shape": name, "N": N, "K": K, "M": M, "epi": epi,
-                        "best_us": res[0][0], "best": [res[0][1], hip.N_CU, 1, res[0][2]],
+                        "best_us": res[0][0], "best": [res[0][1], hip.N_CU, 1, res[0][2], res[0][3]],
                         "best_tflops": round(fl / res[0][0] / 1e6, 1), "cost_model_us": model_us,
                         "all": res, "partial": partial}
                 print(json.dumps(line), flush=True)

@@ -1,4 +1,4 @@
-"""gemm_sk.hip (LDS-DMA 256 x BN tiles, BN = 256 / 192 / 128, data-parallel rounds + stream-K, fused epilogues)
+"""gemm_sk.hip (LDS-DMA BM x BN tiles, BM = 256 / 128, BN = 256 / 192 / 128, data-parallel rounds + stream-K, fused epilogues)
 against plain PyTorch fp32 references: every epilogue, both tile widths, grids that split tiles
 between workgroups (stream-K partial slabs + last-arriver combine) and grids that do not."""
 import pytest
@@ -39,12 +39,15 @@ CFGS = [(0, 0, 1, -1), (256, 256, 1, 0), (128, 256, 1, 0), (256, 37, 0, 0), (128
         (192, 37, 0, 0)]
 
 
+BMS = (256, 128)  # row tile heights (128: decode batches and odd M)
+
+
 def _skip(bn, N):
     """bn = 192 takes any N % 16 == 0 (partial last tile); 128 / 256 need N % bn == 0."""
     return bn and N % (16 if bn == 192 else bn)
 
 
-@pytest.mark.parametrize("M", [1, 129, 256, 300, 512, 777])
+@pytest.mark.parametrize("M", [1, 64, 129, 256, 300, 512, 777])
 @pytest.mark.parametrize("N,K", [(1024, 512), (512, 4096), (768, 1216)])
 def test_gemm_sk_store_resid(M, N, K, ws):
     h = hip()
@@ -53,21 +56,22 @@ def test_gemm_sk_store_resid(M, N, K, ws):
     wp = packing.pack_b(w)
     ref = a.float() @ w.float().T
     r = _rnd(M, N)
-    for (bn, grid, dp, split) in CFGS:
-        if _skip(bn, N):
-            continue
-        nb = 2 if (bn, grid) == (128, 96) else 0
-        tiles = -(-M // 256) * -(-N // (bn or 256))
-        if split > 0 and tiles * split > grid:
-            continue
-        out = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
-        h.gemm_sk(a, wp, M, N, K, h.EPI_STORE, h.make_epi(out=out, ldo=N), bn=bn, grid=grid, dp=dp, split=split,
-                  nb=nb, ws=ws)
-        assert rel_err(out, ref) < 8e-3, (bn, grid, dp, split)
-        o2 = r.clone()
-        h.gemm_sk(a, wp, M, N, K, h.EPI_RESID, h.make_epi(out=o2, resid=o2, ldo=N, ldr=N), bn=bn, grid=grid, dp=dp,
-                  split=split, nb=nb, ws=ws)
-        assert rel_err(o2, r.float() + ref) < 8e-3, (bn, grid, dp, split)
+    for bm in BMS:
+        for (bn, grid, dp, split) in CFGS:
+            if _skip(bn, N) or (bm == 128 and not bn):
+                continue
+            nb = 2 if (bn, grid) == (128, 96) else 0
+            tiles = -(-M // bm) * -(-N // (bn or 256))
+            if split > 0 and tiles * split > grid:
+                continue
+            out = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
+            h.gemm_sk(a, wp, M, N, K, h.EPI_STORE, h.make_epi(out=out, ldo=N), bn=bn, grid=grid, dp=dp, split=split,
+                      nb=nb, ws=ws, bm=bm if bn else 0)
+            assert rel_err(out, ref) < 8e-3, (bm, bn, grid, dp, split)
+            o2 = r.clone()
+            h.gemm_sk(a, wp, M, N, K, h.EPI_RESID, h.make_epi(out=o2, resid=o2, ldo=N, ldr=N), bn=bn, grid=grid, dp=dp,
+                      split=split, nb=nb, ws=ws, bm=bm if bn else 0)
+            assert rel_err(o2, r.float() + ref) < 8e-3, (bm, bn, grid, dp, split)
     assert int(ws.counters.abs().sum()) == 0  # every split tile's ticket was reset
 
 
@@ -84,7 +88,7 @@ def test_gemm_sk_strided_a_and_big_m(ws):
     assert rel_err(out, a.float() @ w.float().T) < 8e-3
 
 
-@pytest.mark.parametrize("M", [200, 512, 1030])
+@pytest.mark.parametrize("M", [96, 200, 512, 1030])
 def test_gemm_sk_swiglu(M, ws):
     h = hip()
     I, H = 1024, 512
@@ -92,14 +96,17 @@ def test_gemm_sk_swiglu(M, ws):
     wg, wu = _rnd(I, H, scale=0.05), _rnd(I, H, scale=0.05)
     wp = packing.pack_b(packing.fuse_gate_up(wg, wu))
     ref = F.silu(x.float() @ wg.float().T) * (x.float() @ wu.float().T)
-    for (bn, grid, dp, split) in CFGS:
-        tiles = -(-M // 256) * -(-2 * I // (bn or 256))
-        if split > 0 and tiles * split > grid:
-            continue
-        out = torch.zeros(M, I, dtype=torch.bfloat16, device=DEV)
-        h.gemm_sk(x, wp, M, 2 * I, H, h.EPI_SWIGLU, h.make_epi(out=out, ldo=I), bn=bn, grid=grid, dp=dp, split=split,
-                  ws=ws)
-        assert rel_err(out, ref) < 1e-2, (bn, grid, dp, split)
+    for bm in BMS:
+        for (bn, grid, dp, split) in CFGS:
+            if bm == 128 and not bn:
+                continue
+            tiles = -(-M // bm) * -(-2 * I // (bn or 256))
+            if split > 0 and tiles * split > grid:
+                continue
+            out = torch.zeros(M, I, dtype=torch.bfloat16, device=DEV)
+            h.gemm_sk(x, wp, M, 2 * I, H, h.EPI_SWIGLU, h.make_epi(out=out, ldo=I), bn=bn, grid=grid, dp=dp,
+                      split=split, ws=ws, bm=bm if bn else 0)
+            assert rel_err(out, ref) < 1e-2, (bm, bn, grid, dp, split)
 
 
 def _rope_ref(t, pos, cos, sin):
@@ -110,7 +117,8 @@ def _rope_ref(t, pos, cos, sin):
 
 
 @pytest.mark.parametrize("nh,nkv,hd", [(32, 32, 128), (8, 2, 64), (24, 8, 128)])
-@pytest.mark.parametrize("cfg", [(0, 0, 1, -1), (128, 29, 0, 0), (256, 256, 1, 3), (192, 256, 1, 2)])
+@pytest.mark.parametrize("cfg", [(0, 0, 1, -1), (128, 29, 0, 0), (256, 256, 1, 3), (192, 256, 1, 2),
+                                 (128, 256, 1, 3, 128), (192, 256, 1, 2, 128), (256, 37, 0, 0, 128)])
 def test_gemm_sk_qkv_rope_kv_append(nh, nkv, hd, cfg, ws):
     from llm_sharding_amd.config import tiny
     from llm_sharding_amd.models.rope import rope_table
@@ -128,10 +136,11 @@ def test_gemm_sk_qkv_rope_kv_append(nh, nkv, hd, cfg, ws):
     N = (nh + 2 * nkv) * hd
     ep = h.make_epi(out=q, k_cache=kc, v_cache=vc, slot=slot, pos=pos, cos=cos, sin=sin, ldo=nh * hd,
                     n_heads=nh, n_kv=nkv, head_dim=hd, t_max=T)
-    bn, grid, dp, split = cfg
+    bn, grid, dp, split = cfg[:4]
     if _skip(bn, N):
         pytest.skip("N not a multiple of bn")
-    h.gemm_sk(x, wp, M, N, H, h.EPI_QKV, ep, bn=bn, grid=grid, dp=dp, split=split, ws=ws)
+    h.gemm_sk(x, wp, M, N, H, h.EPI_QKV, ep, bn=bn, grid=grid, dp=dp, split=split, ws=ws,
+              bm=cfg[4] if len(cfg) > 4 else 0)
     xf, pl, sl = x.float(), pos.long(), slot.long()
     qr = _rope_ref((xf @ wq.float().T).view(M, nh, hd), pl, cos, sin).reshape(M, -1)
     kr = _rope_ref((xf @ wk.float().T).view(M, nkv, hd), pl, cos, sin)
@@ -192,8 +201,9 @@ def test_gemm_sk_partials_resid_rmsnorm(M, N, K, bn, S, ws):
     assert torch.equal(h2, hb)
 
 
-@pytest.mark.parametrize("M,N,bn", [(300, 4096, 256), (512, 32000 // 128 * 128, 0), (777, 2048, 128)])
-def test_gemm_sk_argmax(M, N, bn, ws):
+@pytest.mark.parametrize("M,N,bn,bm", [(300, 4096, 256, 0), (512, 32000 // 128 * 128, 0, 0), (777, 2048, 128, 0),
+                                       (100, 4096, 256, 128), (300, 2048, 128, 128)])
+def test_gemm_sk_argmax(M, N, bn, bm, ws):
     """EPI_ARGMAX (lm_head + greedy argmax keys, 64-bit atomics) against torch.argmax of the fp32
     logits, with a column offset and a -huge bias column, wherever the top-2 margin is clear."""
     h = hip()
@@ -204,7 +214,7 @@ def test_gemm_sk_argmax(M, N, bn, ws):
     bias[7] = -3.0e38
     keys = torch.zeros(M, dtype=torch.int64, device=DEV)
     h.gemm_sk(a, packing.pack_b(w), M, N, K, h.EPI_ARGMAX, h.make_epi(keys=keys, col_offset=100, bias=bias), bn=bn,
-              grid=256 if bn else 0, ws=ws)
+              grid=256 if bn else 0, ws=ws, bm=bm)
     lg = a.float() @ w.float().T + bias
     top = lg.topk(2, dim=-1)
     clear = (top.values[:, 0] - top.values[:, 1]) > 1e-3 * top.values[:, 0].abs()
@@ -212,8 +222,8 @@ def test_gemm_sk_argmax(M, N, bn, ws):
     assert bool((got[clear] == top.indices[clear, 0] + 100).all())
 
 
-@pytest.mark.parametrize("M,bn", [(300, 128), (512, 256), (129, 0)])
-def test_gemm_sk_fused_rmsnorm_across_gemms(M, bn, ws):
+@pytest.mark.parametrize("M,bn,bm", [(300, 128, 0), (512, 256, 0), (129, 0, 0), (96, 128, 128), (200, 256, 128)])
+def test_gemm_sk_fused_rmsnorm_across_gemms(M, bn, bm, ws):
     """RMSNorm fused across GEMMs: a residual GEMM writes per-64-column sums of squares of its
     rounded outputs (ss_out); a SwiGLU / QKV GEMM reading that raw residual stream as A scales
     each row by rsqrt(mean + eps) from them (ss_in) - against fp32 torch RMSNorm + projection."""
@@ -226,7 +236,7 @@ def test_gemm_sk_fused_rmsnorm_across_gemms(M, bn, ws):
     hb = r.clone()
     ss = torch.full((M, H // 64), float("nan"), device=DEV)
     h.gemm_sk(x, packing.pack_b(wo), M, H, K0, h.EPI_RESID, h.make_epi(out=hb, resid=hb, ldo=H, ldr=H, ss_out=ss),
-              bn=bn, grid=256 if bn else 0, ws=ws)
+              bn=bn, grid=256 if bn else 0, ws=ws, bm=bm)
     assert rel_err(hb, r.float() + x.float() @ wo.float().T) < 8e-3
     assert rel_err(ss, hb.float().pow(2).view(M, H // 64, 64).sum(-1)) < 1e-5
     hf = hb.float()
@@ -235,7 +245,7 @@ def test_gemm_sk_fused_rmsnorm_across_gemms(M, bn, ws):
     wg, wu = _rnd(I, H, scale=0.03), _rnd(I, H, scale=0.03)
     out = torch.zeros(M, I, dtype=torch.bfloat16, device=DEV)
     h.gemm_sk(hb, packing.pack_b(packing.fuse_gate_up(wg, wu)), M, 2 * I, H, h.EPI_SWIGLU,
-              h.make_epi(out=out, ldo=I, ss_in=ss, ss_eps=eps), ws=ws)
+              h.make_epi(out=out, ldo=I, ss_in=ss, ss_eps=eps), ws=ws, bn=bn, grid=256 if bn else 0, bm=bm)
     assert rel_err(out, F.silu(xn @ wg.float().T) * (xn @ wu.float().T)) < 1e-2
     # QKV consumer (RoPE + KV append after the norm scale)
     nh, nkv, hd, T = 8, 2, 128, 512
@@ -248,7 +258,8 @@ def test_gemm_sk_fused_rmsnorm_across_gemms(M, bn, ws):
     vc = torch.zeros_like(kc)
     h.gemm_sk(hb, packing.pack_b(packing.fuse_qkv(wq, wk, wv, nh, nkv, hd)), M, (nh + 2 * nkv) * hd, H, h.EPI_QKV,
               h.make_epi(out=q, k_cache=kc, v_cache=vc, slot=slot, pos=pos, cos=cos, sin=sin, ldo=nh * hd, n_heads=nh,
-                         n_kv=nkv, head_dim=hd, t_max=T, ss_in=ss, ss_eps=eps), ws=ws)
+                         n_kv=nkv, head_dim=hd, t_max=T, ss_in=ss, ss_eps=eps), ws=ws, bn=bn, grid=256 if bn else 0,
+              bm=bm)
     pl = pos.long()
     assert rel_err(q, _rope_ref((xn @ wq.float().T).view(M, nh, hd), pl, cos, sin).reshape(M, -1)) < 1e-2
     assert rel_err(vc[0, :, pl].transpose(0, 1), (xn @ wv.float().T).view(M, nkv, hd)) < 1e-2

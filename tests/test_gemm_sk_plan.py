@@ -9,20 +9,21 @@ def test_tuned_shapes_use_the_table():
     assert tab, "ops/gemm_sk_tuning.json missing or empty"
     for (N, K), rows in tab.items():
         for M, cfg in rows:
-            assert hip.gemm_sk_plan(M, N, K) == (cfg[0], hip.N_CU, cfg[2], cfg[3])
+            assert hip.gemm_sk_plan(M, N, K) == (cfg[0], hip.N_CU, cfg[2], cfg[3], cfg[4] if len(cfg) > 4 else 256)
 
 
 def test_nearest_measured_m_with_same_row_tiles():
     tab = hip._sk_tuned()
     rows = dict(tab[(4096, 4096)])
-    # 500 rows -> two 256-row tiles: the M=512 (or 384) entry, never the M=256 one
+    # 500 rows -> four 128-row tiles: the M=512 entry, never the M=384 or M=640 one
     got = hip.gemm_sk_plan(500, 4096, 4096)
-    want = rows[512] if 512 in rows else rows[384]
-    assert got == (want[0], hip.N_CU, want[2], want[3])
+    want = rows[512]
+    assert got == (want[0], hip.N_CU, want[2], want[3], want[4] if len(want) > 4 else 256)
 
 
 def test_cost_model_for_untuned_shapes():
     for M, N, K in [(65536, 12288, 4096), (300, 5120, 3072), (4096, 128, 64)]:
-        bn, grid, dp, split = hip.gemm_sk_plan(M, N, K)
+        bn, grid, dp, split, bm = hip.gemm_sk_plan(M, N, K)
         assert bn in (128, 192, 256) and N % (16 if bn == 192 else bn) == 0 and grid == hip.N_CU and split >= 0
-        assert hip.gemm_sk_plan(M, N, K, tuned=False) == (bn, grid, dp, split) or (N, K) in hip._sk_tuned()
+        assert bm in (128, 256)
+        assert hip.gemm_sk_plan(M, N, K, tuned=False) == (bn, grid, dp, split, bm) or (N, K) in hip._sk_tuned()
