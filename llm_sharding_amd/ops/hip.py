@@ -408,8 +408,9 @@ def gemm_sk_plan(M: int, N: int, K: int, tuned: bool = True) -> tuple:
                 return (cfg[0], N_CU, cfg[2], cfg[3], cfg[4] if len(cfg) > 4 else SK_BM)
     nkt = K // 64
     best = None
-    # per 64-deep K step: 256 x bn tiles ~1.5 / 1.2 / 1.1 us, 128 x bn ~0.55x that
-    for bm, f in ((256, 1.0), (128, 0.55)):
+    # per 64-deep K step: 256 x bn tiles ~1.5 / 1.2 / 1.1 us; 128 x bn ~0.72x that (the step is bound
+    # by the (bm + bn) x 64 operand bytes each workgroup stages, not by its MFMAs)
+    for bm, f in ((256, 1.0), (128, 0.72)):
         mt = -(-M // bm)
         for bn, c_it in ((256, 1.5 * f), (192, 1.2 * f), (128, 1.1 * f)):
             if N % (16 if bn == 192 else bn):
