@@ -80,7 +80,7 @@ struct SkParams {
 // timings tell what bounds the main loop): 1 = no counted DMA waits in the loop, 2 = no DMA,
 // 5 = A gathered as half-line fragment blocks (the pre-swizzle layout; reads then mismatch),
 // 6 = no A DMA, 7 = no weight DMA, 8 = DMA only (no LDS reads, no MFMA), 9 = non-temporal
-// weight DMA,
+// weight DMA, 10 = no LDS reads (DMA + MFMA on stale registers), 11 = MFMA only,
 // 3 = no MFMA, 4 = no barriers in the loop. The production library never defines it.
 #ifndef LSA_SK_ABLATE
 #define LSA_SK_ABLATE 0
@@ -118,7 +118,7 @@ LSA_DEVICE void loop_barrier() {
 }
 
 LSA_DEVICE void glds16(const void* src, unsigned char* lds_base) {
-  if constexpr (LSA_SK_ABLATE != 2)
+  if constexpr (LSA_SK_ABLATE != 2 && LSA_SK_ABLATE != 11)
     __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
 }
 LSA_DEVICE void glds16_w(const void* src, unsigned char* lds_base) {  // weight stream
@@ -261,7 +261,7 @@ struct Kern {
     const unsigned roff0 = (lane & 15) * 128 + (((lane >> 4) ^ (lane & 7)) * 16);
     const unsigned roff1 = (lane & 15) * 128 + (((4 + (lane >> 4)) ^ (lane & 7)) * 16);
     auto rd_a = [&](int buf, int mh) {
-      if constexpr (LSA_SK_ABLATE == 8) return;
+      if constexpr (LSA_SK_ABLATE == 8 || LSA_SK_ABLATE == 10 || LSA_SK_ABLATE == 11) return;
       const unsigned char* src = smem + buf * BUF + mh * AREG;
 #pragma unroll
       for (int i = 0; i < HM; ++i) {
@@ -270,7 +270,7 @@ struct Kern {
       }
     };
     auto rd_b = [&](int buf, int nh, u32x4_t (&bb)[HN][2]) {
-      if constexpr (LSA_SK_ABLATE == 8) return;
+      if constexpr (LSA_SK_ABLATE == 8 || LSA_SK_ABLATE == 10 || LSA_SK_ABLATE == 11) return;
       const unsigned char* src = smem + buf * BUF + 2 * AREG + nh * BREG + lane * 16;
 #pragma unroll
       for (int j = 0; j < HN; ++j)

@@ -3,7 +3,8 @@
 ablation builds of gemm_sk.hip (-DLSA_SK_ABLATE=n; outputs are garbage, only the time matters):
 0 = production code, 1 = no counted DMA waits, 2 = no DMA, 3 = no MFMA, 4 = no loop barriers,
 5 = A gathered as half-line fragment blocks (pre-swizzle layout), 6 = no A DMA, 7 = no weight DMA,
-8 = DMA only (no LDS reads, no MFMA), 9 = non-temporal weight DMA.
+8 = DMA only (no LDS reads, no MFMA), 9 = non-temporal weight DMA, 10 = DMA + MFMA without LDS
+reads, 11 = MFMA only.
 
     python scripts/sk_ablate.py --build                 (CPU host: hipcc every variant)
     python scripts/sk_ablate.py M N K bn split [...]    (GPU: one JSON line per config)"""
@@ -14,10 +15,10 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-VARIANTS = tuple(range(10))
+VARIANTS = tuple(range(12))
 
 
-NAMES = ["prod", "no_wait", "no_dma", "no_mfma", "no_barrier", "a_full_lines", "no_a_dma", "no_w_dma", "dma_only", "w_nt"]
+NAMES = ["prod", "no_wait", "no_dma", "no_mfma", "no_barrier", "a_full_lines", "no_a_dma", "no_w_dma", "dma_only", "w_nt", "dma_mfma_no_reads", "mfma_only"]
 
 
 def so(v):
