@@ -66,6 +66,9 @@ def parse():
                          "pipeline (b1_p50_tpot_ms / b1_tok_s in the JSON line); 0 = skip")
     ap.add_argument("--stage-layers", type=int, default=0,
                     help="profile one pipeline stage: the model cut to this many layers (NOT the headline metric)")
+    ap.add_argument("--transport", default="rccl", choices=("rccl", "ipc"),
+                    help="stage hand-off: rccl (send/recv per ring edge) or ipc (decode messages through "
+                         "IPC-mapped HBM rings with device flags, parallel/ipc_ring.py; prefill stays on RCCL)")
     ap.add_argument("--device", default="cuda", choices=("cuda", "cpu"),
                     help="cpu: the same schedule on gloo + the torch CPU path (multi-rank rehearsal)")
     return ap.parse_args()
@@ -128,7 +131,8 @@ def main():
                                batch=a.batch, prompt_len=a.prompt_len, max_seq=a.max_seq,
                                microbatches=a.microbatches, seed=a.seed, use_graph=not a.no_graph,
                                weight_dtype=a.weight_dtype, streams=a.streams, dp=a.dp,
-                               latency_steps=a.latency_steps, device=a.device, stage_layers=a.stage_layers)
+                               latency_steps=a.latency_steps, device=a.device, stage_layers=a.stage_layers,
+                               transport=a.transport)
     if res is None:  # non-zero ranks
         return
     line = {

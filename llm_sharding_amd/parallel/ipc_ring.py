@@ -1,0 +1,214 @@
+"""Stage-to-stage hand-off through IPC-mapped rings in HBM (csrc/kernels/ipc_ring.hip).
+
+The p2p transport the pipeline plugs in beside :class:`~.pipeline.DistP2P` (RCCL) and
+:class:`~.pipeline.LocalP2P`: ``isend(t, dst)`` / ``recv(t, src)`` with the same stream
+semantics, but each is ONE kernel on the caller's stream that moves the bytes over xGMI into a
+ring slot in the receiver's HBM and signals with device flags - no communicator, no proxy
+thread, nothing host-side per message. Every index the kernels use lives in device memory, so a
+send / receive can be captured inside a hipGraph with the decode step it feeds (SURVEY.md §5.8,
+the graph-captured IPC hand-off; the reference's hop is ZMQ + torch.save through a file:
+/root/reference/utils/node_worker.py:44-67).
+
+Per directed edge ``src -> dst`` (default: the pipeline ring r -> r+1 plus the back-edge):
+  * dst allocates the inbox (R flag words + R slots of ``slot_bytes``), src the ack box (R words);
+  * handles go through one ``all_gather_object`` on a gloo group (a control-plane exchange at
+    construction only); each side maps the other's buffer with ``hipIpcOpenMemHandle``.
+A message must be a multiple of 4 bytes and at most ``slot_bytes``. Up to R messages per edge
+are in flight; a sender that runs R ahead waits in-kernel for the receiver's ack. Every spin is
+bounded (``timeout_s``); :meth:`check` raises if any launch timed out.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import torch
+
+from ..ops import hip
+
+_FLAG_BYTES = 256
+
+
+def _lib():
+    L = hip.lib()
+    if not getattr(L, "_ipc_typed", False):
+        vp, ll, i = ctypes.c_void_p, ctypes.c_longlong, ctypes.c_int
+        L.lsa_ipc_alloc.argtypes = [ll, ctypes.POINTER(vp), vp]
+        L.lsa_ipc_handle_bytes.argtypes = []
+        L.lsa_ipc_open.argtypes = [vp, ctypes.POINTER(vp)]
+        L.lsa_ipc_close.argtypes = [vp]
+        L.lsa_ipc_free.argtypes = [vp]
+        L.lsa_ipc_send.argtypes = [vp, ll, vp, ll, vp, vp, i, vp, vp, ll, i, vp]
+        L.lsa_ipc_recv.argtypes = [vp, ll, vp, ll, vp, vp, i, vp, vp, ll, i, vp]
+        L._ipc_typed = True
+    return L
+
+
+def _ok(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"{what} failed (status {rc})")
+
+
+class _Work:
+    """Send handle: ``wait()`` orders the caller's current stream after the send kernel (the
+    source buffer may be rewritten from then on) - RCCL's Work semantics."""
+
+    def __init__(self, ev):
+        self.ev = ev
+
+    def wait(self):
+        if self.ev is not None:
+            torch.cuda.current_stream().wait_event(self.ev)
+
+
+class IpcRingP2P:
+    """``rank``: this process's global rank; ``edges``: directed (src, dst) global-rank pairs
+    (default: the ring over ``ranks``); ``ranks``: stage index -> global rank (as DistP2P);
+    ``slot_bytes``: largest message; ``slots``: ring depth R per edge. Collective: every rank of
+    ``group`` (a gloo group; default: a new one over the world) constructs it at the same point."""
+
+    def __init__(self, rank: int, slot_bytes: int, slots: int = 4, ranks: Optional[list] = None,
+                 edges: Optional[list] = None, group=None, timeout_s: float = 30.0, grid: int = 32):
+        import torch.distributed as dist
+        self.rank, self.R, self.grid = rank, int(slots), int(grid)
+        hip._req(1 <= self.R <= _FLAG_BYTES // 4, f"ipc ring: 1..{_FLAG_BYTES // 4} slots")
+        self.slot_bytes = -(-int(slot_bytes) // 256) * 256
+        self.timeout_us = int(timeout_s * 1e6)
+        self.ranks = ranks
+        world = dist.get_world_size() if dist.is_initialized() else 1
+        if edges is None:
+            ring = ranks if ranks is not None else list(range(world))
+            edges = [(ring[i], ring[(i + 1) % len(ring)]) for i in range(len(ring))] if len(ring) > 1 else []
+        self.edges = [tuple(e) for e in edges]
+        self.dev = torch.device("cuda", torch.cuda.current_device())
+        L = _lib()
+        hb = L.lsa_ipc_handle_bytes()
+        self._own, self._opened = [], []
+        mine = {}  # (edge, "inbox" | "acks") -> handle bytes
+        self.inbox, self.ackbox = {}, {}
+        for e in self.edges:
+            if e[1] == rank:
+                ptr, h = ctypes.c_void_p(), ctypes.create_string_buffer(hb)
+                _ok(L.lsa_ipc_alloc(_FLAG_BYTES + self.R * self.slot_bytes, ctypes.byref(ptr), h), "lsa_ipc_alloc")
+                self._own.append(ptr.value)
+                self.inbox[e] = ptr.value
+                mine[(e, "inbox")] = h.raw
+            if e[0] == rank:
+                ptr, h = ctypes.c_void_p(), ctypes.create_string_buffer(hb)
+                _ok(L.lsa_ipc_alloc(_FLAG_BYTES, ctypes.byref(ptr), h), "lsa_ipc_alloc")
+                self._own.append(ptr.value)
+                self.ackbox[e] = ptr.value
+                mine[(e, "acks")] = h.raw
+        if group is None and dist.is_initialized():
+            group = dist.new_group(backend="gloo")
+        self.group = group
+        allh = [None] * world
+        if dist.is_initialized():
+            dist.all_gather_object(allh, mine, group=group)
+        else:
+            allh = [mine]
+        theirs = {}
+        for d in allh:
+            theirs.update(d or {})
+        self.peer_inbox, self.peer_acks = {}, {}
+        for e in self.edges:
+            if e[0] == rank:  # sender: map the receiver's inbox
+                self.peer_inbox[e] = self._open(theirs[(e, "inbox")])
+            if e[1] == rank:  # receiver: map the sender's ack box
+                self.peer_acks[e] = self._open(theirs[(e, "acks")])
+        # per edge end: {count, ticket}; one error word for every launch of this endpoint. Each edge
+        # end issues on its own stream (ordered against the caller's by events), so sends of one
+        # edge made from several compute streams still run one at a time, in issue order
+        self.state = {e: torch.zeros(2, dtype=torch.int32, device=self.dev) for e in self.edges if rank in e}
+        self.streams = {e: torch.cuda.Stream(self.dev) for e in self.state}
+        self.err = torch.zeros(1, dtype=torch.int32, device=self.dev)
+        if dist.is_initialized():
+            dist.barrier(group=group)  # every mapping is in place before anyone sends
+
+    def _open(self, handle: bytes) -> int:
+        ptr = ctypes.c_void_p()
+        _ok(_lib().lsa_ipc_open(ctypes.create_string_buffer(handle, len(handle)), ctypes.byref(ptr)), "lsa_ipc_open")
+        self._opened.append(ptr.value)
+        return ptr.value
+
+    def _global(self, stage: int) -> int:
+        return self.ranks[stage] if self.ranks is not None else stage
+
+    @staticmethod
+    def _nbytes(t: torch.Tensor) -> int:
+        n = t.numel() * t.element_size()
+        hip._req(t.is_cuda and t.is_contiguous() and n % 4 == 0 and t.data_ptr() % 16 == 0,
+                 "ipc ring: contiguous 16-B aligned cuda tensor, bytes % 4 == 0")
+        return n
+
+    def isend(self, t: torch.Tensor, dst: int):
+        e = (self.rank, self._global(dst))
+        n = self._nbytes(t)
+        hip._req(n <= self.slot_bytes, f"ipc ring: message {n} B > slot {self.slot_bytes} B")
+        base = self.peer_inbox[e]
+        cur, cs = torch.cuda.current_stream(self.dev), self.streams[e]
+        cs.wait_stream(cur)
+        _ok(_lib().lsa_ipc_send(t.data_ptr(), n, base + _FLAG_BYTES, self.slot_bytes, base, self.ackbox[e], self.R,
+                                self.state[e].data_ptr(), self.err.data_ptr(), self.timeout_us, self.grid,
+                                cs.cuda_stream), "lsa_ipc_send")
+        t.record_stream(cs)
+        if torch.cuda.is_current_stream_capturing():
+            cur.wait_stream(cs)  # a captured send joins the capturing stream before the capture ends
+            return _Work(None)
+        ev = torch.cuda.Event()
+        ev.record(cs)
+        return _Work(ev)
+
+    def recv(self, t: torch.Tensor, src: int) -> None:
+        e = (self._global(src), self.rank)
+        n = self._nbytes(t)
+        hip._req(n <= self.slot_bytes, f"ipc ring: message {n} B > slot {self.slot_bytes} B")
+        base = self.inbox[e]
+        cur, cs = torch.cuda.current_stream(self.dev), self.streams[e]
+        cs.wait_stream(cur)
+        _ok(_lib().lsa_ipc_recv(t.data_ptr(), n, base + _FLAG_BYTES, self.slot_bytes, base, self.peer_acks[e], self.R,
+                                self.state[e].data_ptr(), self.err.data_ptr(), self.timeout_us, self.grid,
+                                cs.cuda_stream), "lsa_ipc_recv")
+        t.record_stream(cs)
+        cur.wait_stream(cs)
+
+    def fits(self, t: torch.Tensor) -> bool:
+        n = t.numel() * t.element_size()
+        return t.is_cuda and t.is_contiguous() and n % 4 == 0 and n <= self.slot_bytes and t.data_ptr() % 16 == 0
+
+    def check(self) -> None:
+        """Raise if any send (1: no ack) or receive (2: no message) gave up waiting."""
+        code = int(self.err.item())
+        if code:
+            raise RuntimeError(f"ipc ring: a {'send' if code == 1 else 'receive'} timed out waiting for its peer")
+
+    def close(self) -> None:
+        """Unmap the peers' buffers, then (once every rank has unmapped ours) free our own."""
+        import torch.distributed as dist
+        torch.cuda.synchronize(self.dev)
+        L = _lib()
+        for p in self._opened:
+            L.lsa_ipc_close(p)
+        if dist.is_initialized():
+            dist.barrier(group=self.group)
+        for p in self._own:
+            L.lsa_ipc_free(p)
+        self._opened, self._own = [], []
+
+
+class HybridP2P:
+    """Messages that fit a ring slot go through ``ipc`` (IpcRingP2P), larger ones (the prompt
+    prefill's hidden states) through ``fallback`` (DistP2P / RCCL). Both ends decide by the
+    message's size, so each channel stays FIFO per edge."""
+
+    def __init__(self, ipc: IpcRingP2P, fallback):
+        self.ipc, self.fallback = ipc, fallback
+
+    def isend(self, t: torch.Tensor, dst: int):
+        return self.ipc.isend(t, dst) if self.ipc.fits(t) else self.fallback.isend(t, dst)
+
+    def recv(self, t: torch.Tensor, src: int) -> None:
+        if self.ipc.fits(t):
+            self.ipc.recv(t, src)
+        else:
+            self.fallback.recv(t, src)

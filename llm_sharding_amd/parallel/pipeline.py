@@ -416,9 +416,10 @@ class PipelineStage:
 
 def run_pipeline_generate(cfg, source, prompts: Optional[torch.Tensor], n_new: int, rank: int, world: int,
                           device="cpu", batch: int = 1, microbatches: int = 1, max_seq: int = 256,
-                          plan=None, dtype=torch.float32, streams: int = 1) -> Optional[torch.Tensor]:
+                          plan=None, dtype=torch.float32, streams: int = 1, p2p=None) -> Optional[torch.Tensor]:
     """Greedy generation through the micro-batched pipeline (torch.distributed already
     initialised; gloo on CPU or nccl/RCCL on GPUs). ``prompts`` [M, B, P] on rank 0.
+    ``p2p``: the stage hand-off transport (default DistP2P; e.g. ipc_ring.IpcRingP2P).
     Returns [n_new, M, B] generated ids on rank 0 (gathered from the last stage)."""
     import torch.distributed as dist
     plan = plan or plan_stages(cfg, world, head_split=world > 1)
@@ -429,7 +430,7 @@ def run_pipeline_generate(cfg, source, prompts: Optional[torch.Tensor], n_new: i
         dist.broadcast(pl, 0)
         P = int(pl[0])
     stage = PipelineStage(cfg, rank, world, st.start, st.end, device, batch, microbatches, max_seq, source,
-                          use_graph=True, max_prefill_rows=batch * P, dtype=dtype, streams=streams)
+                          use_graph=True, max_prefill_rows=batch * P, dtype=dtype, streams=streams, p2p=p2p)
     firsts = stage.prefill(prompts, P)
     stage.build_graphs(firsts, history_len=n_new - 1)
     for s in range(n_new - 1):
@@ -552,7 +553,7 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
                          microbatches: int = 0, seed: int = 0, use_graph: bool = True,
                          verbose: bool = True, weight_dtype: str = "bf16", streams: int = 1,
                          device: str = "cuda", dp: int = 1, latency_steps: int = 0,
-                         stage_layers: int = 0) -> Optional[dict]:
+                         stage_layers: int = 0, transport: str = "rccl") -> Optional[dict]:
     """``microbatches`` 0 = ``streams`` x stages (every GPU holds ``streams`` micro-batches of
     ``batch`` sequences: weak scaling); ``max_seq`` 0 = what the run needs, rounded up to 64.
 
@@ -565,7 +566,11 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
 
     ``stage_layers`` > 0: a STAGE PROFILE, not the headline number - the model's architecture
     cut to that many decoder layers (embedding and lm_head kept), e.g. one 10-layer stage of
-    Llama-2-70B's 8-stage plan on one GPU with ``microbatches=8`` to hold that stage's KV."""
+    Llama-2-70B's 8-stage plan on one GPU with ``microbatches=8`` to hold that stage's KV.
+
+    ``transport`` "ipc": decode-step messages (hidden states, argmax keys, token ids) go through
+    IPC-mapped rings in the receiver's HBM (parallel/ipc_ring.py: one kernel per send / receive,
+    device flags, no communicator); the prompt prefill's larger messages stay on RCCL."""
     cfg = get_preset(model)
     if stage_layers:
         import dataclasses
@@ -621,6 +626,14 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
         print(f"[bench] {cfg.name} {'dp%d x ' % dp if dp > 1 else ''}pp{pp} plan: {plan.summary()}", flush=True)
     rings = [list(range(d * pp, (d + 1) * pp)) for d in range(dp)]
     p2p = DistP2P(ranks=rings[replica], rings=rings)
+    if transport == "ipc" and gpu and pp > 1:
+        from .ipc_ring import HybridP2P, IpcRingP2P
+        edges = [(r[i], r[(i + 1) % pp]) for r in rings for i in range(pp)]
+        ipc = IpcRingP2P(rank, slot_bytes=batch * cfg.hidden_size * 2, slots=min(64, max(2, M)),
+                         ranks=rings[replica], edges=edges)
+        p2p = HybridP2P(ipc, p2p)
+    elif transport not in ("rccl", "ipc"):
+        raise ValueError(f"transport {transport!r}: rccl or ipc")
     t0 = time.perf_counter()
     stage = PipelineStage(cfg, srank, pp, st.start, st.end, dev, batch, M, max_seq,
                           RandomSource(cfg, seed), use_graph=use_graph,
