@@ -67,6 +67,8 @@ class IpcRingP2P:
     ``slot_bytes``: largest message; ``slots``: ring depth R per edge. Collective: every rank of
     ``group`` (a gloo group; default: a new one over the world) constructs it at the same point."""
 
+    graph_capturable = True  # sends / receives may be captured in a hipGraph (device-side indices)
+
     def __init__(self, rank: int, slot_bytes: int, slots: int = 4, ranks: Optional[list] = None,
                  edges: Optional[list] = None, group=None, timeout_s: float = 30.0, grid: int = 32):
         import torch.distributed as dist
@@ -121,6 +123,7 @@ class IpcRingP2P:
         # edge made from several compute streams still run one at a time, in issue order
         self.state = {e: torch.zeros(2, dtype=torch.int32, device=self.dev) for e in self.edges if rank in e}
         self.streams = {e: torch.cuda.Stream(self.dev) for e in self.state}
+        self.captured_ops = 0  # sends / receives recorded into hipGraphs (diagnostics)
         self.err = torch.zeros(1, dtype=torch.int32, device=self.dev)
         if dist.is_initialized():
             dist.barrier(group=group)  # every mapping is in place before anyone sends
@@ -153,6 +156,7 @@ class IpcRingP2P:
                                 cs.cuda_stream), "lsa_ipc_send")
         t.record_stream(cs)
         if torch.cuda.is_current_stream_capturing():
+            self.captured_ops += 1
             cur.wait_stream(cs)  # a captured send joins the capturing stream before the capture ends
             return _Work(None)
         ev = torch.cuda.Event()
@@ -170,6 +174,7 @@ class IpcRingP2P:
                                 self.state[e].data_ptr(), self.err.data_ptr(), self.timeout_us, self.grid,
                                 cs.cuda_stream), "lsa_ipc_recv")
         t.record_stream(cs)
+        self.captured_ops += int(torch.cuda.is_current_stream_capturing())
         cur.wait_stream(cs)
 
     def fits(self, t: torch.Tensor) -> bool:
@@ -201,8 +206,13 @@ class HybridP2P:
     prefill's hidden states) through ``fallback`` (DistP2P / RCCL). Both ends decide by the
     message's size, so each channel stays FIFO per edge."""
 
+    graph_capturable = True  # what fits the ring (every decode message) is graph-capturable
+
     def __init__(self, ipc: IpcRingP2P, fallback):
         self.ipc, self.fallback = ipc, fallback
+
+    def fits(self, t: torch.Tensor) -> bool:
+        return self.ipc.fits(t)
 
     def isend(self, t: torch.Tensor, dst: int):
         return self.ipc.isend(t, dst) if self.ipc.fits(t) else self.fallback.isend(t, dst)

@@ -314,8 +314,43 @@ class PipelineStage:
                 if first_tokens is not None and mode in ("full", "first"):
                     g.tokens.copy_(first_tokens[mb])
             if self.use_graph:
+                if self.graph_comm:
+                    self._attach_comm(g)
                 g.capture()
             self.graphs.append(g)
+
+    @property
+    def graph_comm(self) -> bool:
+        """Hand-offs captured inside the decode graphs: a graph-capturable transport (IPC ring),
+        one compute stream (graphs of one edge must not run concurrently: the ring's device
+        counters order its messages) and every decode message small enough for the ring. The
+        first stage's back-edge receive stays outside (it is skipped after a drain)."""
+        if not (self.gpu and self.use_graph and self.world > 1 and self.S == 1
+                and getattr(self.p2p, "graph_capturable", False)
+                and os.environ.get("LSA_GRAPH_COMM", "1") == "1"):
+            return False
+        H = self.cfg.hidden_size
+        probe = [torch.empty((self.B, H), dtype=self.dtype, device=self.device),
+                 torch.empty(self.B, dtype=torch.int64, device=self.device),
+                 torch.empty(self.B, dtype=torch.int32, device=self.device)]
+        return all(self.p2p.fits(t) for t in probe)
+
+    def _attach_comm(self, g: DecodeGraph) -> None:
+        p2p, r = self.p2p, self.rank
+        if self.mode in ("mid", "last"):
+            g.pre_comm = lambda: p2p.recv(g.h_in, r - 1)
+        if self.mode == "last" and self.split:
+            def post():
+                p2p.isend(g.out_hidden, 0)
+                p2p.isend(g.keys, 0)
+        elif self.mode == "last":
+            def post():
+                p2p.isend(g.tokens, 0)
+        else:
+            def post():
+                p2p.isend(g.out_hidden, r + 1)
+        g.post_comm = post
+        g.in_graph_comm = True
 
     def _run_mb(self, g: DecodeGraph):
         if self.use_graph:
@@ -351,7 +386,8 @@ class PipelineStage:
     def _step_mb(self, s: int, mb: int, events: Optional[list] = None) -> None:
         g = self.graphs[mb]
         tl = self.tl
-        if self.world > 1:
+        in_graph = getattr(g, "in_graph_comm", False)
+        if self.world > 1 and not (in_graph and not self.first):
             with tl.span("recv", mb=mb, step=s):
                 if self.first:
                     if not self.tokens_ready[mb]:
@@ -369,7 +405,7 @@ class PipelineStage:
             ev = torch.cuda.Event(enable_timing=True)
             ev.record()
             events.append((s, mb, ev))
-        if self.world > 1:
+        if self.world > 1 and not in_graph:
             if self.last and self.split:
                 # private copies: the next replay rewrites the engine's hidden buffer / keys
                 self._wait_send(("hb", mb))

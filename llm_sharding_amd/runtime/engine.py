@@ -938,6 +938,10 @@ class DecodeGraph:
         self.step_ctr = torch.zeros(1, dtype=torch.int32, device=dev)
         self.graph = None
         self._hip = hip
+        # stage hand-off captured INTO the graph (pipeline over a graph-capturable transport,
+        # parallel/ipc_ring.py): receive into h_in before the step, send the step's output after
+        self.pre_comm = None
+        self.post_comm = None
         # split lm_head (pipeline): "last" leaves partial keys over its vocab slice + the raw
         # final hidden; "first" completes the PREVIOUS step's keys over its slice from
         # (h_fin, keys_in), finalises the token ids (and history) and then embeds them
@@ -1000,7 +1004,8 @@ class DecodeGraph:
         return self._out
 
     def capture(self, warmup: bool = True) -> "DecodeGraph":
-        """Capture the step. The warm-up replay (if any) is undone (positions restored)."""
+        """Capture the step (with ``pre_comm`` / ``post_comm`` around it when set). The warm-up
+        run (if any) is undone (positions restored) and never communicates."""
         pos0, tok0 = self.pos.clone(), self.tokens.clone()
         kin0 = self.keys_in.clone() if self.split_head else None
         s = torch.cuda.Stream(device=self.eng.device)
@@ -1011,7 +1016,11 @@ class DecodeGraph:
         torch.cuda.current_stream(self.eng.device).wait_stream(s)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, stream=s):
+            if self.pre_comm is not None:
+                self.pre_comm()
             self._body()
+            if self.post_comm is not None:
+                self.post_comm()
         self.graph = g
         self.pos.copy_(pos0)
         self.tokens.copy_(tok0)

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """The micro-batched pipeline with the IPC ring as its stage hand-off (parallel/ipc_ring.py):
-two ranks (processes) of a tiny Llama, here both on one GPU, prefill + hipGraph decode with
-micro-batches on concurrent streams; rank 0 checks the generated ids token-exact against the
+two ranks (processes) of a tiny Llama, here both on one GPU, prefill + hipGraph decode (one
+stream: the hand-offs captured inside the decode graphs; several: micro-batches on concurrent
+streams with the ring kernels launched between replays); rank 0 checks the generated ids token-exact against the
 same model run as a single stage in-process.
 
     python scripts/ipc_pipeline_check.py --rank R --port P [--streams S]"""
@@ -41,7 +42,7 @@ def main():
     torch.cuda.synchronize()
     print(f"[rank {a.rank}] pipeline done", flush=True)
     p2p.check()
-    res = {"rank": a.rank, "ok": True}
+    res = {"rank": a.rank, "ok": True, "captured_ops": p2p.captured_ops}
     if a.rank == 0:
         # (a single stage sends nothing; LocalP2P keeps DistP2P's collective group setup out of it)
         single = run_pipeline_generate(cfg, src, prompts, 10, 0, 1, p2p=LocalP2P().bind(0), **kw)
