@@ -46,11 +46,15 @@ LSA_DEVICE void glds16(const void* src, unsigned char* lds_base) {
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
 }
 
-template <int HD, int HPW>
+// DEC: decode mode (GQA decode attention on MFMA, lsa_attn_decode_mfma): work item tix is decode
+// row tix - one query position per sequence, its tile derived on the device from slot / pos /
+// kv_len (graph-replay safe), and the G query heads of a KV head share every staged K/V block.
+template <int HD, int HPW, bool DEC = false>
 __global__ __launch_bounds__(NTHR) void flash_prefill_kernel(
     const bf16_raw* __restrict__ q, int ldq, const bf16_raw* __restrict__ kc, const bf16_raw* __restrict__ vc,
     const PrefillTile* __restrict__ tiles, int n_heads, int n_kv, int t_max, float scale_log2, int causal,
-    bf16_raw* __restrict__ out, int ldo) {
+    bf16_raw* __restrict__ out, int ldo, const int* __restrict__ dslot = nullptr,
+    const int* __restrict__ dpos = nullptr, const int* __restrict__ dkvlen = nullptr) {
   constexpr int KF = HD / 32;                 // 32-dim fragments of a query/key row
   constexpr int DT = HD / 16;                 // 16-dim output tiles
   constexpr int NC = HD / 8;                  // 16-B chunks per row
@@ -73,7 +77,17 @@ __global__ __launch_bounds__(NTHR) void flash_prefill_kernel(
     tix = blockIdx.x % n_tiles;
     grp = blockIdx.x / n_tiles;
   }
-  const PrefillTile tile = tiles[tix];
+  PrefillTile tile;
+  if constexpr (DEC) {
+    tile.row0 = tix;
+    tile.nrows = 1;
+    tile.slot = dslot[tix];
+    tile.pos0 = dpos[tix];
+    const int kl = dkvlen ? dkvlen[tix] : dpos[tix] + 1;
+    tile.kvlen = kl < t_max ? kl : t_max;  // never read past the static cache
+  } else {
+    tile = tiles[tix];
+  }
   const int G = n_heads / n_kv;
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, l16 = lane & 15;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -263,6 +277,25 @@ int dispatch_hpw(int hpw, const bf16_raw* q, int ldq, const bf16_raw* k, const b
   return LSA_OK;
 }
 
+template <int HD>
+int launch_decode_mfma(int hpw, const bf16_raw* q, int ldq, const bf16_raw* k, const bf16_raw* v, const int* slot,
+                       const int* pos, const int* kvlen, int rows, int n_heads, int n_kv, int t_max, float sl2,
+                       bf16_raw* o, int ldo, hipStream_t stream) {
+  dim3 grid(rows * (n_heads / hpw)), block(NTHR);
+  switch (hpw) {
+    case 4:
+      flash_prefill_kernel<HD, 4, true><<<grid, block, 0, stream>>>(q, ldq, k, v, nullptr, n_heads, n_kv, t_max, sl2, 0,
+                                                                   o, ldo, slot, pos, kvlen);
+      break;
+    case 8:
+      flash_prefill_kernel<HD, 8, true><<<grid, block, 0, stream>>>(q, ldq, k, v, nullptr, n_heads, n_kv, t_max, sl2, 0,
+                                                                   o, ldo, slot, pos, kvlen);
+      break;
+    default: return LSA_UNSUPPORTED;
+  }
+  return LSA_OK;
+}
+
 }  // namespace
 
 // tiles: device array of n_tiles PrefillTile {row0, nrows, slot, pos0, kvlen, pad x3}; nrows <=
@@ -289,6 +322,33 @@ extern "C" int lsa_attn_prefill(const void* q, int ldq, const void* kc, const vo
     rc = dispatch_hpw<128>(hpw, qq, ldq, k, v, t, n_tiles, n_heads, n_kv, t_max, sl2, causal, o, ldo, stream);
   else if (head_dim == 64)
     rc = dispatch_hpw<64>(hpw, qq, ldq, k, v, t, n_tiles, n_heads, n_kv, t_max, sl2, causal, o, ldo, stream);
+  else
+    return LSA_UNSUPPORTED;
+  if (rc != LSA_OK) return rc;
+  LSA_CHECK_LAUNCH();
+  return LSA_OK;
+}
+
+// GQA decode attention on MFMA: one workgroup per (decode row, KV head) with the group's
+// G = n_heads / n_kv query heads (G = 4 or 8), keys [0, kv_len or pos + 1) of the row's cache
+// slot, no split over keys (callers use it when rows x n_kv fills the GPU). Same numerics as
+// the prefill kernel (bf16 P for the PV MFMA).
+extern "C" int lsa_attn_decode_mfma(const void* q, int ldq, const void* kc, const void* vc, const int* slot,
+                                    const int* pos, const int* kv_len, int rows, int n_heads, int n_kv, int head_dim,
+                                    int t_max, float scale, void* out, int ldo, hipStream_t stream) {
+  if (rows < 1 || n_kv < 1 || n_heads % n_kv || !slot || !pos) return LSA_BAD_SHAPE;
+  const int g = n_heads / n_kv;
+  if (g != 4 && g != 8) return LSA_UNSUPPORTED;
+  const float sl2 = scale * 1.4426950408889634f;
+  const auto* qq = static_cast<const bf16_raw*>(q);
+  const auto* k = static_cast<const bf16_raw*>(kc);
+  const auto* v = static_cast<const bf16_raw*>(vc);
+  auto* o = static_cast<bf16_raw*>(out);
+  int rc;
+  if (head_dim == 128)
+    rc = launch_decode_mfma<128>(g, qq, ldq, k, v, slot, pos, kv_len, rows, n_heads, n_kv, t_max, sl2, o, ldo, stream);
+  else if (head_dim == 64)
+    rc = launch_decode_mfma<64>(g, qq, ldq, k, v, slot, pos, kv_len, rows, n_heads, n_kv, t_max, sl2, o, ldo, stream);
   else
     return LSA_UNSUPPORTED;
   if (rc != LSA_OK) return rc;

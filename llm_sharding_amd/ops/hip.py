@@ -64,6 +64,7 @@ def lib() -> ctypes.CDLL:
     L.lsa_gemm.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(EpiArgs), i, i, vp, vp, vp]
     L.lsa_attn_decode.argtypes = [vp, i, vp, vp, vp, vp, vp, i, i, i, i, i, f, i, i, vp, vp, vp, i, vp, vp]
     L.lsa_attn_prefill.argtypes = [vp, i, vp, vp, vp, i, i, i, i, i, f, i, vp, i, vp]
+    L.lsa_attn_decode_mfma.argtypes = [vp, i, vp, vp, vp, vp, vp, i, i, i, i, i, f, vp, i, vp]
     L.lsa_embed.argtypes = [vp, i, vp, i, vp, i, vp]
     L.lsa_rmsnorm.argtypes = [vp, i, vp, i, i, f, vp, i, vp]
     L.lsa_layernorm.argtypes = [vp, i, vp, vp, vp, vp, i, i, f, vp, i, vp]
@@ -495,6 +496,15 @@ def attn(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, slot: to
     _req(slot.dtype == torch.int32 and pos.dtype == torch.int32, "attn: int32 slot/pos")
     t_max = k_cache.shape[2]
     sc = head_dim ** -0.5 if scale is None else scale
+    g = n_heads // n_kv
+    if g in (4, 8) and rows * n_kv >= ATTN_MFMA_MIN_ITEMS and ATTN_MFMA:
+        # GQA with enough (row, kv-head) work items to fill the GPU unsplit: the MFMA kernel
+        # (attn_prefill.hip decode mode: one K/V stream per item serves all G query heads)
+        rc = lib().lsa_attn_decode_mfma(_p(q), q.stride(0), _p(k_cache), _p(v_cache), _p(slot), _p(pos), _p(kv_len),
+                                        rows, n_heads, n_kv, head_dim, t_max, float(sc), _p(out), out.stride(0),
+                                        _stream())
+        _check(rc, "lsa_attn_decode_mfma")
+        return
     if nsplit > 1 and counters is None:
         counters = default_workspace(q.device).counters
     _req(nsplit == 1 or (counters.dtype == torch.int32 and counters.numel() >= rows * n_kv),
@@ -505,6 +515,11 @@ def attn(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, slot: to
                                _p(counters) if nsplit > 1 else None, _stream())
     _check(rc, "lsa_attn_decode")
 
+
+# GQA decode attention on MFMA (lsa_attn_decode_mfma) from this many (row, kv-head) items up;
+# below it the split-KV VALU kernel, which spreads long contexts over more workgroups
+ATTN_MFMA_MIN_ITEMS = int(os.environ.get("LSA_ATTN_MFMA_MIN_ITEMS", "512"))
+ATTN_MFMA = os.environ.get("LSA_ATTN_MFMA", "1") == "1"
 
 PREFILL_TILE_ROWS = 128  # positions per tile with one query head per workgroup
 
