@@ -34,12 +34,22 @@ struct PrefillTile {
 
 typedef short v4s_t __attribute__((ext_vector_type(4)));
 
-// byte offset of 16-B chunk ch of row r in a [BKV][HD] bf16 image: rows XOR-swizzled so that
-// 16-lane ds_read_b128 row reads and 4-row ds_read_b64_tr_b16 reads are (near) conflict-free
+// chunk swizzle of row r (HD = 128: 16 chunks of 16 B per row). ((r & 3) << 2) ^ (((r >> 2) & 3) << 1)
+// makes both read patterns conflict-free: the 16-lane ds_read_b128 groups of the K reads (rows
+// l16, chunks kf*4 + lane/16) and the 32-lane ds_read_b64_tr_b16 groups of the V^T reads (8 keys x
+// the two chunks of a 16-dim tile) each hit 16 distinct 16-B bank slots. (The previous
+// ((r & 3) << 2) | ((r >> 2) & 3) only flipped bit 0 for rows 4-7, which the tr reads' chunk
+// pairs {2d, 2d+1} absorb: 2.55 conflict cycles per LDS op in profiles/r2_pmc_hot_kernels.txt.)
+template <int HD>
+LSA_DEVICE int swz(int r) {
+  if constexpr (HD == 128) return ((r & 3) << 2) ^ (((r >> 2) & 3) << 1);
+  else return (r >> 1) & 7;
+}
+
+// byte offset of 16-B chunk ch of row r in a [BKV][HD] bf16 image
 template <int HD>
 LSA_DEVICE int sw_off(int r, int ch) {
-  if constexpr (HD == 128) return r * 256 + ((ch ^ (((r & 3) << 2) | ((r >> 2) & 3))) << 4);
-  else return r * 128 + ((ch ^ ((r >> 1) & 7)) << 4);
+  return r * (HD * 2) + ((ch ^ swz<HD>(r)) << 4);
 }
 
 LSA_DEVICE void glds16(const void* src, unsigned char* lds_base) {
@@ -124,7 +134,7 @@ __global__ __launch_bounds__(NTHR) void flash_prefill_kernel(
     for (int s = 0; s < PPW; ++s) {
       const int pc = w * PPW + s;
       const int r = pc * RPP + lane / NC, slot = lane % NC;
-      const int ch = HD == 128 ? (slot ^ (((r & 3) << 2) | ((r >> 2) & 3))) : (slot ^ ((r >> 1) & 7));
+      const int ch = slot ^ swz<HD>(r);
       const int key = min(kb * BKV + r, lim - 1);  // clamped rows are masked in the softmax
       glds16(kb_ptr + (size_t)key * HD + ch * 8, kd + pc * 1024);
       glds16(vb_ptr + (size_t)key * HD + ch * 8, kd + BLK + pc * 1024);
@@ -226,7 +236,7 @@ __global__ __launch_bounds__(NTHR) void flash_prefill_kernel(
 #pragma unroll
       for (int d = 0; d < DT; ++d) {
         // rows key_lo + f2*32 (+16): same swizzle term as key_lo (it depends on row & 15 only
-        // through row & 3 and (row >> 2) & 3, unchanged by multiples of 16)
+        // through row & 3 and (row >> 2) & 3, unchanged by multiples of 16; HD = 64: (row >> 1) & 7)
         const v4s_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
             (__attribute__((address_space(3))) v4s_t*)(vs + f2 * 32 * (HD * 2) + v_off[d]));
         const v4s_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
