@@ -9,8 +9,8 @@
 // 16 query rows of one head (positions (w / HPW) * 16 ..), so a tile holds 128 / HPW
 // positions and every staged K/V block serves the whole GQA group (no re-staging per head).
 // Per 64-key block:
-//   * K and V arrive by LDS-DMA (global_load_lds, 16 B/lane) into a double-buffered ring,
-//     block kb+1 in flight while block kb is computed; one barrier per block. The swizzle is
+//   * K and V arrive by LDS-DMA (global_load_lds, 16 B/lane) into an NBUF-deep ring, blocks
+//     kb+1 .. kb+NBUF-1 in flight (counted vmcnt) while block kb is computed; one barrier per block. The swizzle is
 //     applied on the SOURCE address, so each 1 KiB piece lands lane-linear.
 //   * S^T[key][row] = K . Q^T   A = K rows (ds_read_b128, XOR-swizzled rows: conflict-free),
 //                               B = Q^T held in registers for the whole tile
@@ -27,6 +27,10 @@
 namespace {
 
 constexpr int BKV = 64, NWV = 8, NTHR = NWV * 64;  // 64-key blocks, 8 waves x 16 query rows
+// K/V ring depth. 2 (block kb+1 in flight while kb is computed) keeps the workgroup at 64 KiB of
+// LDS, two per CU; a 4-deep ring (128 KiB, one per CU) measured 6-16 % slower at S >= 2048
+// and no faster at S = 512 (scripts/prefill_attn_bench.py)
+constexpr int NBUF = 2;
 
 struct PrefillTile {
   int row0, nrows, slot, pos0, kvlen, pad0, pad1, pad2;
@@ -72,7 +76,7 @@ __global__ __launch_bounds__(NTHR) void flash_prefill_kernel(
   constexpr int PPW = BLK / 1024 / NWV;       // 1 KiB DMA pieces per wave per operand
   constexpr int RPP = 1024 / (HD * 2);        // rows per piece
   static_assert(PPW >= 1 && NWV % HPW == 0, "geometry");
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * 2 * BLK];  // [buffer][K | V]
+  __shared__ __attribute__((aligned(16))) unsigned char smem[NBUF * 2 * BLK];  // [buffer][K | V]
 
   // work item -> (tile, head group). XCD-aware when the group count is a multiple of 8: XCD x
   // (= blockIdx.x % 8 in dispatch order) owns groups x, x+8, ... so their K/V blocks stay in
@@ -155,12 +159,19 @@ __global__ __launch_bounds__(NTHR) void flash_prefill_kernel(
 #pragma unroll
   for (int d = 0; d < DT; ++d) v_off[d] = sw_off<HD>(key_lo, 2 * d + ((l16 & 3) >> 1)) + 8 * (l16 & 1);
 
-  if (nkb > 0) stage(0, 0);
+  // prologue: blocks 0 .. NBUF-2 in flight
+  for (int b = 0; b < NBUF - 1 && b < nkb; ++b) stage(b, b);
   for (int kb = 0; kb < nkb; ++kb) {
-    const int cur = kb & 1;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of block kb landed
-    __syncthreads();                                    // ... every wave's; block kb-1 reads done
-    if (kb + 1 < nkb) stage(kb + 1, cur ^ 1);
+    const int cur = kb % NBUF;
+    // counted wait: this wave's DMA of block kb landed, its later blocks (up to NBUF-2 of them,
+    // 2 * PPW instructions each) may stay in flight
+    const int later = min(NBUF - 2, nkb - 1 - kb);
+    static_assert(NBUF >= 2 && NBUF <= 4, "ring depth");
+    if (later >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * 2 * PPW) : "memory");
+    else if (later == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * PPW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // ... every wave's; every wave's reads of block kb-1 done
+    if (kb + NBUF - 1 < nkb) stage(kb + NBUF - 1, (kb + NBUF - 1) % NBUF);  // into block kb-1's buffer
     if (kb * BKV >= wave_lim) continue;                 // wave-uniform: all keys above the diagonal
     const unsigned char* ks = smem + cur * (2 * BLK);
     const unsigned char* vs = ks + BLK;

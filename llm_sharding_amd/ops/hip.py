@@ -524,11 +524,18 @@ ATTN_MFMA = os.environ.get("LSA_ATTN_MFMA", "1") == "1"
 PREFILL_TILE_ROWS = 128  # positions per tile with one query head per workgroup
 
 
-def prefill_tile_rows(n_heads: int, n_kv: int) -> int:
+def prefill_tile_rows(n_heads: int, n_kv: int, rows: int = 0) -> int:
     """Positions per flash-prefill tile: 8 waves x 16 rows shared by the GQA group's heads
-    that one workgroup covers (all G of them when G divides 8; lsa_prefill_tile_rows)."""
+    that one workgroup covers (all G of them when G divides 8; lsa_prefill_tile_rows). With
+    ``rows`` (the prefill's total query rows) the tile is halved, down to 16 positions, while
+    the (tile, head-group) work items would leave CUs idle - a 512-token 7B prompt gets 256
+    items of 64 positions instead of 128 of 128."""
     g = n_heads // n_kv
-    return PREFILL_TILE_ROWS // (g if 8 % g == 0 else 1)
+    hpw = g if 8 % g == 0 else 1
+    t = PREFILL_TILE_ROWS // hpw
+    while rows and t > 16 and -(-rows // t) * (n_heads // hpw) < N_CU:
+        t //= 2
+    return t
 
 
 def build_prefill_tiles(slot, pos, kv_len=None, device=None, tile_rows: int = PREFILL_TILE_ROWS):

@@ -513,7 +513,7 @@ class StageEngine:
                 # prefill: flash attention over per-sequence tiles (host-built table)
                 from ..ops import hip
                 th = hip.build_prefill_tiles(slot, pos, kv_len, tile_rows=hip.prefill_tile_rows(
-                    self.cfg.num_attention_heads, self.cfg.num_key_value_heads))
+                    self.cfg.num_attention_heads, self.cfg.num_key_value_heads, rows))
                 tiles = (th, th.to(self.device, non_blocking=True))
             return self._forward_hip(h, slot_t, pos_t, kvl_t, rows, tiles=tiles)
         return self._forward_torch(h, slot_t.long(), pos_t.long(), None if kvl_t is None else kvl_t.long())

@@ -22,7 +22,7 @@ def main():
             vc = torch.randn_like(kc)
             q = torch.randn(S, nh * hd, device=DEV).to(torch.bfloat16)
             out = torch.zeros(S, nh * hd, dtype=torch.bfloat16, device=DEV)
-            th = hip.build_prefill_tiles([0] * S, list(range(S)), tile_rows=hip.prefill_tile_rows(nh, nkv))
+            th = hip.build_prefill_tiles([0] * S, list(range(S)), tile_rows=hip.prefill_tile_rows(nh, nkv, S))
             td = th.to(DEV)
 
             def run():
