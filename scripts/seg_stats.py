@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-segment kernel breakdown of a rocprofv3 kernel-trace CSV: a new segment starts at every
+"""Per-segment kernel breakdown of a rocprofv3 kernel trace (CSV or rocpd .db): a new segment starts at every
 dispatch of a marker kernel (default embed_kernel = one forward). usage: seg_stats.py csv [marker] [min_us]"""
 import collections
 import csv
@@ -17,7 +17,14 @@ def main():
     path = sys.argv[1]
     marker = sys.argv[2] if len(sys.argv) > 2 else "embed_kernel"
     min_us = float(sys.argv[3]) if len(sys.argv) > 3 else 1000
-    rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
+    if path.endswith(".db"):  # rocprofv3 >= 7 default output (rocpd sqlite)
+        import sqlite3
+        con = sqlite3.connect(path)
+        rows = [{"Kernel_Name": n, "Start_Timestamp": s, "End_Timestamp": e}
+                for n, s, e in con.execute("select name, start, end from kernels")]
+    else:
+        rows = list(csv.DictReader(open(path)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     segs, cur = [], []
     for r in rows:
         if marker in r["Kernel_Name"] and cur:
