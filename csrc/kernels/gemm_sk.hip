@@ -55,8 +55,8 @@ struct Geo {
   static constexpr int EROWS = (TN > 64 || TM < 64) ? 32 : 64;  // rows per epilogue transpose pass
   static constexpr int ELD = TN + 4;                // fp32 row stride of the transpose image
   static constexpr int EPI_BYTES = 8 * EROWS * ELD * 4;
-  static constexpr int RS_OFF = (NB * BUF > EPI_BYTES ? NB * BUF : EPI_BYTES);  // per-wave row rstd [8][EROWS]
-  static constexpr int SMEM = RS_OFF + 8 * EROWS * 4 + 16;
+  static constexpr int RS_OFF = (NB * BUF > EPI_BYTES ? NB * BUF : EPI_BYTES);  // row rstd of the tile [BM]
+  static constexpr int SMEM = RS_OFF + BM * 4 + 16;
   static_assert(SMEM <= 160 * 1024, "LDS budget");
   static_assert(BHI_WAVES == 0 || BGL_LO == 0 || BHI_WAVES == 4, "B blocks per wave");
   static_assert(AGL >= 1 && TM % EROWS == 0 && FM % 2 == 0, "tile geometry");
@@ -419,24 +419,36 @@ struct Kern {
     const SkParams& P = *p;
     constexpr int EROWS = G_::EROWS, ELD = G_::ELD, FPP = EROWS / 16;  // rows / fragments per pass
     float* img = reinterpret_cast<float*>(smem) + w * (EROWS * ELD);
-    float* s_rs = reinterpret_cast<float*>(smem + G_::RS_OFF) + w * EROWS;
+    // fused RMSNorm: the rstd of each of the tile's BM rows from the producer's 64-column
+    // partials, computed ONCE per workgroup (one thread per row, all of its partials' loads in
+    // flight) and summed in the same order as before (bitwise-identical rstd). Before, every
+    // wave column recomputed its rows' rstd per pass: 4x the partials traffic, +23 us on a
+    // 2048-row gate_up (scripts/epi_cost_probe.py)
+    float* s_rs = reinterpret_cast<float*>(smem + G_::RS_OFF);
     constexpr bool SS_IN = EPI == EPI_QKV || EPI == EPI_SWIGLU;
+    if (SS_IN && ep.ss_in) {
+      for (int r = tid; r < BM; r += NTHR) {
+        const int m = min(mt * BM + r, P.M - 1);
+        const float* sp = ep.ss_in + (size_t)m * ep.ss_n;
+        float t = 0.f;
+        for (int i0 = 0; i0 < ep.ss_n; i0 += 64) {
+          f32x4_t q4[16];
+#pragma unroll
+          for (int j = 0; j < 16; ++j)
+            q4[j] = i0 + 4 * j < ep.ss_n ? *reinterpret_cast<const f32x4_t*>(sp + i0 + 4 * j)
+                                          : f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int j = 0; j < 16; ++j)
+            if (i0 + 4 * j < ep.ss_n) t += (q4[j][0] + q4[j][1]) + (q4[j][2] + q4[j][3]);
+        }
+        s_rs[r] = rsqrtf(t / (float)(64 * ep.ss_n) + ep.ss_eps);
+      }
+      __syncthreads();
+    }
     constexpr int PASSES = TM / EROWS;
 #pragma unroll
     for (int ps = 0; ps < PASSES; ++ps) {
-      if (SS_IN && ep.ss_in) {
-        // fused RMSNorm: rstd of this pass's rows from the producer's 64-column partials
-        if (lane < EROWS) {
-          const int m = min(mt * BM + wr * TM + ps * EROWS + lane, P.M - 1);
-          const float* sp = ep.ss_in + (size_t)m * ep.ss_n;
-          float t = 0.f;
-          for (int i = 0; i < ep.ss_n; i += 4) {
-            const f32x4_t q4 = *reinterpret_cast<const f32x4_t*>(sp + i);
-            t += (q4[0] + q4[1]) + (q4[2] + q4[3]);
-          }
-          s_rs[lane] = rsqrtf(t / (float)(64 * ep.ss_n) + ep.ss_eps);
-        }
-      }
+      const float* rs = s_rs + wr * TM + ps * EROWS;  // this pass's rows
 #pragma unroll
       for (int i = 0; i < FPP; ++i)
 #pragma unroll
@@ -466,7 +478,7 @@ struct Kern {
           const int c0 = col_base + pr * 32;
           if (m < P.M && (BN != 192 || c0 < P.N)) {
             if (ep.ss_in) {
-              const float r = s_rs[row];
+              const float r = rs[row];
 #pragma unroll
               for (int q = 0; q < 16; ++q) {
                 g[q] *= r;
@@ -537,7 +549,7 @@ struct Kern {
             if (m < P.M && (lane % FN) == 0) ep.ss_out[(size_t)m * ep.ss_n + (col_base >> 6)] = ssq;
           } else if (m < P.M && (BN != 192 || col_base + j * 16 < P.N)) {
             if (EPI == EPI_QKV && ep.ss_in) {
-              const float r = s_rs[row];
+              const float r = rs[row];
 #pragma unroll
               for (int q = 0; q < 16; ++q) v[q] *= r;
             }
