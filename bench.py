@@ -145,7 +145,9 @@ def main():
         "ms_per_step": round(res["ms_per_step"], 4),
         "higher_is_better": True,
         "scaling": "weak",
-        "vs_baseline": (round(res["tok_s"] / BASELINE_TOK_S, 3) if BASELINE_TOK_S else None),
+        # the reference publishes no benchmark number (its only figure is a ~4.3 tok/s
+        # code-comment anecdote on other hardware, kept below as reference_anecdote_tok_s)
+        "vs_baseline": None,
         "dtype": "bf16" if a.weight_dtype == "bf16" else "bf16 activations, fp8-e4m3 weights (W8A16)",
         "data": f"synthetic prompts, random-init weights ({res['model_name']} architecture)",
         "config": {"model": res["model_name"], "global_batch": res["global_batch"],
@@ -159,8 +161,13 @@ def main():
         "b1_p50_tpot_ms": None if res["b1_p50_tpot_ms"] is None else round(res["b1_p50_tpot_ms"], 4),
         "b1_tok_s": None if res["b1_tok_s"] is None else round(res["b1_tok_s"], 2),
         "mem_pred_gb": res["mem_pred_gb"], "mem_peak_gb": res["mem_peak_gb"],
-        "reference_anecdote_tok_s": 4.3,
+        "reference_anecdote_tok_s": BASELINE_TOK_S,
     }
+    if res.get("transport"):
+        line["config"]["transport"] = res["transport"]
+    if res.get("tokens_mb0"):  # parity digest across layouts (same prompts -> same tokens)
+        import hashlib
+        line["tokens_mb0_sha16"] = hashlib.sha256(json.dumps(res["tokens_mb0"]).encode()).hexdigest()[:16]
     print(json.dumps(line), flush=True)
     if a.json_out:
         with open(a.json_out, "w") as f:

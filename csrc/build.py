@@ -79,9 +79,15 @@ def build(force: bool = False, jobs: int = 8, arch: str = "gfx950", verbose: boo
         list(ex.map(_run, jobs_list))
     out = {}
     klib = os.path.join(OUT, "liblsa_kernels.so")
-    if kobjs and (force or not os.path.exists(klib) or
+    # relink also when the set of translation units changed (a removed kernel file must not
+    # leave its symbols in the library)
+    manifest = os.path.join(OBJ, "liblsa_kernels.objs")
+    listed = open(manifest).read() if os.path.exists(manifest) else ""
+    if kobjs and (force or not os.path.exists(klib) or listed != "\n".join(kobjs) or
                   os.path.getmtime(klib) < max(os.path.getmtime(o) for o in kobjs)):
         _run([hipcc, "-shared", "-fPIC", f"--offload-arch={arch}", *kobjs, "-o", klib])
+        with open(manifest, "w") as f:
+            f.write("\n".join(kobjs))
     out["kernels"] = klib
     clib = os.path.join(OUT, "liblsa_comm.so")
     if cobjs and (force or not os.path.exists(clib) or

@@ -9,8 +9,9 @@
 // Layout (bytes, all 256-B aligned):
 //   inbox  (receiver memory, opened by the sender): flags[R] (u32, padded to 256 B), then R slots
 //   ackbox (sender memory, opened by the receiver): acks[R] (u32)
-//   state  (each endpoint's own memory):           {count, ticket} - messages so far on this edge
-//                                                   end, workgroups done with the current one
+//   state  (each endpoint's own memory):           {count, ticket, fail} - messages so far on
+//                                                   this edge end, workgroups done with the current
+//                                                   one, "a workgroup of this launch gave up"
 // Message n of an edge uses slot n % R with epoch n / R + 1.
 //
 // Messages are any multiple of 4 bytes (16-B chunks + a dword tail).
@@ -23,8 +24,21 @@
 //   memory, which the peer writes over xGMI), reads its share of the slot with sc0 sc1 loads (no
 //   stale L2 / L1 copy of an earlier message can be returned), stores it into dst, drains, takes a
 //   ticket; the last workgroup stores acks[slot] = epoch into the sender's memory, advances count.
-// Every spin is bounded by a wall-clock budget (s_memrealtime, 100 MHz): on timeout a workgroup
-// records a code in *err and returns, so a lost peer ends the launch instead of hanging the GPU.
+// Publication and failure handling:
+//  * every storing wave drains its write-through stores (vmcnt(0)) before its workgroup's ticket;
+//    the ticket is an acq_rel RMW, and the last arriver publishes flags[slot] / acks[slot] with a
+//    SYSTEM-scope release store, so every workgroup's payload happens-before the flag the peer
+//    (another agent) reads; the consumer polls relaxed and takes ONE system-scope acquire load
+//    once the value matches, then reads the slot with sc0 sc1 loads.
+//  * every spin is bounded by a wall-clock budget (s_memrealtime, 100 MHz). A workgroup that
+//    gives up records a code in the endpoint's sticky *err and marks the launch failed
+//    (state[2]) but STILL takes its ticket, so the last arriver always completes the election,
+//    resets the ticket and the failure word, and never publishes a partial message: the ring
+//    state is never left half-advanced for the next launch.
+//  * once *err is set (by any launch of the endpoint) every later launch is poisoned at entry: a
+//    receive fills its destination with 0xFF bytes (bf16 NaN / int -1 ids) instead of reading
+//    the slot, a send stores nothing, neither publishes, and the host's check() raises. A lost
+//    peer therefore ends each launch within the budget and can never yield silent garbage.
 #include <cstdint>
 #include <cstring>
 
@@ -35,41 +49,63 @@ namespace {
 constexpr int IPC_THREADS = 256;
 constexpr int AUX_SYS = 17;  // sc0 | sc1: system-coherent (write-through / cache-bypassing) access
 
-LSA_DEVICE unsigned ld_sys(const unsigned* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); }
-LSA_DEVICE void st_sys(unsigned* p, unsigned v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); }
+LSA_DEVICE unsigned ld_relaxed(const unsigned* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); }
+LSA_DEVICE unsigned ld_acquire(const unsigned* p) { return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM); }
+LSA_DEVICE void st_release(unsigned* p, unsigned v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+LSA_DEVICE unsigned ld_err(const unsigned* err) { return __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 
 LSA_DEVICE __amdgpu_buffer_rsrc_t rsrc_n(const void* base, long long bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
 }
 
-// thread 0 polls *w until pred(value) or the deadline; the verdict is broadcast through LDS
+// thread 0: skip if the endpoint already failed, else poll *w (relaxed) until pred(value) or the
+// deadline, then one acquire load; on timeout record ``code`` and mark the launch failed. The
+// verdict is broadcast through LDS.
 template <bool GE>
-LSA_DEVICE bool wait_word(const unsigned* w, unsigned want, unsigned* err, unsigned code, long long ticks, int* s_ok) {
+LSA_DEVICE bool wait_word(const unsigned* w, unsigned want, unsigned* err, unsigned code, long long ticks,
+                          unsigned* fail, int* s_ok) {
   if (threadIdx.x == 0) {
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    int ok = 1;
-    for (;;) {
-      const unsigned v = ld_sys(w);
-      if (GE ? (int)(v - want) >= 0 : v == want) break;
-      if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > ticks) {
-        ok = 0;
-        atomicMax(err, code);
-        break;
+    int ok = ld_err(err) == 0u;
+    if (ok) {
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      for (;;) {
+        const unsigned v = ld_relaxed(w);
+        if (GE ? (int)(v - want) >= 0 : v == want) {
+          (void)ld_acquire(w);  // orders this workgroup's slot reads after the peer's release
+          break;
+        }
+        if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > ticks) {
+          ok = 0;
+          atomicMax(err, code);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
       }
-      __builtin_amdgcn_s_sleep(2);
     }
+    if (!ok) __hip_atomic_fetch_or(fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     *s_ok = ok;
   }
   __syncthreads();
   return *s_ok != 0;
 }
 
-// last-arriver election over the launch's workgroups (after this workgroup's memory ops drained)
-LSA_DEVICE bool last_arriver(unsigned* ticket, int* s_flag) {
+// last-arriver election over the launch's workgroups (after this workgroup's memory ops
+// drained); every workgroup takes a ticket, failed or not. The winner learns whether any
+// workgroup of the launch failed and resets the ticket and the failure word for the next launch.
+LSA_DEVICE bool last_arriver(unsigned* state, int* s_flag, int* s_failed) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0)
-    *s_flag = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  if (threadIdx.x == 0) {
+    const bool last =
+        __hip_atomic_fetch_add(state + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    *s_flag = last;
+    if (last) {
+      *s_failed = __hip_atomic_exchange(state + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+      __hip_atomic_store(state + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
   __syncthreads();
   return *s_flag != 0;
 }
@@ -78,24 +114,24 @@ __global__ __launch_bounds__(IPC_THREADS) void ipc_send_kernel(const unsigned ch
                                                                unsigned char* peer_slots, long long slot_bytes,
                                                                unsigned* peer_flags, const unsigned* acks, int R,
                                                                unsigned* state, unsigned* err, long long ticks) {
-  __shared__ int s_ok, s_last;
+  __shared__ int s_ok, s_last, s_failed;
   const unsigned n = state[0];
   const int slot = (int)(n % (unsigned)R);
   const unsigned epoch = n / (unsigned)R + 1u;
-  if (!wait_word<true>(acks + slot, epoch - 1u, err, 1u, ticks, &s_ok)) return;
-  const __amdgpu_buffer_rsrc_t dst = rsrc_n(peer_slots + (size_t)slot * slot_bytes, slot_bytes);
-  const long long n16 = nbytes >> 4;
-  for (long long i = (long long)blockIdx.x * IPC_THREADS + threadIdx.x; i < n16; i += (long long)gridDim.x * IPC_THREADS)
-    __builtin_amdgcn_raw_buffer_store_b128(ld16(src + i * 16), dst, (int)(i * 16), 0, AUX_SYS);
-  const int tail = (int)((nbytes & 15) >> 2);  // trailing dwords of a message not a multiple of 16 B
-  if (blockIdx.x == 0 && (int)threadIdx.x < tail) {
-    const int off = (int)(n16 * 16) + 4 * threadIdx.x;
-    __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const unsigned*>(src + off), dst, off, 0, AUX_SYS);
+  if (wait_word<true>(acks + slot, epoch - 1u, err, 1u, ticks, state + 2, &s_ok)) {
+    const __amdgpu_buffer_rsrc_t dst = rsrc_n(peer_slots + (size_t)slot * slot_bytes, slot_bytes);
+    const long long n16 = nbytes >> 4;
+    for (long long i = (long long)blockIdx.x * IPC_THREADS + threadIdx.x; i < n16; i += (long long)gridDim.x * IPC_THREADS)
+      __builtin_amdgcn_raw_buffer_store_b128(ld16(src + i * 16), dst, (int)(i * 16), 0, AUX_SYS);
+    const int tail = (int)((nbytes & 15) >> 2);  // trailing dwords of a message not a multiple of 16 B
+    if (blockIdx.x == 0 && (int)threadIdx.x < tail) {
+      const int off = (int)(n16 * 16) + 4 * threadIdx.x;
+      __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const unsigned*>(src + off), dst, off, 0, AUX_SYS);
+    }
   }
-  if (last_arriver(state + 1, &s_last) && threadIdx.x == 0) {
-    st_sys(peer_flags + slot, epoch);
+  if (last_arriver(state, &s_last, &s_failed) && threadIdx.x == 0 && !s_failed && ld_err(err) == 0u) {
+    st_release(peer_flags + slot, epoch);
     state[0] = n + 1u;
-    state[1] = 0u;
   }
 }
 
@@ -103,24 +139,24 @@ __global__ __launch_bounds__(IPC_THREADS) void ipc_recv_kernel(unsigned char* __
                                                                const unsigned char* slots, long long slot_bytes,
                                                                const unsigned* flags, unsigned* peer_acks, int R,
                                                                unsigned* state, unsigned* err, long long ticks) {
-  __shared__ int s_ok, s_last;
+  __shared__ int s_ok, s_last, s_failed;
   const unsigned n = state[0];
   const int slot = (int)(n % (unsigned)R);
   const unsigned epoch = n / (unsigned)R + 1u;
-  if (!wait_word<false>(flags + slot, epoch, err, 2u, ticks, &s_ok)) return;
+  const bool ok = wait_word<false>(flags + slot, epoch, err, 2u, ticks, state + 2, &s_ok);
   const __amdgpu_buffer_rsrc_t srcr = rsrc_n(slots + (size_t)slot * slot_bytes, slot_bytes);
+  const u32x4_t poison = {~0u, ~0u, ~0u, ~0u};
   const long long n16 = nbytes >> 4;
   for (long long i = (long long)blockIdx.x * IPC_THREADS + threadIdx.x; i < n16; i += (long long)gridDim.x * IPC_THREADS)
-    st16(dst + i * 16, __builtin_amdgcn_raw_buffer_load_b128(srcr, (int)(i * 16), 0, AUX_SYS));
+    st16(dst + i * 16, ok ? __builtin_amdgcn_raw_buffer_load_b128(srcr, (int)(i * 16), 0, AUX_SYS) : poison);
   const int tail = (int)((nbytes & 15) >> 2);
   if (blockIdx.x == 0 && (int)threadIdx.x < tail) {
     const int off = (int)(n16 * 16) + 4 * threadIdx.x;
-    *reinterpret_cast<unsigned*>(dst + off) = __builtin_amdgcn_raw_buffer_load_b32(srcr, off, 0, AUX_SYS);
+    *reinterpret_cast<unsigned*>(dst + off) = ok ? __builtin_amdgcn_raw_buffer_load_b32(srcr, off, 0, AUX_SYS) : ~0u;
   }
-  if (last_arriver(state + 1, &s_last) && threadIdx.x == 0) {
-    st_sys(peer_acks + slot, epoch);
+  if (last_arriver(state, &s_last, &s_failed) && threadIdx.x == 0 && !s_failed && ld_err(err) == 0u) {
+    st_release(peer_acks + slot, epoch);
     state[0] = n + 1u;
-    state[1] = 0u;
   }
 }
 

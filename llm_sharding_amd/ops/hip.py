@@ -71,15 +71,13 @@ def lib() -> ctypes.CDLL:
     L.lsa_layernorm.argtypes = [vp, i, vp, vp, vp, vp, i, i, f, vp, i, vp]
     L.lsa_resid_rmsnorm_partials.argtypes = [vp, i, vp, i, ctypes.c_longlong, i, vp, i, i, f, vp, i, vp]
     L.lsa_row_ss.argtypes = [vp, i, i, i, vp, vp]
-    L.lsa_decode_persistent.argtypes = [vp, i, i, i, i, i, i, i, i, f, f, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i,
-                                        vp, vp, i, i, vp, i, vp, vp, i, vp]
     L.lsa_argmax_finalize.argtypes = [vp, i, vp, vp, i, vp, i, i, vp, vp]
     L.lsa_pos_advance.argtypes = [vp, i, i, vp]
     L.lsa_gemm_sk.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(EpiArgs), i, i, i, i, i, i, i, vp, vp, ctypes.c_longlong, i,
                               vp]
     for name in ("lsa_gemv", "lsa_gemv_coop", "lsa_gemv_fp8", "lsa_dequant_fp8_packed", "lsa_gemv_coop_fp8", "lsa_gemm",
                  "lsa_gemm_sk", "lsa_attn_decode", "lsa_attn_prefill", "lsa_embed", "lsa_rmsnorm", "lsa_layernorm",
-                 "lsa_resid_rmsnorm_partials", "lsa_decode_persistent", "lsa_row_ss",
+                 "lsa_resid_rmsnorm_partials", "lsa_row_ss",
                  "lsa_argmax_finalize", "lsa_pos_advance", "lsa_version"):
         getattr(L, name).restype = ctypes.c_int
     _lib = L
@@ -374,7 +372,10 @@ def _sk_load() -> None:
             for e in json.load(f).get("entries", []):
                 _SK_TUNED.setdefault((e["N"], e["K"]), []).append((e["M"], tuple(e["cfg"])))
                 if "partial" in e:  # measured on a residual projection: [bn, split] or null
-                    _SK_PARTIAL.setdefault((e["N"], e["K"]), []).append((e["M"], e["partial"]))
+                    pp = e["partial"]
+                    if pp is not None and not (1 <= pp[1] <= PARTIAL_MAX_SPLIT):
+                        pp = None  # the engine's partial buffer holds PARTIAL_MAX_SPLIT K ranges
+                    _SK_PARTIAL.setdefault((e["N"], e["K"]), []).append((e["M"], pp))
 
 
 def _sk_tuned() -> dict:
@@ -436,11 +437,12 @@ def gemm_sk_plan(M: int, N: int, K: int, tuned: bool = True) -> tuple:
 
 def gemm_sk(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep: EpiArgs,
             bn: int = 0, grid: int = 0, dp: int = 1, group_m: int = 8, nb: int = 0, split: int = -1,
-            ws: Optional[SkWorkspace] = None, bm: int = 0) -> None:
+            ws: Optional[SkWorkspace] = None, bm: int = 0, out_numel: int = 0) -> None:
     """Projection GEMM for any M (gemm_sk.hip): ``bm`` x ``bn`` tiles (bm 256 / 128), LDS-DMA
     staged, data-parallel rounds + stream-K, fused epilogue. ``wp`` = pack_b(W[N, K]); K % 64
     == 0; N % bn == 0 for bn = 128 / 256, N % 16 == 0 for bn = 192 (partial last column tile).
-    bn = bm = 0: the plan's (gemm_sk_plan)."""
+    bn = bm = 0: the plan's (gemm_sk_plan). EPI_PARTIAL writes ``split`` x M x ldo fp32 values
+    to ``ep.out``: ``out_numel`` (its capacity in floats) is required and checked first."""
     _req(_is_bf16_cuda(a, wp), "gemm_sk: bf16 cuda tensors required")
     _req(wp.numel() == N * K and K % 64 == 0 and K >= 64, "gemm_sk: packed weight shape")
     _req(a.dim() == 2 and a.shape[0] >= M >= 1 and a.shape[1] >= K and a.stride(1) == 1 and a.stride(0) % 8 == 0,
@@ -450,6 +452,8 @@ def gemm_sk(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int,
     _req(epi in (EPI_STORE, EPI_RESID, EPI_SWIGLU, EPI_QKV, EPI_PARTIAL, EPI_ARGMAX), f"gemm_sk: epilogue {epi} not supported")
     if epi == EPI_PARTIAL:  # exactly `split` K ranges per tile, every tile in one round
         _req(bn in (128, 192, 256) and split >= 1 and grid >= 1, "gemm_sk partial: explicit bn, grid and split required")
+        _req(out_numel >= split * M * ep.ldo, f"gemm_sk partial: output holds {out_numel} floats, "
+             f"split {split} x {M} rows x ldo {ep.ldo} needed")
     pb, pg, pd, ps, pm = gemm_sk_plan(M, N, K)
     if ep.ss_out and pb == 192:  # the fused-norm partials are per 64 columns of one wave (TN = 64)
         pb = 256 if N % 256 == 0 else 128
@@ -629,36 +633,6 @@ def resid_rmsnorm_partials(h: torch.Tensor, partials: torch.Tensor, S: int, rows
     rc = lib().lsa_resid_rmsnorm_partials(_p(h), h.stride(0), _p(partials), S, rows * H, H, _p(w), rows, H, float(eps),
                                           _p(out), 0 if out is None else out.stride(0), _stream())
     _check(rc, "lsa_resid_rmsnorm_partials")
-
-
-def decode_persistent(layers: torch.Tensor, n_layers: int, H: int, I: int, nh: int, nkv: int, hd: int, t_max: int,
-                      eps: float, slot: torch.Tensor, pos: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor,
-                      h: torch.Tensor, q: torch.Tensor, attn_out: torch.Tensor, act: torch.Tensor,
-                      bar: torch.Tensor, err: torch.Tensor, embed: Optional[torch.Tensor] = None,
-                      tokens: Optional[torch.Tensor] = None, head: Optional[torch.Tensor] = None, head_n: int = 0,
-                      keys: Optional[torch.Tensor] = None, history: Optional[torch.Tensor] = None,
-                      step_ctr: Optional[torch.Tensor] = None, pos_inc: int = 1, grid: int = 0) -> None:
-    """One batch-1 decode step of a stage as ONE persistent launch (decode_persistent.hip):
-    [embed] -> layers (qkv+norm+RoPE+KV, attention, o+resid, gate_up+norm+SwiGLU, down+resid)
-    -> [final norm + lm_head + argmax -> tokens/history] -> pos += pos_inc. ``layers``: int64
-    [n_layers, 6] device table of (qkv, o, gate_up, down, k_cache, v_cache) pointers (packed
-    bf16 weights with the norms folded). ``bar``: int32[>= grid] barrier epoch flags, zeroed
-    once and never reset; ``err``: int32[1], set to 1 if a barrier timed out (the grid was not
-    resident)."""
-    _req(layers.dtype == torch.int64 and layers.is_cuda and layers.shape == (n_layers, 6), "persistent: layer table")
-    _req(_is_bf16_cuda(h, q, attn_out, act, embed, head), "persistent: bf16 cuda buffers")
-    _req(bar.dtype == torch.int32 and bar.numel() >= (grid or N_CU) and err.dtype == torch.int32,
-         "persistent: barrier state")
-    _req(slot.dtype == torch.int32 and pos.dtype == torch.int32, "persistent: int32 slot/pos")
-    _req(cos is not None and cos.dtype == torch.float32 and sin.dtype == torch.float32, "persistent: RoPE tables")
-    _req(embed is None or (tokens is not None and tokens.dtype == torch.int32), "persistent: tokens")
-    _req(head is None or (keys is not None and keys.dtype == torch.int64 and head_n % 16 == 0), "persistent: head")
-    hs, hl = (history.stride(0), history.shape[0]) if history is not None else (0, 0)
-    rc = lib().lsa_decode_persistent(_p(layers), n_layers, 1, H, I, nh, nkv, hd, t_max, float(eps), float(hd ** -0.5),
-                                     _p(slot), _p(pos), _p(cos), _p(sin), _p(h), _p(q), _p(attn_out), _p(act),
-                                     _p(embed), _p(tokens), _p(head), head_n, _p(keys), _p(history), hs, hl,
-                                     _p(step_ctr), pos_inc, _p(bar), _p(err), grid or N_CU, _stream())
-    _check(rc, "lsa_decode_persistent")
 
 
 def gemm_sk_partial_plan(M: int, N: int, K: int) -> Optional[tuple]:

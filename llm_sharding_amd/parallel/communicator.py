@@ -123,6 +123,11 @@ class Communicator:
         self._fault_drop = 0
         self.device = device
         self._pending_sends: list = []
+        # set once an rccl tensor receive timed out: its irecv stays posted on the edge group (it
+        # cannot be cancelled), so a late message would land one receive off - every later
+        # send / receive raises instead of silently returning misaligned data
+        self.failed: Optional[str] = None
+        self._orphans: list = []  # (work, tensor) of timed-out receives: keep the target alive
         if backend == "rccl":
             import torch.distributed as dist
             if not dist.is_initialized():
@@ -170,7 +175,12 @@ class Communicator:
         return self.dst_addr
 
     # -- data --------------------------------------------------------------------------
+    def _check_failed(self) -> None:
+        if self.failed:
+            raise RuntimeError(f"communicator unusable after an earlier failure: {self.failed}")
+
     def transfer_data(self, data, data_path: str = "results/send_data.pt", keep_data: bool = False):
+        self._check_failed()
         tensors: list = []
         if self.backend == "rccl":
             data = _extract_tensors(data, tensors)
@@ -191,6 +201,7 @@ class Communicator:
 
     def receive_data(self, no_block: bool = False, data_path: str = "results/recv_data.pt",
                      keep_data: bool = False, timeout_ms: Optional[int] = None):
+        self._check_failed()
         tmo = 0 if no_block else (-1 if timeout_ms is None else int(timeout_ms))
         if self.backend in ("tcp", "rccl"):
             payload = self.recv_socket.recv_bytes(tmo)
@@ -232,11 +243,17 @@ class Communicator:
         try:
             ok = work.wait(timeout=datetime.timedelta(seconds=self.recv_timeout_s))
         except RuntimeError as e:  # backend-specific timeout error
-            raise RuntimeError(f"rccl recv from rank {self.src_rank} failed or timed out "
-                               f"({self.recv_timeout_s:.0f} s): {e}") from e
+            self._fail(work, t, f"rccl recv from rank {self.src_rank} failed or timed out "
+                                f"({self.recv_timeout_s:.0f} s): {e}")
+            raise RuntimeError(self.failed) from e
         if ok is False:
-            raise RuntimeError(f"rccl recv from rank {self.src_rank} timed out ({self.recv_timeout_s:.0f} s)")
+            self._fail(work, t, f"rccl recv from rank {self.src_rank} timed out ({self.recv_timeout_s:.0f} s)")
+            raise RuntimeError(self.failed)
         return t
+
+    def _fail(self, work, t, why: str) -> None:
+        self.failed = why
+        self._orphans.append((work, t))
 
     def flush(self, timeout_ms: int = 5000) -> bool:
         for w, _ in self._pending_sends:

@@ -13,9 +13,14 @@ Per directed edge ``src -> dst`` (default: the pipeline ring r -> r+1 plus the b
   * dst allocates the inbox (R flag words + R slots of ``slot_bytes``), src the ack box (R words);
   * handles go through one ``all_gather_object`` on a gloo group (a control-plane exchange at
     construction only); each side maps the other's buffer with ``hipIpcOpenMemHandle``.
-A message must be a multiple of 4 bytes and at most ``slot_bytes``. Up to R messages per edge
+A message must be a multiple of 4 bytes; one larger than ``slot_bytes`` (a prompt prefill's
+hidden states) is carried as consecutive slot-sized chunks, so every message of a run - decode
+and prefill - can go through the rings with no communicator at all. Up to R messages per edge
 are in flight; a sender that runs R ahead waits in-kernel for the receiver's ack. Every spin is
-bounded (``timeout_s``); :meth:`check` raises if any launch timed out.
+bounded (``timeout_s``, env ``LSA_IPC_TIMEOUT_S``): a launch that gives up sets a sticky error
+word, poisons its receive buffer (0xFF bytes) instead of returning stale data, and every later
+launch of the endpoint is poisoned too; :meth:`check` raises once that happened.
+An edge whose two ends are the same rank (loopback) works without IPC mapping.
 """
 from __future__ import annotations
 
@@ -70,11 +75,15 @@ class IpcRingP2P:
     graph_capturable = True  # sends / receives may be captured in a hipGraph (device-side indices)
 
     def __init__(self, rank: int, slot_bytes: int, slots: int = 4, ranks: Optional[list] = None,
-                 edges: Optional[list] = None, group=None, timeout_s: float = 30.0, grid: int = 32):
+                 edges: Optional[list] = None, group=None, timeout_s: Optional[float] = None, grid: int = 32):
+        import os
+
         import torch.distributed as dist
         self.rank, self.R, self.grid = rank, int(slots), int(grid)
         hip._req(1 <= self.R <= _FLAG_BYTES // 4, f"ipc ring: 1..{_FLAG_BYTES // 4} slots")
         self.slot_bytes = -(-int(slot_bytes) // 256) * 256
+        if timeout_s is None:
+            timeout_s = float(os.environ.get("LSA_IPC_TIMEOUT_S", "30"))
         self.timeout_us = int(timeout_s * 1e6)
         self.ranks = ranks
         world = dist.get_world_size() if dist.is_initialized() else 1
@@ -114,15 +123,22 @@ class IpcRingP2P:
             theirs.update(d or {})
         self.peer_inbox, self.peer_acks = {}, {}
         for e in self.edges:
+            if e[0] == rank == e[1]:  # loopback edge: both buffers are our own
+                self.peer_inbox[e], self.peer_acks[e] = self.inbox[e], self.ackbox[e]
+                continue
             if e[0] == rank:  # sender: map the receiver's inbox
                 self.peer_inbox[e] = self._open(theirs[(e, "inbox")])
             if e[1] == rank:  # receiver: map the sender's ack box
                 self.peer_acks[e] = self._open(theirs[(e, "acks")])
-        # per edge end: {count, ticket}; one error word for every launch of this endpoint. Each edge
+        # per edge end: {count, ticket, fail}; one error word for every launch of this endpoint. Each edge
         # end issues on its own stream (ordered against the caller's by events), so sends of one
         # edge made from several compute streams still run one at a time, in issue order
-        self.state = {e: torch.zeros(2, dtype=torch.int32, device=self.dev) for e in self.edges if rank in e}
+        self.state = {e: torch.zeros((2, 4) if e[0] == e[1] else 4, dtype=torch.int32, device=self.dev)
+                      for e in self.edges if rank in e}
         self.streams = {e: torch.cuda.Stream(self.dev) for e in self.state}
+        for e in self.state:  # a loopback edge's receive must not queue behind its own send
+            if e[0] == e[1]:
+                self.streams[(e, "recv")] = torch.cuda.Stream(self.dev)
         self.captured_ops = 0  # sends / receives recorded into hipGraphs (diagnostics)
         self.err = torch.zeros(1, dtype=torch.int32, device=self.dev)
         if dist.is_initialized():
@@ -137,24 +153,34 @@ class IpcRingP2P:
     def _global(self, stage: int) -> int:
         return self.ranks[stage] if self.ranks is not None else stage
 
+    def _state(self, e, send: bool) -> int:
+        st = self.state[e]
+        return (st[0] if send else st[1]).data_ptr() if e[0] == e[1] else st.data_ptr()
+
     @staticmethod
-    def _nbytes(t: torch.Tensor) -> int:
-        n = t.numel() * t.element_size()
-        hip._req(t.is_cuda and t.is_contiguous() and n % 4 == 0 and t.data_ptr() % 16 == 0,
-                 "ipc ring: contiguous 16-B aligned cuda tensor, bytes % 4 == 0")
-        return n
+    def _staged(t: torch.Tensor) -> bool:
+        """Tensors the kernels cannot address directly (non-contiguous or not 16-B aligned) go
+        through a private contiguous copy; routing never depends on it (only on byte counts)."""
+        return not (t.is_contiguous() and t.data_ptr() % 16 == 0)
+
+    def _chunks(self, n: int):
+        hip._req(n > 0 and n % 4 == 0, "ipc ring: message bytes must be a positive multiple of 4")
+        return [(o, min(self.slot_bytes, n - o)) for o in range(0, n, self.slot_bytes)]
 
     def isend(self, t: torch.Tensor, dst: int):
         e = (self.rank, self._global(dst))
-        n = self._nbytes(t)
-        hip._req(n <= self.slot_bytes, f"ipc ring: message {n} B > slot {self.slot_bytes} B")
+        hip._req(t.is_cuda, "ipc ring: cuda tensor")
+        src = t.contiguous().clone() if self._staged(t) else t
+        n = src.numel() * src.element_size()
         base = self.peer_inbox[e]
         cur, cs = torch.cuda.current_stream(self.dev), self.streams[e]
         cs.wait_stream(cur)
-        _ok(_lib().lsa_ipc_send(t.data_ptr(), n, base + _FLAG_BYTES, self.slot_bytes, base, self.ackbox[e], self.R,
-                                self.state[e].data_ptr(), self.err.data_ptr(), self.timeout_us, self.grid,
-                                cs.cuda_stream), "lsa_ipc_send")
-        t.record_stream(cs)
+        L = _lib()
+        for off, nb in self._chunks(n):
+            _ok(L.lsa_ipc_send(src.data_ptr() + off, nb, base + _FLAG_BYTES, self.slot_bytes, base, self.ackbox[e],
+                               self.R, self._state(e, True), self.err.data_ptr(), self.timeout_us, self.grid,
+                               cs.cuda_stream), "lsa_ipc_send")
+        src.record_stream(cs)
         if torch.cuda.is_current_stream_capturing():
             self.captured_ops += 1
             cur.wait_stream(cs)  # a captured send joins the capturing stream before the capture ends
@@ -165,27 +191,38 @@ class IpcRingP2P:
 
     def recv(self, t: torch.Tensor, src: int) -> None:
         e = (self._global(src), self.rank)
-        n = self._nbytes(t)
-        hip._req(n <= self.slot_bytes, f"ipc ring: message {n} B > slot {self.slot_bytes} B")
+        hip._req(t.is_cuda, "ipc ring: cuda tensor")
+        dst = torch.empty(t.shape, dtype=t.dtype, device=t.device) if self._staged(t) else t
+        n = dst.numel() * dst.element_size()
         base = self.inbox[e]
-        cur, cs = torch.cuda.current_stream(self.dev), self.streams[e]
+        cur, cs = torch.cuda.current_stream(self.dev), self.streams.get((e, "recv"), self.streams[e])
         cs.wait_stream(cur)
-        _ok(_lib().lsa_ipc_recv(t.data_ptr(), n, base + _FLAG_BYTES, self.slot_bytes, base, self.peer_acks[e], self.R,
-                                self.state[e].data_ptr(), self.err.data_ptr(), self.timeout_us, self.grid,
-                                cs.cuda_stream), "lsa_ipc_recv")
-        t.record_stream(cs)
+        L = _lib()
+        for off, nb in self._chunks(n):
+            _ok(L.lsa_ipc_recv(dst.data_ptr() + off, nb, base + _FLAG_BYTES, self.slot_bytes, base, self.peer_acks[e],
+                               self.R, self._state(e, False), self.err.data_ptr(), self.timeout_us, self.grid,
+                               cs.cuda_stream), "lsa_ipc_recv")
+        dst.record_stream(cs)
         self.captured_ops += int(torch.cuda.is_current_stream_capturing())
         cur.wait_stream(cs)
+        if dst is not t:
+            t.copy_(dst)
 
     def fits(self, t: torch.Tensor) -> bool:
+        """One ring slot, decided by the byte count only (both ends of an edge agree on it)."""
         n = t.numel() * t.element_size()
-        return t.is_cuda and t.is_contiguous() and n % 4 == 0 and n <= self.slot_bytes and t.data_ptr() % 16 == 0
+        return t.is_cuda and n % 4 == 0 and 0 < n <= self.slot_bytes
+
+    def error_code(self) -> int:
+        return int(self.err.item())
 
     def check(self) -> None:
-        """Raise if any send (1: no ack) or receive (2: no message) gave up waiting."""
-        code = int(self.err.item())
+        """Raise if any send (1: no ack) or receive (2: no message) of this endpoint gave up
+        waiting - from then on its receives deliver poison (0xFF bytes), never stale data."""
+        code = self.error_code()
         if code:
-            raise RuntimeError(f"ipc ring: a {'send' if code == 1 else 'receive'} timed out waiting for its peer")
+            raise RuntimeError(f"ipc ring: a {'send' if code == 1 else 'receive'} timed out waiting for its peer "
+                               f"(rank {self.rank}); the edge is poisoned")
 
     def close(self) -> None:
         """Unmap the peers' buffers, then (once every rank has unmapped ours) free our own."""
@@ -204,7 +241,7 @@ class IpcRingP2P:
 class HybridP2P:
     """Messages that fit a ring slot go through ``ipc`` (IpcRingP2P), larger ones (the prompt
     prefill's hidden states) through ``fallback`` (DistP2P / RCCL). Both ends decide by the
-    message's size, so each channel stays FIFO per edge."""
+    message's byte count only (:meth:`IpcRingP2P.fits`), so each channel stays FIFO per edge."""
 
     graph_capturable = True  # what fits the ring (every decode message) is graph-capturable
 
@@ -222,3 +259,6 @@ class HybridP2P:
             self.ipc.recv(t, src)
         else:
             self.fallback.recv(t, src)
+
+    def check(self) -> None:
+        self.ipc.check()

@@ -141,8 +141,7 @@ class PipelineStage:
                  microbatches: int, max_seq: int, source, use_graph: bool = True,
                  max_prefill_rows: int = 2048, dtype=torch.bfloat16, p2p=None,
                  split_head: Optional[bool] = None, weight_dtype: str = "bf16", streams: int = 1,
-                 pp_streams: Optional[bool] = None, engine: Optional[StageEngine] = None,
-                 persistent: bool = False):
+                 pp_streams: Optional[bool] = None, engine: Optional[StageEngine] = None):
         """``engine``: reuse a loaded StageEngine (its weights, KV cache and scratch) instead of
         building one - e.g. a batch-1 latency pass after a throughput pass; it must cover this
         stage's layers and hold >= batch x microbatches KV slots."""
@@ -187,7 +186,6 @@ class PipelineStage:
             self.seed = [None] * microbatches   # stage 0: (h_fin, keys) of each micro-batch's prefill
             self.final_tokens = [None] * microbatches
         self.graphs: list = []
-        self.persistent = persistent  # batch-1 decode graphs run decode_persistent.hip where eligible
         self.send_works: dict = {}
         self.tokens_ready = [True] * microbatches  # stage 0: next-step token ids are in place
         self.tl = tracing.from_env(rank, self.device if self.gpu else "cpu")  # LSA_TRACE=dir
@@ -299,7 +297,7 @@ class PipelineStage:
         self.graphs = []
         for mb in range(self.M):
             # micro-batches that share a stream replay one after another: one scratch set each
-            extra = {"scratch": mb % self.S, "persistent": self.persistent} if self.gpu else {}
+            extra = {"scratch": mb % self.S} if self.gpu else {}
             cls = DecodeGraph if self.gpu else EagerDecode
             if self.split and mode in ("first", "last"):
                 # stage 0 re-derives token s at step s: one more history row than the last stage keeps
@@ -437,6 +435,9 @@ class PipelineStage:
         for k in list(self.send_works):
             self._wait_send(k)
         self.join_streams()
+        chk = getattr(self.p2p, "check", None)
+        if chk is not None:  # a transport with device-side timeouts (IPC ring): surface them here
+            chk()
 
     def _drain_mb(self, mb: int, g) -> None:
         if self.split:
@@ -557,8 +558,7 @@ def _latency_pass(cfg, stage: "PipelineStage", srank: int, pp: int, st, dev, max
     eng = stage.eng
     eng.reset([0])
     b1 = PipelineStage(cfg, srank, pp, st.start, st.end, dev, 1, 1, max_seq, None,
-                       use_graph=stage.use_graph, dtype=stage.dtype, p2p=p2p, engine=eng,
-                       persistent=os.environ.get("LSA_PERSISTENT", "0") == "1")
+                       use_graph=stage.use_graph, dtype=stage.dtype, p2p=p2p, engine=eng)
     b1.tl = stage.tl
     p1 = prompts[:1, :1].contiguous() if prompts is not None else None
     firsts = b1.prefill(p1, prompt_len)
@@ -604,9 +604,12 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
     cut to that many decoder layers (embedding and lm_head kept), e.g. one 10-layer stage of
     Llama-2-70B's 8-stage plan on one GPU with ``microbatches=8`` to hold that stage's KV.
 
-    ``transport`` "ipc": decode-step messages (hidden states, argmax keys, token ids) go through
-    IPC-mapped rings in the receiver's HBM (parallel/ipc_ring.py: one kernel per send / receive,
-    device flags, no communicator); the prompt prefill's larger messages stay on RCCL."""
+    ``transport`` "ipc": every stage hand-off (decode hidden states, argmax keys, token ids, and
+    the prompt prefill's hidden states as slot-sized chunks) goes through IPC-mapped rings in the
+    receiver's HBM (parallel/ipc_ring.py: one kernel per send / receive, device flags, no
+    communicator); the process group is then gloo (barriers and the final statistics only), so
+    N ranks may also share ONE GPU (``LOCAL_RANK % device_count``) - a multi-process rehearsal
+    of the exact N-stage pipeline on a 1-GPU box. A timed-out hand-off raises (exit non-zero)."""
     cfg = get_preset(model)
     if stage_layers:
         import dataclasses
@@ -629,13 +632,16 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
     else:
         dev = torch.device("cpu")
     dist = None
+    ipc_only = transport == "ipc" and gpu and pp > 1
+    if transport not in ("rccl", "ipc"):
+        raise ValueError(f"transport {transport!r}: rccl or ipc")
     if world > 1:
         import datetime
 
         import torch.distributed as dist
         # a stuck peer surfaces as an error after 5 minutes instead of the 10-minute default
         tmo = datetime.timedelta(seconds=int(os.environ.get("LSA_DIST_TIMEOUT_S", "300")))
-        if gpu:
+        if gpu and not ipc_only:
             dist.init_process_group("nccl", device_id=dev, timeout=tmo)
         else:
             dist.init_process_group("gloo", timeout=tmo)
@@ -661,15 +667,13 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
     if verbose and rank == 0:
         print(f"[bench] {cfg.name} {'dp%d x ' % dp if dp > 1 else ''}pp{pp} plan: {plan.summary()}", flush=True)
     rings = [list(range(d * pp, (d + 1) * pp)) for d in range(dp)]
-    p2p = DistP2P(ranks=rings[replica], rings=rings)
-    if transport == "ipc" and gpu and pp > 1:
-        from .ipc_ring import HybridP2P, IpcRingP2P
+    if ipc_only:
+        from .ipc_ring import IpcRingP2P
         edges = [(r[i], r[(i + 1) % pp]) for r in rings for i in range(pp)]
-        ipc = IpcRingP2P(rank, slot_bytes=batch * cfg.hidden_size * 2, slots=min(64, max(2, M)),
+        p2p = IpcRingP2P(rank, slot_bytes=batch * cfg.hidden_size * 2, slots=min(64, max(2, M)),
                          ranks=rings[replica], edges=edges)
-        p2p = HybridP2P(ipc, p2p)
-    elif transport not in ("rccl", "ipc"):
-        raise ValueError(f"transport {transport!r}: rccl or ipc")
+    else:
+        p2p = DistP2P(ranks=rings[replica], rings=rings)
     t0 = time.perf_counter()
     stage = PipelineStage(cfg, srank, pp, st.start, st.end, dev, batch, M, max_seq,
                           RandomSource(cfg, seed), use_graph=use_graph,
@@ -736,9 +740,13 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
         lat_p50, lat_el = _latency_pass(cfg, stage, srank, pp, st, dev, max_seq, prompts, prompt_len,
                                         latency_steps, dist, sync, p2p)
     mem_peak = float(torch.cuda.max_memory_allocated(dev)) if gpu else 0.0
+    chk = getattr(p2p, "check", None)
+    if chk is not None:
+        chk()  # a timed-out IPC hand-off ends the run with an error, never with poisoned tokens
     stats = torch.tensor([elapsed, ttft_ms, _percentile(tpot, 0.5) if tpot else 0.0,
                           _percentile(tpot, 0.9) if tpot else 0.0, load_s, lat_el, lat_p50,
-                          mem_pred["total"], mem_peak], dtype=torch.float64, device=dev)
+                          mem_pred["total"], mem_peak], dtype=torch.float64,
+                         device="cpu" if ipc_only else dev)  # gloo gathers host tensors
     if not gpu and stage.last:  # no device events on CPU: wall-clock step time stands in for TPOT
         stats[2] = stats[3] = elapsed * 1e3 / steps
     if dist:
@@ -775,6 +783,7 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
         "load_s": load_s,
         "plan": plan.ranges(),
         "tokens_mb0": tokens_mb0,  # rank 0 only when it holds the history (1 stage or split head)
+        "transport": transport if pp > 1 else None,
         "b1_p50_tpot_ms": lat_p50 if latency_steps > 0 else None,
         "b1_tok_s": (dp * latency_steps / lat_el) if latency_steps > 0 and lat_el > 0 else None,
         # max over ranks: the memory model's stage bytes and torch's measured peak allocation
@@ -787,6 +796,8 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
     if stage.history_stage and verbose:
         hist = stage.graphs[0].history[:8, :4].cpu().tolist() if stage.graphs[0].history is not None else []
         print(f"[bench] rank {rank} sample tokens (step x seq): {hist}", flush=True)
+    if ipc_only:
+        p2p.close()
     if dist:
         dist.barrier()
         dist.destroy_process_group()

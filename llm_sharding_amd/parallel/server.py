@@ -22,6 +22,14 @@ and rank 0 - the stage that owns the embedding - is also the ingress and the sch
 A slot whose request finished is re-armed (device position reset) with the next command of
 its micro-batch; a free slot still rides along in graph replays (its outputs are ignored),
 which keeps the graph static.
+
+Live re-sharding (the reference's hot re-configuration, ``/root/reference/utils/node_worker.py
+:445-474``, on the deployed pipeline): :meth:`request_replan` (rank 0; the master's ``replan``
+command arrives through the ingress) stops admitting requests, lets every request in flight
+finish on the current layer split, then broadcasts ``REPLAN`` with the new stage boundaries in
+the same ordered command stream; every rank drains its sends, frees its engine, loads its new
+``[start, end)`` range, rebuilds KV cache and decode graphs, and rank 0 resumes admission. The
+ring edges (and their communicators) are unchanged - only the layer ranges move.
 """
 from __future__ import annotations
 
@@ -38,7 +46,7 @@ from ..runtime.engine import DecodeGraph, StageEngine
 from ..utils import tracing
 from .pipeline import DistP2P, _percentile
 
-CMD_DECODE, CMD_PREFILL, CMD_STOP = 1, 2, 3
+CMD_DECODE, CMD_PREFILL, CMD_STOP, CMD_REPLAN = 1, 2, 3, 4
 WAITING, PREFILLING, DECODING, DONE = "waiting", "prefilling", "decoding", "done"
 
 
@@ -69,10 +77,11 @@ class Request:
 
 
 class _Header:
-    """int32 command header: [cmd, mb, n_items, n_resets, items (slot, p0, n, emit)..., resets...]."""
+    """int32 command header: [cmd, mb, n_items, n_resets, items (slot, p0, n, emit)..., resets...];
+    REPLAN: [cmd, 0, world + 1, 0, stage boundaries...]."""
 
-    def __init__(self, batch: int):
-        self.size = 4 + 4 * batch + batch
+    def __init__(self, batch: int, world: int = 1):
+        self.size = 4 + max(4 * batch + batch, world + 1)
 
     def pack(self, cmd, mb, items=(), resets=()) -> torch.Tensor:
         t = torch.zeros(self.size, dtype=torch.int32)
@@ -114,12 +123,12 @@ class PipelineServer:
         self.dtype = torch.bfloat16 if self.gpu else dtype
         self.budget = int(prefill_budget)
         self.verbose = verbose
-        self.eng = StageEngine(cfg, start, end, self.device, self.dtype, has_embed=self.first, has_head=self.last,
-                               source=source, max_slots=batch * microbatches, max_seq=max_seq,
-                               max_prefill_rows=max(self.budget, batch), causal=causal)
+        self.source, self.causal, self.max_seq = source, causal, max_seq
+        self.start, self.end = start, end
+        self.eng = self._build_engine(start, end)
         self.p2p = p2p if p2p is not None else DistP2P()
         self.ctrl = ctrl_group
-        self.hdr = _Header(batch)
+        self.hdr = _Header(batch, world)
         self.graphs: List = []
         # Concurrent micro-batches (one GPU, graph mode): every command of micro-batch mb -
         # prefill, decode replay, result collection - runs on stream mb % S against engine
@@ -127,15 +136,7 @@ class PipelineServer:
         # GPU at once (see pipeline.PipelineStage); a micro-batch's own commands stay ordered.
         self.S = max(1, min(streams, microbatches)) if (self.graph_mode and world == 1) else 1
         self.streams = [torch.cuda.Stream(self.device) for _ in range(self.S)] if self.S > 1 else []
-        for k in range(1, self.S):
-            self.eng.decode_scratch(k, rows=self.eng.max_prefill_rows)
-        if self.graph_mode:
-            mode = "full" if world == 1 else ("first" if self.first else ("last" if self.last else "mid"))
-            for mb in range(microbatches):
-                self.graphs.append(DecodeGraph(self.eng, batch, mode, slots=self._slots(mb),
-                                               scratch=mb % self.S).capture())
-        for st in self.streams:  # after weight loading and graph capture on the current stream
-            st.wait_stream(torch.cuda.current_stream(self.device))
+        self._build_graphs()
         # rank 0 state
         self.incoming: "queue.Queue[Request]" = queue.Queue()
         self.waiting: List[Request] = []
@@ -149,9 +150,75 @@ class PipelineServer:
         self._ctrl_works: list = []
         self._send_works: list = []
         self._lock = threading.Lock()
+        self._replan: Optional[list] = None  # rank 0: stage boundaries waiting for a drained pipeline
+        self.replans = 0
         self.tokens_generated = 0
         self.t_start = None
         self.tl = tracing.from_env(rank, self.device)  # LSA_TRACE=dir -> per-rank Chrome trace
+
+    # ------------------------------------------------------------------ engine (re)build
+    def _build_engine(self, start: int, end: int) -> StageEngine:
+        return StageEngine(self.cfg, start, end, self.device, self.dtype, has_embed=self.first, has_head=self.last,
+                           source=self.source, max_slots=self.B * self.M, max_seq=self.max_seq,
+                           max_prefill_rows=max(self.budget, self.B), causal=self.causal)
+
+    def _build_graphs(self) -> None:
+        for k in range(1, self.S):
+            self.eng.decode_scratch(k, rows=self.eng.max_prefill_rows)
+        self.graphs = []
+        if self.graph_mode:
+            mode = "full" if self.world == 1 else ("first" if self.first else ("last" if self.last else "mid"))
+            for mb in range(self.M):
+                self.graphs.append(DecodeGraph(self.eng, self.B, mode, slots=self._slots(mb),
+                                               scratch=mb % self.S).capture())
+        for st in self.streams:  # after weight loading and graph capture on the current stream
+            st.wait_stream(torch.cuda.current_stream(self.device))
+
+    def _reshard(self, start: int, end: int) -> None:
+        """Every rank, pipeline drained: free this stage's engine, load layers [start, end),
+        rebuild the KV cache and the decode graphs (same slots, micro-batches and streams)."""
+        self._flush_sends()
+        if self.gpu:
+            torch.cuda.synchronize(self.device)
+        with self.tl.span("replan", start=start, end=end):
+            self.graphs = []
+            self.eng = None
+            if self.gpu:
+                torch.cuda.empty_cache()
+            self.eng = self._build_engine(start, end)
+            self.start, self.end = start, end
+            self._build_graphs()
+            if self.gpu:
+                torch.cuda.synchronize(self.device)
+        self.cur_tok.clear()
+        self.pending_resets = [[] for _ in range(self.M)]
+        self.replans += 1
+        if self.verbose:
+            print(f"[INFO] rank {self.rank}: re-sharded to layers [{start}, {end})", flush=True)
+
+    def request_replan(self, stages) -> None:
+        """Rank 0 (thread-safe): move the layer split to ``stages`` ([[start, end], ...] per rank,
+        contiguous from 0 to num_hidden_layers). New requests wait; requests in flight finish
+        on the current split first (:meth:`serve` applies it once the pipeline is drained)."""
+        if not self.first:
+            raise RuntimeError("re-plans are requested on rank 0 (the pipeline's command stream)")
+        st = [(int(a), int(b)) for a, b in stages]
+        L = self.cfg.num_hidden_layers
+        ok = (len(st) == self.world and st[0][0] == 0 and st[-1][1] == L
+              and all(a < b for a, b in st) and all(x[1] == y[0] for x, y in zip(st, st[1:])))
+        if not ok:
+            raise ValueError(f"replan: {st} is not a contiguous split of {L} layers over {self.world} stages")
+        with self._lock:
+            self._replan = [a for a, _ in st] + [L]
+
+    def _apply_replan(self) -> None:
+        with self._lock:
+            bounds, self._replan = self._replan, None
+        t = torch.zeros(self.hdr.size, dtype=torch.int32)
+        t[0], t[2] = CMD_REPLAN, len(bounds)
+        t[4:4 + len(bounds)] = torch.tensor(bounds, dtype=torch.int32)
+        self._bcast_header(t)
+        self._reshard(bounds[0], bounds[1])
 
     # ------------------------------------------------------------------ helpers
     def _mb_ctx(self, mb: int):
@@ -392,9 +459,9 @@ class PipelineServer:
     def _schedule(self, mb: int) -> bool:
         """Issue the next command for ``mb``. Returns False if it has nothing to do."""
         resets = self.pending_resets[mb]
-        # admission: waiting requests into free slots
+        # admission: waiting requests into free slots (held back while a re-plan drains)
         for s in self._free_slots(mb):
-            if not self.waiting:
+            if not self.waiting or self._replan is not None:
                 break
             r = self.waiting.pop(0)
             r.slot, r.state, r.prefilled = s, PREFILLING, 0
@@ -446,7 +513,7 @@ class PipelineServer:
 
     def _busy(self) -> bool:
         return bool(self.waiting or self.by_slot or any(o is not None for o in self.outstanding)
-                    or not self.incoming.empty())
+                    or not self.incoming.empty() or self._replan is not None)
 
     # ------------------------------------------------------------------ main loops
     def serve(self, stop_when_idle: bool = True, idle_sleep_s: float = 0.0005,
@@ -458,6 +525,8 @@ class PipelineServer:
             return
         self.t_start = self.t_start or time.perf_counter()
         while True:
+            if self._replan is not None and not self.by_slot and all(o is None for o in self.outstanding):
+                self._apply_replan()  # drained: every stage moves to the new split together
             self._intake()
             any_work = False
             for mb in range(self.M):
@@ -486,6 +555,10 @@ class PipelineServer:
         hdr = torch.zeros(self.hdr.size, dtype=torch.int32)
         while True:
             dist.recv(hdr, 0, group=self.ctrl)
+            if int(hdr[0]) == CMD_REPLAN:
+                b = hdr[4:4 + int(hdr[2])].tolist()
+                self._reshard(b[self.rank], b[self.rank + 1])
+                continue
             cmd, mb, items, resets = _Header.unpack(hdr)
             if cmd == CMD_STOP:
                 break

@@ -384,23 +384,6 @@ class StageEngine:
         return torch.empty((hip.PARTIAL_MAX_SPLIT, rows, self.cfg.hidden_size), dtype=torch.float32,
                            device=self.device)
 
-    def persistent_ok(self) -> bool:
-        """Can a batch-1 decode step of this stage run as the persistent kernel? (bf16 Llama-family
-        weights on a GPU, RoPE, whole-vocabulary head without padding bias, widths it stages.)"""
-        cfg = self.cfg
-        return (self.gpu and not self.fp8 and not cfg.is_gpt2 and self.cos is not None and self.n_layers > 0
-                and cfg.hidden_size % 256 == 0 and cfg.intermediate_size % 128 == 0
-                and max(cfg.hidden_size, cfg.intermediate_size) <= 32768 and cfg.head_dim in (64, 128)
-                and (not self.has_head or (self.head_bias is None and (self.head_v0, self.head_v1) == (0, cfg.head_rows))))
-
-    def persistent_table(self) -> torch.Tensor:
-        """int64 [n_layers, 6] device table (qkv, o, gate_up, down, k_cache, v_cache) pointers."""
-        if getattr(self, "_ptable", None) is None:
-            rows = [[lw.qkv.data_ptr(), lw.o.data_ptr(), lw.gate_up.data_ptr(), lw.down.data_ptr(),
-                     self.k_cache[i].data_ptr(), self.v_cache[i].data_ptr()] for i, lw in enumerate(self.layers)]
-            self._ptable = torch.tensor(rows, dtype=torch.int64, device=self.device)
-        return self._ptable
-
     # buffers a forward pass writes besides the KV cache: one set per concurrently running graph
     SCRATCH_ATTRS = ("buf_h", "buf_xn", "buf_q", "buf_attn", "buf_act", "part_o", "part_lse", "attn_cnt",
                      "coop_ws", "sk_ws", "part_k", "ss_buf", "w_scratch", "keys", "tokens", "ws_rows")
@@ -688,7 +671,7 @@ class StageEngine:
                 return 0
             bn, sp = pp
             hip.gemm_sk(x, wbf(w, s, N, K), rows, N, K, hip.EPI_PARTIAL, hip.make_epi(out=self.part_k, ldo=N),
-                        bn=bn, grid=hip.N_CU, dp=0, split=sp, ws=self.sk_ws)
+                        bn=bn, grid=hip.N_CU, dp=0, split=sp, ws=self.sk_ws, out_numel=self.part_k.numel())
             return sp
 
         # RMSNorm fused across the GEMMs: residual GEMMs write per-64-column sums of squares of
@@ -911,10 +894,7 @@ class DecodeGraph:
     """
 
     def __init__(self, eng: StageEngine, rows: int, mode: str, slots: Optional[list] = None,
-                 history_len: int = 0, split_head: bool = False, scratch: int = 0, persistent: bool = False):
-        """``persistent``: run the whole step (batch 1) as ONE persistent kernel launch
-        (decode_persistent.hip) when the stage qualifies (:meth:`StageEngine.persistent_ok`);
-        otherwise, or when False, the per-projection kernels. ``self.persistent`` says which."""
+                 history_len: int = 0, split_head: bool = False, scratch: int = 0):
         from ..ops import hip
         if not eng.gpu:
             raise RuntimeError("DecodeGraph needs a GPU stage")
@@ -946,10 +926,6 @@ class DecodeGraph:
         # final hidden; "first" completes the PREVIOUS step's keys over its slice from
         # (h_fin, keys_in), finalises the token ids (and history) and then embeds them
         self.split_head = split_head
-        self.persistent = bool(persistent) and rows == 1 and not split_head and eng.persistent_ok()
-        if self.persistent:
-            self.bar = torch.zeros(hip.N_CU, dtype=torch.int32, device=dev)
-            self.err = torch.zeros(1, dtype=torch.int32, device=dev)
         if split_head:
             if mode not in ("first", "last"):
                 raise ValueError("split_head needs mode 'first' or 'last'")
@@ -963,21 +939,6 @@ class DecodeGraph:
     def _step(self) -> None:
         hip, eng, rows = self._hip, self.eng, self.rows
         h = eng.buf_h[:rows]
-        if self.persistent:
-            if self.mode in ("mid", "last"):
-                h.copy_(self.h_in)
-            cfg = eng.cfg
-            head = self.mode in ("full", "last")
-            hip.decode_persistent(eng.persistent_table(), eng.n_layers, cfg.hidden_size, cfg.intermediate_size,
-                                  cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim, eng.max_seq,
-                                  cfg.rms_norm_eps, self.slot, self.pos, eng.cos, eng.sin, h, eng.buf_q[:1],
-                                  eng.buf_attn[:1], eng.buf_act[:1], self.bar, self.err,
-                                  embed=eng.embed_w if self.mode in ("full", "first") else None, tokens=self.tokens,
-                                  head=eng.lm_head if head else None,
-                                  head_n=(eng.head_v1 - eng.head_v0) if head else 0, keys=self.keys,
-                                  history=self.history if head else None,
-                                  step_ctr=self.step_ctr if (head and self.history is not None) else None)
-            return
         if self.split_head and self.mode == "first":
             self.keys.copy_(self.keys_in)
             eng.head_gemv(self.h_fin, rows, self.keys)

@@ -21,14 +21,24 @@ the master that calls ``ConfigSender``; the repository only ships a hand-written
    GPU i, config port base + i) and sends each the reference config extended with
    ``mode="pipeline"``, its rank, the world size, the whole stage list and the serving
    geometry; the controllers then run the micro-batched RCCL pipeline (PipelineServer) and
-   :meth:`submit` feeds requests to rank 0.
+   :meth:`submit` feeds requests to rank 0;
+6. live re-shard of that deployed pipeline (the reference's hot re-configuration,
+   ``/root/reference/utils/node_worker.py:445-474``, which there rebinds one ZMQ chain):
+   :meth:`replan` re-plans the split inside the same torchrun world - new device speeds
+   (e.g. fresh ``NodeProfiler`` measurements) or explicit ranges - and sends it to rank 0,
+   which drains the requests in flight and moves every stage to its new ``[start, end)``
+   (PipelineServer.request_replan); the ring edges stay, so no communicator is rebuilt.
 """
 from __future__ import annotations
 
+import json
+import time
+from dataclasses import replace
 from typing import List, Optional, Sequence
 
 from ..config import LlamaConfig
 from ..parallel.scheduler import DeviceSpec, Plan, build_chain_configs, plan_stages
+from ..parallel.transport import PushSocket
 from .config_sender import ConfigSender
 from .node_worker import ping_node, send_shutdown, send_user_request
 
@@ -101,7 +111,40 @@ class MasterNode:
             self.senders.append(s)
             cfgs.append(dict(c))
         self.mode = "pipeline"
+        self._kv_tokens_pipeline = max_seq * batch * M
         return cfgs
+
+    def replan(self, stages: Optional[Sequence] = None, speeds: Optional[Sequence[float]] = None,
+               timeout_s: float = 120.0, wait: bool = True) -> list:
+        """Move the deployed pipeline to a new layer split without restarting it. ``stages``:
+        explicit [[start, end], ...] per rank; else ``speeds`` (relative time multipliers per
+        device, e.g. :meth:`speed_from_profiles`) re-run the exact min-max planner. The split is
+        sent to rank 0; with ``wait`` this returns once every rank reports its new range."""
+        if self.mode != "pipeline" or self.plan is None:
+            raise RuntimeError("replan: no pipeline deployed (deploy_pipeline first)")
+        if stages is None:
+            if speeds is not None:
+                if len(speeds) != len(self.devices):
+                    raise ValueError("replan: one speed per device")
+                self.devices = [replace(d, speed=float(v)) for d, v in zip(self.devices, speeds)]
+            self.plan = plan_stages(self.cfg, self.devices, kv_tokens=self._kv_tokens_pipeline)
+            stages = [[st.start, st.end] for st in self.plan.stages]
+        stages = [[int(a), int(b)] for a, b in stages]
+        ing = self.devices[0]
+        s = PushSocket(f"tcp://{ing.host}:{ing.config_port}")
+        s.send_bytes(json.dumps({"command": "replan", "stages": stages}).encode())
+        s.close(linger_ms=5000)
+        if wait:
+            deadline = time.monotonic() + timeout_s
+            while True:
+                st = self.health(timeout_ms=2000)
+                if all(x is not None and list(x.get("shards", [])) == stages[i] for i, (_, x) in enumerate(st)):
+                    break
+                if time.monotonic() > deadline:
+                    raise TimeoutError(f"replan: ranks did not reach {stages}: {[x for _, x in st]}")
+                time.sleep(0.2)
+        self.plan_ranges = stages
+        return stages
 
     def health(self, timeout_ms: int = 2000) -> list:
         """[(DeviceSpec, status dict | None)] for every device of the current plan."""
@@ -116,7 +159,8 @@ class MasterNode:
         if not dead:
             return []
         if self.mode == "pipeline":
-            # an RCCL job cannot lose a rank and continue: the torchrun world is fixed
+            # an RCCL job cannot lose a rank and continue: the torchrun world is fixed (a slow
+            # but live rank is re-balanced with replan(speeds=...) instead)
             raise RuntimeError(f"[ERROR] pipeline ranks unreachable: {[(d.host, d.config_port) for d in dead]}; "
                                "restart the torchrun job and redeploy")
         alive = [d for d, st in status if st is not None]

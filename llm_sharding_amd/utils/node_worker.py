@@ -356,7 +356,8 @@ class NodeController:
         if self.server is not None:
             c = self.received_config or {}
             return {"listen_port": self.listen_port, "configured": True, "mode": "pipeline",
-                    "shards": [c.get("shards_start"), c.get("shards_end")], "rank": c.get("rank"),
+                    "shards": [self.server.start, self.server.end], "replans": self.server.replans,
+                    "rank": c.get("rank"),
                     "ingress": c.get("rank") == 0, "finished_requests": len(self.finished_outputs),
                     "uptime_s": time.monotonic() - self.t_boot}
         w = self.node_worker
@@ -409,7 +410,8 @@ class NodeController:
             raise RuntimeError(f"[ERROR] pipeline config for rank {cfg['rank']}/{cfg['world_size']} delivered to "
                                f"rank {r}/{n}")
         if self.server is not None:
-            raise RuntimeError("[ERROR] a pipeline is already deployed here: shut it down before re-planning")
+            raise RuntimeError("[ERROR] a pipeline is already deployed here: re-plan it through rank 0 "
+                               "(MasterNode.replan) or shut it down first")
         if self.node_worker is not None:
             self.node_worker.close()
             self.node_worker = None
@@ -441,8 +443,23 @@ class NodeController:
         stop = threading.Event()
 
         def other(msg):
-            if isinstance(msg, dict) and msg.get("command") == "ping":
+            if not isinstance(msg, dict):
+                return
+            if msg.get("command") == "ping":
                 self._pong(msg)
+            elif msg.get("command") == "replan" or (msg.get("mode") == "pipeline" and "stages" in msg):
+                # live re-shard of the deployed pipeline (reference hot re-config, node_worker.py
+                # :445-474): rank 0 owns the command stream, so the new split is applied there,
+                # in order, once the requests in flight have finished
+                if not self.server.first:
+                    _log("[WARNING] replan ignored: send it to rank 0 (the ingress)")
+                    return
+                try:
+                    self.server.request_replan(msg["stages"])
+                    if self.verbose:
+                        _log(f"[CONFIG] re-plan requested: {msg['stages']}")
+                except ValueError as e:
+                    _log(f"[ERROR] {e}")
 
         if self.server.first:
             replies = Replies(self.tokenizer, verbose=self.verbose,

@@ -55,26 +55,19 @@ def main():
     for B in [int(x) for x in a.decode_batches.split(",")]:
         for s in range(B):
             eng.seq_len[s] = 128
-        for persistent in ((False, True) if B == 1 else (False,)):
-            for s in range(B):
-                eng.seq_len[s] = 128
-            dg = DecodeGraph(eng, B, "full", slots=list(range(B)), persistent=persistent).capture()
-            for _ in range(4):
-                dg.replay()
-            torch.cuda.synchronize()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            for _ in range(a.decode_steps):
-                dg.replay()
-            e1.record()
-            torch.cuda.synchronize()
-            ms = e0.elapsed_time(e1) / a.decode_steps
-            key = f"{B}p" if dg.persistent else B
-            res["tpot_ms"][key] = round(ms, 3)
-            print(f"[sweep] decode batch {B:3d}{' persistent' if dg.persistent else ''}: {ms:.3f} ms/token/step "
-                  f"({B / ms * 1e3:.0f} tok/s)", flush=True)
-            if dg.persistent and int(dg.err.item()):
-                raise RuntimeError("persistent decode: grid barrier timed out")
+        dg = DecodeGraph(eng, B, "full", slots=list(range(B))).capture()
+        for _ in range(4):
+            dg.replay()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(a.decode_steps):
+            dg.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / a.decode_steps
+        res["tpot_ms"][B] = round(ms, 3)
+        print(f"[sweep] decode batch {B:3d}: {ms:.3f} ms/token/step ({B / ms * 1e3:.0f} tok/s)", flush=True)
     wbytes = sum(p.numel() * p.element_size() for lw in eng.layers for p in (lw.qkv, lw.o, lw.gate_up, lw.down))
     wbytes += eng.lm_head.numel() * 2
     res["weight_GB"] = round(wbytes / 1e9, 2)

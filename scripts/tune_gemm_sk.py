@@ -118,7 +118,7 @@ def main():
 
                             def part(i):
                                 hip.gemm_sk(x, ws[i % nbuf], M, N, K, hip.EPI_PARTIAL, epp, bn=bn, grid=hip.N_CU, dp=0,
-                                            split=sp, ws=sk_ws)
+                                            split=sp, ws=sk_ws, out_numel=pbuf.numel())
                                 hip.resid_rmsnorm_partials(out, pbuf, sp, M, 1e-5, out=xn)
                             pres.append((round(timeit(part, a.iters), 2), bn, sp))
                     pres.sort()

@@ -115,7 +115,16 @@ def _timeout_worker(rank, port, ports, q):
                 c.receive_data(timeout_ms=30000)
                 q.put((rank, "no error"))
             except RuntimeError as e:
-                q.put((rank, "timeout" if "timed out" in str(e) or "failed" in str(e) else repr(e)))
+                verdict = "timeout" if "timed out" in str(e) or "failed" in str(e) else repr(e)
+                # the timed-out irecv stays posted: the communicator refuses further traffic
+                for op in (lambda: c.receive_data(no_block=True), lambda: c.transfer_data({"a": 1})):
+                    try:
+                        op()
+                        verdict = "usable after failure"
+                    except RuntimeError as e2:
+                        if "unusable" not in str(e2):
+                            verdict = repr(e2)
+                q.put((rank, verdict))
         dist.barrier()
         c.close()
     finally:

@@ -185,8 +185,11 @@ def test_gemm_sk_partials_resid_rmsnorm(M, N, K, bn, S, ws):
     r = _rnd(M, N)
     ref = a.float() @ w.float().T
     P = torch.full((h.PARTIAL_MAX_SPLIT, M, N), float("nan"), device=DEV)
+    with pytest.raises(ValueError, match="partial"):  # capacity is checked before anything is written
+        h.gemm_sk(a, packing.pack_b(w), M, N, K, h.EPI_PARTIAL, h.make_epi(out=P, ldo=N), bn=bn, grid=256, dp=0,
+                  split=S, ws=ws, out_numel=(S - 1) * M * N)
     h.gemm_sk(a, packing.pack_b(w), M, N, K, h.EPI_PARTIAL, h.make_epi(out=P, ldo=N), bn=bn, grid=256, dp=0, split=S,
-              ws=ws)
+              ws=ws, out_numel=P.numel())
     assert rel_err(P[:S].sum(0), ref) < 1e-5
     assert bool(torch.isnan(P[S:]).all())  # nothing beyond the S partials is written
     hb, xn = r.clone(), torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)

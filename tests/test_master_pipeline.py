@@ -102,3 +102,96 @@ def test_master_deploys_rccl_pipeline_token_exact(tiny_shards, world):
             want = want[:next(i for i, t in enumerate(want) if t in eos) + 1]
         assert got[rid] == want, (rid, got[rid], want)
     assert sorted(map(tuple, res[0])) == sorted(tuple(got[r]) for r in range(len(prompts)))
+
+
+@pytest.fixture(scope="module")
+def tiny8_shards(tmp_path_factory):
+    from llm_sharding_amd.config import tiny
+    from llm_sharding_amd.models.weights import write_random_shards
+    d = tmp_path_factory.mktemp("shards8")
+    return write_random_shards(tiny(layers=8), str(d / "tiny8-llama"), dtype=torch.float32, seed=11)
+
+
+def _golden(shards, prompts, n_new):
+    cfg, emb, layers, fn, lm = W.load_full_model(shards)
+    ref = ReferenceLlama(cfg, emb, layers, fn, lm)
+    eos = set(cfg.eos_ids)
+    out = []
+    for pr in prompts:
+        want = ref.generate(torch.tensor([pr]), n_new)[0].tolist()
+        if any(t in eos for t in want):
+            want = want[:next(i for i, t in enumerate(want) if t in eos) + 1]
+        out.append(want)
+    return out
+
+
+def test_master_replans_live_pipeline_token_exact(tiny8_shards):
+    """Live re-shard of the DEPLOYED pipeline (reference hot re-config, node_worker.py:445-474):
+    deploy 4 ranks, serve, re-plan inside the same world (explicit ranges moving two
+    boundaries while a request is in flight, then a speed-driven re-plan through the planner),
+    serve again - every output equals the fp32 golden model's greedy tokens."""
+    from llm_sharding_amd.parallel import protocol
+    from llm_sharding_amd.parallel.scheduler import DeviceSpec
+    from llm_sharding_amd.parallel.transport import PullSocket
+    from llm_sharding_amd.utils.master_node import MasterNode
+    world = 4
+    port = _ports(1)[0]
+    cfg_ports, data_ports = _ports(world), _ports(world)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_node, args=(r, world, port, cfg_ports[r], tiny8_shards, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    reply = PullSocket("tcp://127.0.0.1:0")
+    to = f"tcp://127.0.0.1:{reply.port}"
+    rounds = [[[1, 33, 44, 55, 66], [7, 8, 9]], [[100, 5, 17, 200, 3, 41, 12], [2, 2, 2, 2]], [[9, 19, 29], [4, 40, 4]]]
+    n_new = 6
+    got, rid = [], 0
+
+    def serve(prompts):
+        nonlocal rid
+        for pr in prompts:
+            master.submit(input_ids=[pr], max_new_tokens=n_new, reply_to=to)
+        out = {}
+        for _ in prompts:
+            m = protocol.decode(reply.recv_bytes(timeout_ms=120000))
+            out[m["request_id"]] = m["output_ids"]
+        got.append([out[rid + i] for i in range(len(prompts))])
+        rid += len(prompts)
+
+    try:
+        devs = [DeviceSpec(host="127.0.0.1", config_port=cfg_ports[i], data_port=data_ports[i]) for i in range(world)]
+        master = MasterNode.from_shards(tiny8_shards, devs)
+        cfgs = master.deploy_pipeline(batch=2, microbatches=world, max_seq=64, prefill_budget=64)
+        before = [[c["shards_start"], c["shards_end"]] for c in cfgs]
+        assert before == [[0, 2], [2, 4], [4, 6], [6, 8]], before
+        serve(rounds[0])
+        # a request in flight while the re-plan arrives: it finishes on the old split
+        master.submit(input_ids=[[5, 6, 7, 8]], max_new_tokens=n_new, reply_to=to)
+        new = master.replan(stages=[[0, 3], [3, 4], [4, 7], [7, 8]])
+        m = protocol.decode(reply.recv_bytes(timeout_ms=120000))
+        inflight = m["output_ids"]
+        rid += 1
+        st = master.health()
+        assert [s["shards"] for _, s in st] == new and all(s["replans"] == 1 for _, s in st), st
+        serve(rounds[1])
+        # planner-driven: rank 1 is 3x slower -> it gets the fewest layers
+        new2 = master.replan(speeds=[1.0, 3.0, 1.0, 1.0])
+        assert new2 != new and new2[1][1] - new2[1][0] == min(b - a for a, b in new2), new2
+        serve(rounds[2])
+        master.shutdown()
+        res = {}
+        for _ in range(world):
+            r, v = q.get(timeout=120)
+            res[r] = v
+    finally:
+        reply.close()
+        for p in ps:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    assert all(res[r] == "ok" for r in range(1, world)), res
+    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+    for prompts, outs in zip(rounds, got):
+        assert outs == _golden(tiny8_shards, prompts, n_new), (prompts, outs)
+    assert inflight == _golden(tiny8_shards, [[5, 6, 7, 8]], n_new)[0]
