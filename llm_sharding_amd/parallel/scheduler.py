@@ -77,11 +77,14 @@ def default_costs(cfg: LlamaConfig, elem_bytes: int = 2) -> tuple:
 def plan_stages(cfg: LlamaConfig, devices: Sequence[DeviceSpec] | int, *,
                 layer_costs: Optional[Sequence[float]] = None, embed_cost: Optional[float] = None,
                 head_cost: Optional[float] = None, kv_tokens: int = 0, elem_bytes: int = 2,
-                min_layers: int = 1, head_split: bool = False, scratch: float = 0.0) -> Plan:
+                min_layers: int = 1, head_split: bool = False, scratch: float = 0.0,
+                stage_overhead: float = 0.0) -> Plan:
     """Exact min-max contiguous partition. ``devices`` is a list (chain order) or a count.
     ``head_split``: the lm_head is shared by the last and the first stage (pipeline.py), so each
     carries half of its cost and memory. ``scratch``: per-stage engine scratch bytes
-    (:func:`scratch_bytes`), counted against every device's memory next to weights and KV."""
+    (:func:`scratch_bytes`), counted against every device's memory next to weights and KV.
+    ``stage_overhead``: fixed cost of one stage step (measured costs:
+    node_profiler.costs_for_planner), added to every stage before its device's speed factor."""
     if isinstance(devices, int):
         devices = [DeviceSpec() for _ in range(devices)]
     n, L = len(devices), cfg.num_hidden_layers
@@ -104,7 +107,7 @@ def plan_stages(cfg: LlamaConfig, devices: Sequence[DeviceSpec] | int, *,
     hfrac_last = 0.5 if split else 1.0
 
     def stage_cost(k: int, a: int, b: int) -> float:
-        t = pre[b] - pre[a]
+        t = pre[b] - pre[a] + stage_overhead
         if k == 0:
             t += ec + (hc * 0.5 if split else 0.0)
         if k == n - 1:

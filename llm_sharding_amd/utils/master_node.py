@@ -85,16 +85,36 @@ class MasterNode:
             self.senders.append(s)
         return cfgs
 
+    def plan_from_profiles(self, profiles: Sequence[dict], kv_tokens: int = 0) -> Plan:
+        """Plan with MEASURED costs of the deployed engine: ``profiles[i]`` is device i's
+        :func:`~.node_profiler.profile_stage_costs` result. Device 0's per-layer / embedding /
+        head / per-stage costs are the cost model, every device's speed factor its per-layer
+        decode time relative to device 0 (est_time of each stage = predicted ms per step)."""
+        from .node_profiler import costs_for_planner
+        if len(profiles) != len(self.devices):
+            raise ValueError("plan_from_profiles: one profile per device")
+        base = profiles[0]["layer_decode_ms"]
+        self.devices = [replace(d, speed=(p["layer_decode_ms"] / base if base > 0 else 1.0))
+                        for d, p in zip(self.devices, profiles)]
+        self._plan_costs = costs_for_planner(self.cfg, profiles[0])
+        self.plan = plan_stages(self.cfg, self.devices, kv_tokens=kv_tokens, **self._plan_costs)
+        return self.plan
+
     def deploy_pipeline(self, batch: int = 8, microbatches: int = 0, max_seq: int = 2048,
                         prefill_budget: int = 2048, streams: int = 1, use_graph: bool = True,
-                        timeout_ms: int = 10000) -> list:
+                        timeout_ms: int = 10000, profiles: Optional[Sequence[dict]] = None) -> list:
         """Plan contiguous layer ranges over the devices (device i = torchrun rank i, KV cache of
         ``microbatches`` x ``batch`` sequences of ``max_seq`` tokens counted against each GPU's
-        HBM) and configure every controller for the micro-batched RCCL pipeline. Returns the
-        configs sent (rank order)."""
+        HBM) and configure every controller for the micro-batched RCCL pipeline. ``profiles``:
+        per-device stage-cost profiles of the deployed engine (NodeProfiler
+        .profile_pipeline_costs) - the plan then balances measured step times
+        (:meth:`plan_from_profiles`). Returns the configs sent (rank order)."""
         n = len(self.devices)
         M = microbatches or max(2, n)
-        self.plan = plan_stages(self.cfg, self.devices, kv_tokens=max_seq * batch * M)
+        if profiles is not None:
+            self.plan_from_profiles(profiles, kv_tokens=max_seq * batch * M)
+        else:
+            self.plan = plan_stages(self.cfg, self.devices, kv_tokens=max_seq * batch * M)
         stages = [[st.start, st.end] for st in self.plan.stages]
         ing = self.plan.stages[0].device
         cfgs, self.senders = [], []
@@ -127,7 +147,8 @@ class MasterNode:
                 if len(speeds) != len(self.devices):
                     raise ValueError("replan: one speed per device")
                 self.devices = [replace(d, speed=float(v)) for d, v in zip(self.devices, speeds)]
-            self.plan = plan_stages(self.cfg, self.devices, kv_tokens=self._kv_tokens_pipeline)
+            self.plan = plan_stages(self.cfg, self.devices, kv_tokens=self._kv_tokens_pipeline,
+                                    **getattr(self, "_plan_costs", {}))
             stages = [[st.start, st.end] for st in self.plan.stages]
         stages = [[int(a), int(b)] for a, b in stages]
         ing = self.devices[0]

@@ -19,6 +19,15 @@ Same class, constants and public methods:
 Every timing is host wall time bracketed by ``torch.cuda.synchronize`` (reference
 ``:300-308``). Results are also *returned* as dicts (the reference only prints), so the master
 scheduler (``plan_stages`` layer costs / device speed factors) can consume them directly.
+
+The scheduler's inputs should come from the path that is DEPLOYED, not from the reference-API
+worker: :func:`profile_stage_costs` (``NodeProfiler.profile_pipeline_costs``) times the
+pipeline's own hipGraph decode replays (hipEvents; ``DecodeGraph`` modes mid / first / full on
+1 and n layers -> per-layer, embedding, head and per-stage fixed costs at a given batch and
+context) plus the engine's prefill forward, and :func:`costs_for_planner` /
+``MasterNode.deploy_pipeline(profiles=...)`` turn that into the planner's cost model
+(reference: ``c_k`` feeds the master scheduler, ``/root/reference/README.md:7-8``,
+``/root/reference/utils/node_profiler.py:822-979``).
 Fixes: Q11 (``_resolve_assisted_target_loaded_layer_num(None)`` no longer computes ``None - 1``).
 """
 from __future__ import annotations
@@ -32,6 +41,129 @@ import torch
 from ..config import LlamaConfig
 from ..models.tokenizer import load_tokenizer
 from .node_worker import NodeWorker
+
+
+def _timed_replays(step, n: int, gpu: bool) -> float:
+    """Median-free mean ms per call of ``step`` over ``n`` back-to-back calls (device events on
+    a GPU, so the host launch cost of a graph replay is not counted)."""
+    if gpu:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(n):
+            step()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / n
+    ts = []
+    for _ in range(n):
+        t0 = time.perf_counter()
+        step()
+        ts.append((time.perf_counter() - t0) * 1e3)
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
+def profile_stage_costs(cfg: LlamaConfig, source, device, batch: int = 1, context: int = 128,
+                        n_layers: int = 4, prefill_len: int = 128, replays: int = 20,
+                        dtype=torch.bfloat16) -> dict:
+    """Cost model of the DEPLOYED stage engine (runtime/engine.py StageEngine + DecodeGraph):
+    one engine with ``n_layers`` layers (+ embedding + lm_head) and ``batch`` sequences whose
+    KV caches hold ``context`` tokens; decode steps are timed as the pipeline runs them
+    (hipGraph replays, hipEvents; the eager step on CPU) in the modes a stage can have:
+
+        mid(j)  = overhead + j * layer          (hidden in -> j layers -> hidden out)
+        first(n) = mid(n) + embed               (token ids -> embedding -> layers)
+        full(n)  = first(n) + head              (... -> final norm + lm_head + argmax)
+
+    from j = 1 and j = n; prefill per layer from the engine's forward over ``prefill_len``
+    tokens at 1 and n layers. Returns ms: ``layer_decode_ms``, ``embed_decode_ms``,
+    ``head_decode_ms``, ``stage_overhead_ms``, ``layer_prefill_ms``, ``prefill_overhead_ms``
+    plus the geometry."""
+    from ..runtime.engine import DecodeGraph, EagerDecode, StageEngine
+    dev = torch.device(device)
+    gpu = dev.type == "cuda"
+    n = max(2, min(int(n_layers), cfg.num_hidden_layers))
+    max_seq = -(-(context + 4 * (replays + 4) + prefill_len + 8) // 64) * 64
+    eng = StageEngine(cfg, 0, n, dev, dtype if gpu else torch.float32, has_embed=True, has_head=True,
+                      source=source, max_slots=batch, max_seq=max_seq,
+                      max_prefill_rows=max(prefill_len, batch))
+    layers = eng.layers
+    slots = list(range(batch))
+    gen = torch.Generator().manual_seed(0)
+
+    def decode_ms(mode: str, j: int) -> float:
+        eng.layers = layers[:j]
+        try:
+            for s_ in slots:
+                eng.seq_len[s_] = context
+            if gpu:
+                g = DecodeGraph(eng, batch, mode, slots=slots)
+                g.tokens.copy_(torch.randint(3, cfg.vocab_size, (batch,), generator=gen).to(torch.int32))
+                g.capture()
+            else:
+                g = EagerDecode(eng, batch, mode, slots=slots)
+            for _ in range(3):
+                g.replay()
+            if gpu:
+                torch.cuda.synchronize()
+            return _timed_replays(g.replay, replays, gpu)
+        finally:
+            eng.layers = layers
+
+    def prefill_ms(j: int) -> float:
+        eng.layers = layers[:j]
+        try:
+            ids = torch.randint(3, cfg.vocab_size, (prefill_len,), generator=gen)
+
+            def run():
+                eng.reset([0])
+                sl, po = eng.prefill_rows([0], [prefill_len])
+                eng.forward(eng.embed(ids.to(dev)), sl, po)
+            run()
+            if gpu:
+                torch.cuda.synchronize()
+            return _timed_replays(run, max(3, replays // 4), gpu)
+        finally:
+            eng.layers = layers
+
+    mid1, midn = decode_ms("mid", 1), decode_ms("mid", n)
+    first_n, full_n = decode_ms("first", n), decode_ms("full", n)
+    p1, pn = prefill_ms(1), prefill_ms(n)
+    layer = max(0.0, (midn - mid1) / (n - 1))
+    lp = max(0.0, (pn - p1) / (n - 1))
+    out = {
+        "batch": batch, "context": context, "profiled_layers": n, "prefill_len": prefill_len,
+        "device": str(dev), "graph": gpu,
+        "layer_decode_ms": layer,
+        "stage_overhead_ms": max(0.0, mid1 - layer),
+        "embed_decode_ms": max(0.0, first_n - midn),
+        "head_decode_ms": max(0.0, full_n - first_n),
+        "layer_prefill_ms": lp,
+        "prefill_overhead_ms": max(0.0, p1 - lp),
+        "decode_c_k": layer * cfg.num_hidden_layers / batch * 1e-3,  # s per token per whole model
+    }
+    del eng
+    if gpu:
+        torch.cuda.empty_cache()
+    return out
+
+
+def predict_stage_ms(prof: dict, n_layers: int, first: bool = False, last: bool = False,
+                     head_frac: float = 1.0) -> float:
+    """Decode step time of a stage of ``n_layers`` layers from :func:`profile_stage_costs`."""
+    t = prof["stage_overhead_ms"] + n_layers * prof["layer_decode_ms"]
+    if first:
+        t += prof["embed_decode_ms"]
+    if last:
+        t += head_frac * prof["head_decode_ms"]
+    return t
+
+
+def costs_for_planner(cfg: LlamaConfig, prof: dict) -> dict:
+    """``plan_stages`` keyword arguments from a stage-cost profile (ms per decode step)."""
+    return {"layer_costs": [prof["layer_decode_ms"]] * cfg.num_hidden_layers,
+            "embed_cost": prof["embed_decode_ms"], "head_cost": prof["head_decode_ms"],
+            "stage_overhead": prof["stage_overhead_ms"]}
 
 
 class NodeProfiler:
@@ -76,6 +208,20 @@ class NodeProfiler:
     def _sleep(self) -> None:
         if self.PROFILE_INTERVAL_SLEEP_TIME:
             time.sleep(self.PROFILE_INTERVAL_SLEEP_TIME)
+
+    def profile_pipeline_costs(self, batch: int = 1, context: int = 128, n_layers: int = 4,
+                               prefill_len: int = 128, replays: int = 20) -> dict:
+        """Graph-replay cost model of the deployed pipeline engine on this device, from this
+        node's shard folder (:func:`profile_stage_costs`); what ``MasterNode.deploy_pipeline
+        (profiles=...)`` plans with."""
+        from ..runtime.engine import ShardFolderSource
+        res = profile_stage_costs(self.config, ShardFolderSource(self.shards_path, self.config), self.device,
+                                  batch=batch, context=context, n_layers=n_layers, prefill_len=prefill_len,
+                                  replays=replays, dtype=self.dtype)
+        self._log(f"[INFO] stage costs (batch {batch}, context {context}): layer {res['layer_decode_ms']:.4f} ms, "
+                  f"embed {res['embed_decode_ms']:.4f} ms, head {res['head_decode_ms']:.4f} ms, "
+                  f"stage overhead {res['stage_overhead_ms']:.4f} ms; prefill layer {res['layer_prefill_ms']:.4f} ms")
+        return res
 
     # ---------------------------------------------------------------------- C8a
     def profile_max_layer_num(self, memory_limit_bytes: Optional[float] = None,

@@ -107,3 +107,55 @@ def test_go_through_every_shards_ring(tiny_shards):
     cfg, emb, layers, fn, lm = W.load_full_model(tiny_shards)
     want = ReferenceLlama(cfg, emb, layers, fn, lm).generate(ids, 6)[0].tolist()
     assert out[4:] == want
+
+
+def _measure_stage(cfg, src, a, b, first, last, batch, context, device="cpu", dtype=torch.float32, reps=15):
+    """Decode step time of ONE deployed stage engine (layers [a, b)), as the pipeline runs it."""
+    from llm_sharding_amd.runtime.engine import DecodeGraph, EagerDecode, StageEngine
+    from llm_sharding_amd.utils.node_profiler import _timed_replays
+    gpu = str(device).startswith("cuda")
+    eng = StageEngine(cfg, a, b, device, dtype, has_embed=first, has_head=last, source=src, max_slots=batch,
+                      max_seq=context + 8 * reps + 64, max_prefill_rows=max(64, batch))
+    for s in range(batch):
+        eng.seq_len[s] = context
+    mode = "full" if first and last else ("first" if first else ("last" if last else "mid"))
+    g = (DecodeGraph if gpu else EagerDecode)(eng, batch, mode, slots=list(range(batch)))
+    g.capture() if gpu else None
+    for _ in range(3):
+        g.replay()
+    if gpu:
+        torch.cuda.synchronize()
+    ms = _timed_replays(g.replay, reps, gpu)
+    del eng, g
+    return ms
+
+
+def test_stage_cost_profile_predicts_deployed_stages():
+    """The planner's stage times, priced with the DEPLOYED engine's measured costs
+    (profile_stage_costs -> MasterNode.plan_from_profiles), are within 15 % of what each planned
+    stage's own decode step measures (reference c_k -> scheduler,
+    /root/reference/utils/node_profiler.py:822-979)."""
+    from llm_sharding_amd.config import tiny
+    from llm_sharding_amd.parallel.scheduler import DeviceSpec
+    from llm_sharding_amd.runtime.engine import RandomSource
+    from llm_sharding_amd.utils.master_node import MasterNode
+    from llm_sharding_amd.utils.node_profiler import predict_stage_ms, profile_stage_costs
+    nt = torch.get_num_threads()
+    torch.set_num_threads(1)  # one thread: CPU step times stable to a few % (thread-pool jitter otherwise)
+    cfg = tiny(layers=8, hidden=512)
+    src = RandomSource(cfg, 1)
+    profile_stage_costs(cfg, src, "cpu", batch=8, context=64, n_layers=4, prefill_len=32, replays=5)  # warm-up
+    prof = profile_stage_costs(cfg, src, "cpu", batch=8, context=64, n_layers=4, prefill_len=32, replays=15)
+    assert prof["layer_decode_ms"] > 0 and prof["head_decode_ms"] >= 0 and prof["layer_prefill_ms"] > 0
+    m = MasterNode(cfg, [DeviceSpec(), DeviceSpec()])
+    plan = m.plan_from_profiles([prof, dict(prof)], kv_tokens=0)
+    for st in plan.stages:
+        want = predict_stage_ms(prof, st.n_layers, st.has_embed, st.has_head)
+        assert abs(st.est_time - want) < 1e-9
+        got = _measure_stage(cfg, src, st.start, st.end, st.has_embed, st.has_head, 8, 64)
+        assert abs(st.est_time - got) / got < 0.15, (st.start, st.end, st.est_time, got, prof)
+    # a device measured 2x slower per layer gets fewer layers
+    slow = dict(prof, layer_decode_ms=2 * prof["layer_decode_ms"])
+    plan2 = m.plan_from_profiles([prof, slow])
+    assert plan2.stages[1].n_layers < plan2.stages[0].n_layers
+    torch.set_num_threads(nt)
