@@ -5,7 +5,7 @@ by `python scripts/gemm_stamps.py --build` on the CPU host), for one configurati
 
 Per work item the stamps are: 0 segment start, 1 prologue DMA landed, 2 main loop done,
 3 partial slab stored + ticket drawn, 4 fixup done, 5 epilogue done.
-usage: gemm_stamps.py M N K bn grid dp split [reps] | --build"""
+usage: gemm_stamps.py M N K bn grid dp split [reps] [bm] | --build"""
 import ctypes
 import os
 import subprocess
@@ -31,6 +31,7 @@ def main():
     from llm_sharding_amd.ops import hip, packing
     M, N, K, bn, grid, dp, split = (int(v) for v in sys.argv[1:8])
     reps = int(sys.argv[8]) if len(sys.argv) > 8 else 5
+    bm = int(sys.argv[9]) if len(sys.argv) > 9 else 256
     L = ctypes.CDLL(SO)
     vp, i = ctypes.c_void_p, ctypes.c_int
     L.lsa_gemm_sk.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(hip.EpiArgs), i, i, i, i, i, i, i, vp, vp,
@@ -46,7 +47,7 @@ def main():
     for r in range(reps):
         st.zero_()
         rc = L.lsa_gemm_sk(ctypes.c_void_p(x.data_ptr()), x.stride(0), ctypes.c_void_p(wps[r % nbuf].data_ptr()), M, N, K,
-                           hip.EPI_STORE, ctypes.byref(ep), 256, bn, 0, grid, dp, split, 8,
+                           hip.EPI_STORE, ctypes.byref(ep), bm, bn, 0, grid, dp, split, 8,
                            ctypes.c_void_p(ws.slab.data_ptr()), ctypes.c_void_p(ws.counters.data_ptr()),
                            ws.slab.numel(), ws.counters.numel(), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
         assert rc == 0, rc
@@ -58,7 +59,8 @@ def main():
     us = (s - t0) / 100.0  # 100 MHz -> us
     us[s == 0] = float("nan")
     names = ["seg_start", "prologue", "loop_end", "ticket", "fixup", "epilogue"]
-    print(f"config M={M} N={N} K={K} bn={bn} grid={grid} dp={dp} split={split}: {int(act.sum())} active workgroups")
+    print(f"config M={M} N={N} K={K} bm={bm} bn={bn} grid={grid} dp={dp} split={split}: {int(act.sum())} active "
+          f"workgroups, kernel span {float(torch.nan_to_num(us, nan=0.0).max()):.2f} us")
     for item in range(5):
         cols = us[:, item * 6:(item + 1) * 6]
         if not torch.isfinite(cols[:, 0]).any():
