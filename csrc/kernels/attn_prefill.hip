@@ -60,15 +60,11 @@ LSA_DEVICE void glds16(const void* src, unsigned char* lds_base) {
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
 }
 
-// DEC: decode mode (GQA decode attention on MFMA, lsa_attn_decode_mfma): work item tix is decode
-// row tix - one query position per sequence, its tile derived on the device from slot / pos /
-// kv_len (graph-replay safe), and the G query heads of a KV head share every staged K/V block.
-template <int HD, int HPW, bool DEC = false>
+template <int HD, int HPW>
 __global__ __launch_bounds__(NTHR) void flash_prefill_kernel(
     const bf16_raw* __restrict__ q, int ldq, const bf16_raw* __restrict__ kc, const bf16_raw* __restrict__ vc,
     const PrefillTile* __restrict__ tiles, int n_heads, int n_kv, int t_max, float scale_log2, int causal,
-    bf16_raw* __restrict__ out, int ldo, const int* __restrict__ dslot = nullptr,
-    const int* __restrict__ dpos = nullptr, const int* __restrict__ dkvlen = nullptr) {
+    bf16_raw* __restrict__ out, int ldo) {
   constexpr int KF = HD / 32;                 // 32-dim fragments of a query/key row
   constexpr int DT = HD / 16;                 // 16-dim output tiles
   constexpr int NC = HD / 8;                  // 16-B chunks per row
@@ -91,17 +87,7 @@ __global__ __launch_bounds__(NTHR) void flash_prefill_kernel(
     tix = blockIdx.x % n_tiles;
     grp = blockIdx.x / n_tiles;
   }
-  PrefillTile tile;
-  if constexpr (DEC) {
-    tile.row0 = tix;
-    tile.nrows = 1;
-    tile.slot = dslot[tix];
-    tile.pos0 = dpos[tix];
-    const int kl = dkvlen ? dkvlen[tix] : dpos[tix] + 1;
-    tile.kvlen = kl < t_max ? kl : t_max;  // never read past the static cache
-  } else {
-    tile = tiles[tix];
-  }
+  const PrefillTile tile = tiles[tix];
   const int G = n_heads / n_kv;
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, l16 = lane & 15;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -298,22 +284,206 @@ int dispatch_hpw(int hpw, const bf16_raw* q, int ldq, const bf16_raw* k, const b
   return LSA_OK;
 }
 
-template <int HD>
-int launch_decode_mfma(int hpw, const bf16_raw* q, int ldq, const bf16_raw* k, const bf16_raw* v, const int* slot,
-                       const int* pos, const int* kvlen, int rows, int n_heads, int n_kv, int t_max, float sl2,
-                       bf16_raw* o, int ldo, hipStream_t stream) {
-  dim3 grid(rows * (n_heads / hpw)), block(NTHR);
-  switch (hpw) {
-    case 4:
-      flash_prefill_kernel<HD, 4, true><<<grid, block, 0, stream>>>(q, ldq, k, v, nullptr, n_heads, n_kv, t_max, sl2, 0,
-                                                                   o, ldo, slot, pos, kvlen);
-      break;
-    case 8:
-      flash_prefill_kernel<HD, 8, true><<<grid, block, 0, stream>>>(q, ldq, k, v, nullptr, n_heads, n_kv, t_max, sl2, 0,
-                                                                   o, ldo, slot, pos, kvlen);
-      break;
-    default: return LSA_UNSUPPORTED;
+// ---- GQA decode attention on MFMA ---------------------------------------------------------
+// One workgroup per (decode row, KV head): the G = n_heads / n_kv query heads of the group are
+// the 16 MFMA columns (G <= 16), so ONE K/V stream serves the whole group and no MFMA row is
+// spent on padding query positions. The NW waves split the row's keys into 32-key sub-blocks
+// (wave w takes sub-blocks w, w + NW, ...), each wave staging its own K/V sub-blocks by LDS-DMA
+// into a private double buffer (no barrier in the loop: the issuing wave's counted vmcnt orders
+// its own reads), computing S^T[key][head] = K . Q^T and O^T += V^T . P^T exactly like the
+// prefill kernel (same swizzled images, same permuted key order for P^T), and the NW partial
+// (max, sum, O) states are merged through LDS at the end. Keys [0, kv_len or pos + 1) of the
+// row's cache slot, tile derived on the device (graph-replay safe).
+template <int HD, int NW>
+__global__ __launch_bounds__(NW * 64) void gqa_decode_kernel(
+    const bf16_raw* __restrict__ q, int ldq, const bf16_raw* __restrict__ kc, const bf16_raw* __restrict__ vc,
+    const int* __restrict__ dslot, const int* __restrict__ dpos, const int* __restrict__ dkvlen, int n_heads,
+    int n_kv, int t_max, float scale_log2, bf16_raw* __restrict__ out, int ldo) {
+  constexpr int SB = 32;                       // keys per sub-block (one 32-deep PV fragment)
+  constexpr int KF = HD / 32, DT = HD / 16, NC = HD / 8;
+  constexpr int BLK = SB * HD * 2;             // bytes of one K (or V) sub-block
+  constexpr int PPW = BLK / 1024;              // 1 KiB DMA pieces per operand and sub-block
+  constexpr int RPP = 1024 / (HD * 2);         // rows per piece
+  constexpr int WREG = 2 * 2 * BLK;            // one wave's staging: [buffer][K | V]
+  constexpr int MERGE = NW * (16 * HD + 32) * 4;
+  constexpr int SMEM = NW * WREG > MERGE ? NW * WREG : MERGE;
+  static_assert(PPW >= 1, "geometry");
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
+
+  const int row = blockIdx.x / n_kv, kvh = blockIdx.x % n_kv;
+  const int G = n_heads / n_kv;
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, l16 = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int slot = dslot[row];
+  int kl = dkvlen ? dkvlen[row] : dpos[row] + 1;
+  kl = kl < t_max ? kl : t_max;  // never read past the static cache
+  const bool col_ok = l16 < G;   // MFMA column l16 = query head kvh * G + l16
+
+  // Q^T fragments (B operand): lane holds Q[head l16][kf*32 + 8g .. +7]
+  u32x4_t qf[KF];
+  {
+    const bf16_raw* qrow = q + (size_t)row * ldq + (size_t)(kvh * G + (col_ok ? l16 : 0)) * HD;
+#pragma unroll
+    for (int kf = 0; kf < KF; ++kf) qf[kf] = col_ok ? ld16(qrow + kf * 32 + g * 8) : u32x4_t{0u, 0u, 0u, 0u};
   }
+  const size_t cache_base = ((size_t)slot * n_kv + kvh) * (size_t)t_max * HD;
+  const bf16_raw* kb_ptr = kc + cache_base;
+  const bf16_raw* vb_ptr = vc + cache_base;
+  unsigned char* my = smem + w * WREG;
+
+  auto stage = [&](int sb, int buf) {
+    unsigned char* kd = my + buf * (2 * BLK);
+#pragma unroll
+    for (int s = 0; s < PPW; ++s) {
+      const int r = s * RPP + lane / NC, cs = lane % NC;
+      const int ch = cs ^ swz<HD>(r);
+      const int key = min(sb * SB + r, kl - 1);  // clamped rows are masked in the softmax
+      glds16(kb_ptr + (size_t)key * HD + ch * 8, kd + s * 1024);
+      glds16(vb_ptr + (size_t)key * HD + ch * 8, kd + BLK + s * 1024);
+    }
+  };
+
+  f32x4_t o[DT];
+#pragma unroll
+  for (int d = 0; d < DT; ++d) o[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float m_run = -INFINITY, l_run = 0.f;
+  int k_off[KF], v_off[DT];
+#pragma unroll
+  for (int kf = 0; kf < KF; ++kf) k_off[kf] = sw_off<HD>(l16, kf * 4 + g);
+  const int key_lo = 4 * g + (l16 >> 2);
+#pragma unroll
+  for (int d = 0; d < DT; ++d) v_off[d] = sw_off<HD>(key_lo, 2 * d + ((l16 & 3) >> 1)) + 8 * (l16 & 1);
+
+  const int nsb = (kl + SB - 1) / SB;
+  int buf = 0;
+  if (w < nsb) stage(w, 0);
+  for (int sb = w; sb < nsb; sb += NW) {
+    const bool more = sb + NW < nsb;
+    if (more) {
+      // the other buffer's previous sub-block was fully read (its ds_reads retired before the
+      // MFMAs that consumed them) - restage it, keep one sub-block in flight
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      stage(sb + NW, buf ^ 1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * PPW) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const unsigned char* ks = my + buf * (2 * BLK);
+    const unsigned char* vs = ks + BLK;
+    f32x4_t s[2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      s[kt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kf = 0; kf < KF; ++kf)
+        s[kt] = mfma16(*reinterpret_cast<const u32x4_t*>(ks + kt * 16 * (HD * 2) + k_off[kf]), qf[kf], s[kt]);
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = sb * SB + kt * 16 + g * 4 + r;
+        const float v = key < kl ? s[kt][r] * scale_log2 : -INFINITY;
+        s[kt][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m_run, mx);
+    const float m_use = m_new == -INFINITY ? 0.f : m_new;
+    const float alpha = __builtin_amdgcn_exp2f(m_run - m_use);
+    float psum = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float pv = __builtin_amdgcn_exp2f(s[kt][r] - m_use);
+        s[kt][r] = pv;
+        psum += pv;
+      }
+    l_run = l_run * alpha + psum;
+    if (__builtin_amdgcn_ballot_w64(m_new != m_run)) {
+#pragma unroll
+      for (int d = 0; d < DT; ++d) o[d] *= alpha;
+    }
+    m_run = m_new;
+    float pf[8];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      pf[r] = s[0][r];
+      pf[4 + r] = s[1][r];
+    }
+    const u32x4_t b = pack8(pf);
+#pragma unroll
+    for (int d = 0; d < DT; ++d) {
+      const v4s_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s_t*)(vs + v_off[d]));
+      const v4s_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (__attribute__((address_space(3))) v4s_t*)(vs + 16 * (HD * 2) + v_off[d]));
+      u32x4_t a;
+      a[0] = __builtin_bit_cast(u32x2_t, lo)[0];
+      a[1] = __builtin_bit_cast(u32x2_t, lo)[1];
+      a[2] = __builtin_bit_cast(u32x2_t, hi)[0];
+      a[3] = __builtin_bit_cast(u32x2_t, hi)[1];
+      o[d] = mfma16(a, b, o[d]);
+    }
+    buf ^= 1;
+  }
+  l_run += __shfl_xor(l_run, 16, 64);
+  l_run += __shfl_xor(l_run, 32, 64);
+
+  // merge the NW partial states through LDS: per wave O^T[dim][head] (fp32), m[head], l[head]
+  __syncthreads();  // every wave is done with its staging buffers
+  float* Ow = reinterpret_cast<float*>(smem);           // [NW][16 heads][HD]
+  float* mw = Ow + NW * 16 * HD;                          // [NW][16]
+  float* lw = mw + NW * 16;                               // [NW][16]
+#pragma unroll
+  for (int d = 0; d < DT; ++d)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) Ow[(w * 16 + l16) * HD + d * 16 + 4 * g + r] = o[d][r];
+  if (g == 0) {
+    mw[w * 16 + l16] = m_run;
+    lw[w * 16 + l16] = l_run;
+  }
+  __syncthreads();
+  // 8 output dims per thread-unit: units (head < G, dim octet)
+  for (int u = tid; u < G * (HD / 8); u += NW * 64) {
+    const int hh = u / (HD / 8), d0 = (u % (HD / 8)) * 8;
+    float M = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) M = fmaxf(M, mw[i * 16 + hh]);
+    const float Mu = M == -INFINITY ? 0.f : M;
+    float L = 0.f, acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+      const float f = __builtin_amdgcn_exp2f(mw[i * 16 + hh] - Mu);
+      L += lw[i * 16 + hh] * f;
+      const float* src = Ow + (i * 16 + hh) * HD + d0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += src[j] * f;
+    }
+    const float inv = L > 0.f ? 1.f / L : 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] *= inv;
+    st16(out + (size_t)row * ldo + (size_t)(kvh * G + hh) * HD + d0, pack8(acc));
+  }
+}
+
+template <int HD>
+int launch_gqa_decode(int nw, const bf16_raw* q, int ldq, const bf16_raw* k, const bf16_raw* v, const int* slot,
+                      const int* pos, const int* kvlen, int rows, int n_heads, int n_kv, int t_max, float sl2,
+                      bf16_raw* o, int ldo, hipStream_t stream) {
+  dim3 grid(rows * n_kv);
+  if (nw == 1)
+    gqa_decode_kernel<HD, 1><<<grid, 64, 0, stream>>>(q, ldq, k, v, slot, pos, kvlen, n_heads, n_kv, t_max, sl2, o, ldo);
+  else if (nw == 2)
+    gqa_decode_kernel<HD, 2><<<grid, 128, 0, stream>>>(q, ldq, k, v, slot, pos, kvlen, n_heads, n_kv, t_max, sl2, o, ldo);
+  else if (nw == 4)
+    gqa_decode_kernel<HD, 4><<<grid, 256, 0, stream>>>(q, ldq, k, v, slot, pos, kvlen, n_heads, n_kv, t_max, sl2, o, ldo);
+  else
+    return LSA_UNSUPPORTED;
   return LSA_OK;
 }
 
@@ -350,26 +520,32 @@ extern "C" int lsa_attn_prefill(const void* q, int ldq, const void* kc, const vo
   return LSA_OK;
 }
 
-// GQA decode attention on MFMA: one workgroup per (decode row, KV head) with the group's
-// G = n_heads / n_kv query heads (G = 4 or 8), keys [0, kv_len or pos + 1) of the row's cache
-// slot, no split over keys (callers use it when rows x n_kv fills the GPU). Same numerics as
-// the prefill kernel (bf16 P for the PV MFMA).
+// GQA decode attention on MFMA (gqa_decode_kernel): one workgroup per (decode row, KV head),
+// the group's G = n_heads / n_kv query heads (2 <= G <= 16) as the MFMA columns, keys
+// [0, kv_len or pos + 1) of the row's cache slot split over ``nw`` (2 / 4) waves, no split over
+// workgroups (callers use it when rows x n_kv fills the GPU). Same numerics as the prefill
+// kernel (bf16 P for the PV MFMA). ``nw``: 1 / 2 / 4 waves per item (0 = 2: measured fastest at
+// 150 keys - 4.4-4.7 TB/s vs 3.1 with 4 waves, whose 32-key sub-blocks leave waves idle - and
+// within 3 % of 4 waves at 1-4k keys: profiles/r3_attn_gqa_decode.jsonl).
 extern "C" int lsa_attn_decode_mfma(const void* q, int ldq, const void* kc, const void* vc, const int* slot,
                                     const int* pos, const int* kv_len, int rows, int n_heads, int n_kv, int head_dim,
-                                    int t_max, float scale, void* out, int ldo, hipStream_t stream) {
+                                    int t_max, float scale, void* out, int ldo, int nw, hipStream_t stream) {
   if (rows < 1 || n_kv < 1 || n_heads % n_kv || !slot || !pos) return LSA_BAD_SHAPE;
   const int g = n_heads / n_kv;
-  if (g != 4 && g != 8) return LSA_UNSUPPORTED;
+  if (g < 2 || g > 16) return LSA_UNSUPPORTED;
+  if (ldo % 8 || reinterpret_cast<uintptr_t>(out) % 16 || ldq % 8 || reinterpret_cast<uintptr_t>(q) % 16)
+    return LSA_BAD_SHAPE;
   const float sl2 = scale * 1.4426950408889634f;
   const auto* qq = static_cast<const bf16_raw*>(q);
   const auto* k = static_cast<const bf16_raw*>(kc);
   const auto* v = static_cast<const bf16_raw*>(vc);
   auto* o = static_cast<bf16_raw*>(out);
+  if (nw == 0) nw = 2;
   int rc;
   if (head_dim == 128)
-    rc = launch_decode_mfma<128>(g, qq, ldq, k, v, slot, pos, kv_len, rows, n_heads, n_kv, t_max, sl2, o, ldo, stream);
+    rc = launch_gqa_decode<128>(nw, qq, ldq, k, v, slot, pos, kv_len, rows, n_heads, n_kv, t_max, sl2, o, ldo, stream);
   else if (head_dim == 64)
-    rc = launch_decode_mfma<64>(g, qq, ldq, k, v, slot, pos, kv_len, rows, n_heads, n_kv, t_max, sl2, o, ldo, stream);
+    rc = launch_gqa_decode<64>(nw, qq, ldq, k, v, slot, pos, kv_len, rows, n_heads, n_kv, t_max, sl2, o, ldo, stream);
   else
     return LSA_UNSUPPORTED;
   if (rc != LSA_OK) return rc;

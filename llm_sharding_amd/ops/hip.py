@@ -65,7 +65,7 @@ def lib() -> ctypes.CDLL:
     L.lsa_gemm.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(EpiArgs), i, i, vp, vp, vp]
     L.lsa_attn_decode.argtypes = [vp, i, vp, vp, vp, vp, vp, i, i, i, i, i, f, i, i, vp, vp, vp, i, vp, vp]
     L.lsa_attn_prefill.argtypes = [vp, i, vp, vp, vp, i, i, i, i, i, f, i, vp, i, vp]
-    L.lsa_attn_decode_mfma.argtypes = [vp, i, vp, vp, vp, vp, vp, i, i, i, i, i, f, vp, i, vp]
+    L.lsa_attn_decode_mfma.argtypes = [vp, i, vp, vp, vp, vp, vp, i, i, i, i, i, f, vp, i, i, vp]
     L.lsa_embed.argtypes = [vp, i, vp, i, vp, i, vp]
     L.lsa_rmsnorm.argtypes = [vp, i, vp, i, i, f, vp, i, vp]
     L.lsa_layernorm.argtypes = [vp, i, vp, vp, vp, vp, i, i, f, vp, i, vp]
@@ -503,12 +503,13 @@ def attn(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, slot: to
     t_max = k_cache.shape[2]
     sc = head_dim ** -0.5 if scale is None else scale
     g = n_heads // n_kv
-    if g in (4, 8) and rows * n_kv >= ATTN_MFMA_MIN_ITEMS and ATTN_MFMA:
+    if 2 <= g <= 16 and rows * n_kv >= ATTN_MFMA_MIN_ITEMS and ATTN_MFMA:
         # GQA with enough (row, kv-head) work items to fill the GPU unsplit: the MFMA kernel
-        # (attn_prefill.hip decode mode: one K/V stream per item serves all G query heads)
+        # (attn_prefill.hip gqa_decode_kernel: the G query heads are the MFMA columns, one K/V
+        # stream per item serves all of them)
         rc = lib().lsa_attn_decode_mfma(_p(q), q.stride(0), _p(k_cache), _p(v_cache), _p(slot), _p(pos), _p(kv_len),
                                         rows, n_heads, n_kv, head_dim, t_max, float(sc), _p(out), out.stride(0),
-                                        _stream())
+                                        ATTN_GQA_NW, _stream())
         _check(rc, "lsa_attn_decode_mfma")
         return
     if nsplit > 1 and counters is None:
@@ -526,6 +527,7 @@ def attn(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, slot: to
 # below it the split-KV VALU kernel, which spreads long contexts over more workgroups
 ATTN_MFMA_MIN_ITEMS = int(os.environ.get("LSA_ATTN_MFMA_MIN_ITEMS", "512"))
 ATTN_MFMA = os.environ.get("LSA_ATTN_MFMA", "1") == "1"
+ATTN_GQA_NW = int(os.environ.get("LSA_ATTN_GQA_NW", "0"))  # waves per (row, kv-head) item: 1 / 2 / 4 (0 = 2)
 
 PREFILL_TILE_ROWS = 128  # positions per tile with one query head per workgroup
 

@@ -1,7 +1,9 @@
-"""GQA decode attention on MFMA (attn_prefill.hip decode mode, lsa_attn_decode_mfma): rows of
-one query position each against their own cache slots, G = 4 / 8 query heads per KV head, head
-dims 64 / 128, per-row lengths (causal pos + 1, or explicit kv_len) - against an fp32 torch
-reference, and the hip.attn dispatch (which picks this kernel for GQA batches that fill the GPU)."""
+"""GQA decode attention on MFMA (attn_prefill.hip gqa_decode_kernel, lsa_attn_decode_mfma): rows
+of one query position each against their own cache slots, G = 2 / 3 / 4 / 8 / 16 query heads per
+KV head (3: Llama-3.2-3B, the reference's configured model; 8: Llama-2-70B), head dims 64 / 128,
+2 or 4 waves splitting the keys, per-row lengths (causal pos + 1, or explicit kv_len) - against
+an fp32 torch reference, and the hip.attn dispatch (which picks this kernel for GQA batches that
+fill the GPU)."""
 import pytest
 import torch
 
@@ -24,9 +26,11 @@ def _ref(q, kc, vc, slot, lens, nh, nkv, hd):
     return out
 
 
-@pytest.mark.parametrize("nh,nkv,hd", [(64, 8, 128), (32, 8, 128), (16, 2, 64)])
+@pytest.mark.parametrize("nh,nkv,hd", [(64, 8, 128), (24, 8, 128), (32, 8, 128), (16, 2, 64), (32, 16, 128),
+                                       (32, 2, 128), (12, 4, 64)])
 @pytest.mark.parametrize("explicit_len", [False, True])
-def test_attn_decode_mfma_vs_fp32(nh, nkv, hd, explicit_len):
+@pytest.mark.parametrize("nw", [1, 2, 4])
+def test_attn_decode_mfma_vs_fp32(nh, nkv, hd, explicit_len, nw):
     from llm_sharding_amd.ops import hip
     torch.manual_seed(0)
     rows, slots, tmax = 40, 48, 320
@@ -40,7 +44,7 @@ def test_attn_decode_mfma_vs_fp32(nh, nkv, hd, explicit_len):
     out = torch.zeros(rows, nh * hd, dtype=torch.bfloat16, device=DEV)
     rc = hip.lib().lsa_attn_decode_mfma(hip._p(q), q.stride(0), hip._p(kc), hip._p(vc), hip._p(slot), hip._p(pos),
                                         hip._p(kv_len), rows, nh, nkv, hd, tmax, float(hd ** -0.5), hip._p(out),
-                                        out.stride(0), hip._stream())
+                                        out.stride(0), nw, hip._stream())
     assert rc == 0
     torch.cuda.synchronize()
     lens = (kv_len if explicit_len else pos + 1).cpu()
@@ -49,12 +53,14 @@ def test_attn_decode_mfma_vs_fp32(nh, nkv, hd, explicit_len):
     assert err < 1e-2, err
 
 
-def test_attn_dispatch_uses_mfma_for_big_gqa_batches():
-    """hip.attn: a 70B-shaped batch (64 / 8 heads, 128 rows) goes to the MFMA kernel and agrees
-    with the split-KV kernel it replaces (LSA_ATTN_MFMA switch), within bf16 rounding."""
+@pytest.mark.parametrize("nh,nkv", [(64, 8), (24, 8)])
+def test_attn_dispatch_uses_mfma_for_big_gqa_batches(nh, nkv):
+    """hip.attn: a 70B-shaped (64 / 8 heads) or 3B-shaped (24 / 8) batch of 128 rows goes to the
+    MFMA kernel and agrees with the split-KV kernel it replaces (LSA_ATTN_MFMA switch), within
+    bf16 rounding."""
     from llm_sharding_amd.ops import hip
     torch.manual_seed(1)
-    rows, nh, nkv, hd, tmax = 128, 64, 8, 128, 256
+    rows, hd, tmax = 128, 128, 256
     kc = torch.randn(rows, nkv, tmax, hd, device=DEV).to(torch.bfloat16)
     vc = torch.randn_like(kc)
     q = torch.randn(rows, nh * hd, device=DEV).to(torch.bfloat16)
