@@ -524,9 +524,9 @@ extern "C" int lsa_attn_prefill(const void* q, int ldq, const void* kc, const vo
 // the group's G = n_heads / n_kv query heads (2 <= G <= 16) as the MFMA columns, keys
 // [0, kv_len or pos + 1) of the row's cache slot split over ``nw`` (2 / 4) waves, no split over
 // workgroups (callers use it when rows x n_kv fills the GPU). Same numerics as the prefill
-// kernel (bf16 P for the PV MFMA). ``nw``: 1 / 2 / 4 waves per item (0 = 2: measured fastest at
-// 150 keys - 4.4-4.7 TB/s vs 3.1 with 4 waves, whose 32-key sub-blocks leave waves idle - and
-// within 3 % of 4 waves at 1-4k keys: profiles/r3_attn_gqa_decode.jsonl).
+// kernel (bf16 P for the PV MFMA). ``nw``: 1 / 2 / 4 waves per item (0 = 1: measured fastest at
+// 150 keys - 5.0-5.2 TB/s vs 4.4-4.7 with 2 waves and 3.1 with 4, whose 32-key sub-blocks leave
+// waves idle - and within 3 % of 4 waves at 1-4k keys: profiles/r3_attn_gqa_decode.jsonl).
 extern "C" int lsa_attn_decode_mfma(const void* q, int ldq, const void* kc, const void* vc, const int* slot,
                                     const int* pos, const int* kv_len, int rows, int n_heads, int n_kv, int head_dim,
                                     int t_max, float scale, void* out, int ldo, int nw, hipStream_t stream) {
@@ -540,7 +540,7 @@ extern "C" int lsa_attn_decode_mfma(const void* q, int ldq, const void* kc, cons
   const auto* k = static_cast<const bf16_raw*>(kc);
   const auto* v = static_cast<const bf16_raw*>(vc);
   auto* o = static_cast<bf16_raw*>(out);
-  if (nw == 0) nw = 2;
+  if (nw == 0) nw = 1;
   int rc;
   if (head_dim == 128)
     rc = launch_gqa_decode<128>(nw, qq, ldq, k, v, slot, pos, kv_len, rows, n_heads, n_kv, t_max, sl2, o, ldo, stream);

@@ -74,7 +74,7 @@ def lib() -> ctypes.CDLL:
     L.lsa_argmax_finalize.argtypes = [vp, i, vp, vp, i, vp, i, i, vp, vp]
     L.lsa_pos_advance.argtypes = [vp, i, i, vp]
     L.lsa_gemm_sk.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(EpiArgs), i, i, i, i, i, i, i, vp, vp, ctypes.c_longlong, i,
-                              vp]
+                              i, vp]
     for name in ("lsa_gemv", "lsa_gemv_coop", "lsa_gemv_fp8", "lsa_dequant_fp8_packed", "lsa_gemv_coop_fp8", "lsa_gemm",
                  "lsa_gemm_sk", "lsa_attn_decode", "lsa_attn_prefill", "lsa_embed", "lsa_rmsnorm", "lsa_layernorm",
                  "lsa_resid_rmsnorm_partials", "lsa_row_ss",
@@ -357,6 +357,10 @@ def default_sk_workspace(device=None) -> SkWorkspace:
 
 
 N_CU = 256
+# gemm_sk: non-temporal weight DMA up to this many rows. Off by default: the ablation builds measured
+# 1.5-4 % at M = 512 (profiles/r3_gemm_sk_ablation.jsonl "w_nt"), but the re-tuned decode shapes and
+# the headline bench did not move beyond noise (36.33k vs 36.56k tok/s; profiles/r3_gemm_nt_retune.jsonl)
+SK_NT_MAX_ROWS = int(os.environ.get("LSA_SK_NT_MAX_ROWS", "0"))
 
 
 SK_TUNING_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_sk_tuning.json")
@@ -437,12 +441,14 @@ def gemm_sk_plan(M: int, N: int, K: int, tuned: bool = True) -> tuple:
 
 def gemm_sk(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep: EpiArgs,
             bn: int = 0, grid: int = 0, dp: int = 1, group_m: int = 8, nb: int = 0, split: int = -1,
-            ws: Optional[SkWorkspace] = None, bm: int = 0, out_numel: int = 0) -> None:
+            ws: Optional[SkWorkspace] = None, bm: int = 0, out_numel: int = 0, wnt: Optional[bool] = None) -> None:
     """Projection GEMM for any M (gemm_sk.hip): ``bm`` x ``bn`` tiles (bm 256 / 128), LDS-DMA
     staged, data-parallel rounds + stream-K, fused epilogue. ``wp`` = pack_b(W[N, K]); K % 64
     == 0; N % bn == 0 for bn = 128 / 256, N % 16 == 0 for bn = 192 (partial last column tile).
     bn = bm = 0: the plan's (gemm_sk_plan). EPI_PARTIAL writes ``split`` x M x ldo fp32 values
-    to ``ep.out``: ``out_numel`` (its capacity in floats) is required and checked first."""
+    to ``ep.out``: ``out_numel`` (its capacity in floats) is required and checked first.
+    ``wnt``: non-temporal weight DMA (default: M <= SK_NT_MAX_ROWS, the decode-sized GEMMs whose
+    weights are streamed once)."""
     _req(_is_bf16_cuda(a, wp), "gemm_sk: bf16 cuda tensors required")
     _req(wp.numel() == N * K and K % 64 == 0 and K >= 64, "gemm_sk: packed weight shape")
     _req(a.dim() == 2 and a.shape[0] >= M >= 1 and a.shape[1] >= K and a.stride(1) == 1 and a.stride(0) % 8 == 0,
@@ -478,8 +484,10 @@ def gemm_sk(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int,
     _req(bm in (128, 256), "gemm_sk: bm")
     _req(ws.slab.numel() >= 2 * grid * bm * bn and ws.counters.numel() >= 2 * grid,
          f"gemm_sk: workspace too small for grid={grid} bn={bn}")
+    if wnt is None:
+        wnt = M <= SK_NT_MAX_ROWS
     rc = lib().lsa_gemm_sk(_p(a), a.stride(0), _p(wp), M, N, K, epi, ctypes.byref(ep), bm, bn, nb, grid, dp, split, group_m,
-                           _p(ws.slab), _p(ws.counters), ws.slab.numel(), ws.counters.numel(), _stream())
+                           _p(ws.slab), _p(ws.counters), ws.slab.numel(), ws.counters.numel(), int(bool(wnt)), _stream())
     _check(rc, "lsa_gemm_sk")
 
 
@@ -527,7 +535,7 @@ def attn(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, slot: to
 # below it the split-KV VALU kernel, which spreads long contexts over more workgroups
 ATTN_MFMA_MIN_ITEMS = int(os.environ.get("LSA_ATTN_MFMA_MIN_ITEMS", "512"))
 ATTN_MFMA = os.environ.get("LSA_ATTN_MFMA", "1") == "1"
-ATTN_GQA_NW = int(os.environ.get("LSA_ATTN_GQA_NW", "0"))  # waves per (row, kv-head) item: 1 / 2 / 4 (0 = 2)
+ATTN_GQA_NW = int(os.environ.get("LSA_ATTN_GQA_NW", "0"))  # waves per (row, kv-head) item: 1 / 2 / 4 (0 = 1)
 
 PREFILL_TILE_ROWS = 128  # positions per tile with one query head per workgroup
 

@@ -47,7 +47,7 @@ def main():
     for v in VARIANTS:
         L = ctypes.CDLL(so(v))
         L.lsa_gemm_sk.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(hip.EpiArgs), i, i, i, i, i, i, i, vp, vp,
-                                  ctypes.c_longlong, i, vp]
+                                  ctypes.c_longlong, i, i, vp]
         libs[v] = L
     ws = hip.SkWorkspace("cuda")
     for c in range(0, len(args), 5):
@@ -62,7 +62,7 @@ def main():
             def run(it, L=L):
                 rc = L.lsa_gemm_sk(x.data_ptr(), x.stride(0), wps[it % nbuf].data_ptr(), M, N, K, hip.EPI_STORE,
                                    ctypes.byref(ep), 256, bn, 0, hip.N_CU, 1, split, 8, ws.slab.data_ptr(),
-                                   ws.counters.data_ptr(), ws.slab.numel(), ws.counters.numel(),
+                                   ws.counters.data_ptr(), ws.slab.numel(), ws.counters.numel(), 0,
                                    torch.cuda.current_stream().cuda_stream)
                 assert rc == 0, rc
             res[v] = round(timeit(run), 2)
