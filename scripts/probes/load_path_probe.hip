@@ -8,16 +8,21 @@
 typedef __attribute__((ext_vector_type(4))) unsigned int u4;
 
 template <int MODE, int DEPTH>
-__global__ __launch_bounds__(512) void probe(const unsigned char* __restrict__ src, int iters, unsigned* sink) {
+__global__ __launch_bounds__(512) void probe(const unsigned char* __restrict__ src, int iters, unsigned* sink,
+                                             long long span) {
   __shared__ __attribute__((aligned(16))) unsigned char lds[128 * 1024];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   u4 acc = {0u, 0u, 0u, 0u};
-  // each wave walks its own 64 KiB window of the 1 MiB buffer (16 waves' windows per 1 MiB)
-  const unsigned char* base = src + ((blockIdx.x * 8 + w) % 16) * 65536;
+  // span == 0: each wave walks its own 64 KiB window of the 1 MiB buffer (L2-resident);
+  // span > 0: each wave streams through its own 1/2048 slice of a span-byte buffer (MALL / HBM)
+  const long long slice = span > 0 ? span / 2048 : 65536;
+  const unsigned char* base = src + (span > 0 ? (long long)(blockIdx.x * 8 + w) * slice
+                                              : (long long)((blockIdx.x * 8 + w) % 16) * 65536);
+  const int nkb = (int)(slice / 1024);
   for (int it = 0; it < iters; ++it) {
 #pragma unroll
     for (int d = 0; d < DEPTH; ++d) {
-      const int off = ((it * DEPTH + d) % 64) * 1024 + lane * 16;
+      const long long off = (long long)((it * DEPTH + d) % nkb) * 1024 + lane * 16;
       if (MODE == 0 || (MODE == 2 && (d & 1) == 0)) {
         __builtin_amdgcn_global_load_lds(base + off, (__attribute__((address_space(3))) void*)(lds + (w * 16 + (d % 16)) * 1024),
                                          16, 0, 0);
@@ -35,15 +40,18 @@ __global__ __launch_bounds__(512) void probe(const unsigned char* __restrict__ s
   if ((acc[0] ^ acc[1] ^ acc[2] ^ acc[3]) == 0x12345678u) sink[0] = 1;
 }
 
-extern "C" int run_probe(int mode, int depth, const void* src, int grid, int iters, unsigned* sink, hipStream_t s) {
+extern "C" int run_probe(int mode, int depth, const void* src, int grid, int iters, unsigned* sink, long long span,
+                         hipStream_t s) {
   const auto* p = static_cast<const unsigned char*>(src);
-#define L(M, D) probe<M, D><<<grid, 512, 0, s>>>(p, iters, sink)
+#define L(M, D) probe<M, D><<<grid, 512, 0, s>>>(p, iters, sink, span)
   if (mode == 0 && depth == 8) L(0, 8);
   else if (mode == 0 && depth == 16) L(0, 16);
   else if (mode == 1 && depth == 8) L(1, 8);
   else if (mode == 1 && depth == 16) L(1, 16);
   else if (mode == 2 && depth == 8) L(2, 8);
   else if (mode == 2 && depth == 16) L(2, 16);
+  else if (mode == 0 && depth == 32) L(0, 32);
+  else if (mode == 1 && depth == 32) L(1, 32);
   else return 1;
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
