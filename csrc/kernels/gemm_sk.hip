@@ -36,14 +36,6 @@ constexpr int BK = 64, NTHR = 512;
 // BN = 192 exists for shapes where 256-wide tiles leave CUs idle or need split-K fixups
 // (Llama-2-7B qkv N=12288 at M=512: 2 x 64 = 128 tiles; gate_up N=22016: 230 tiles in one
 // round at full K); N need not be a multiple of 192 (the last column tile is partial).
-// NB: DMA ring. 2 / 3 = that many K-tile buffers, every wave staging both operands. 4 = ROLE-SPLIT
-// rings: waves 0-3 stage only the weights (B) into an NBB-deep ring and waves 4-7 only the
-// activations (A) into a 3-deep ring. Each wave's counted vmcnt then covers one stream only, so
-// the cold weight stream (HBM latency: every weight byte is read once per decode step) runs
-// 2-3 K-tiles ahead while the L2-resident activations keep a shorter lead - with one shared
-// queue the in-order vmcnt bounds EVERY operand's lead by the operand waited on most often.
-// (scripts/load_path_probe.py: one CU takes ~125 GB/s from L2 by LDS-DMA, gemm_sk's shared
-// ring ~50-60 at decode sizes: profiles/r3_load_path_probe.jsonl, r3_gemm_sk_ablation.jsonl.)
 template <int BM, int BN, int NB>
 struct Geo {
   static constexpr int WM = BN == 256 ? 2 : 4;   // wave grid
@@ -63,24 +55,12 @@ struct Geo {
   static constexpr int EROWS = (TN > 64 || TM < 64) ? 32 : 64;  // rows per epilogue transpose pass
   static constexpr int ELD = TN + 4;                // fp32 row stride of the transpose image
   static constexpr int EPI_BYTES = 8 * EROWS * ELD * 4;
-  // role-split rings (NB == 4): A ring of NA K-tiles, B ring of NBB K-tiles, LDS [A slots][B slots]
-  static constexpr bool RS = NB == 4;
-  static constexpr int ATILE = 2 * AREG, BTILE = 2 * BREG;
-  static constexpr int NA = 3;
-  static constexpr int NBB_FIT = (160 * 1024 - NA * ATILE) / BTILE;
-  static constexpr int NBB = NBB_FIT > 6 ? 6 : NBB_FIT;
-  static constexpr int AGLW = AREG / 1024 / 4;      // RS: A DMA per A-wave per region
-  static constexpr int BGLW = BBLK / 4;             // RS: B DMA per B-wave per region
-  static constexpr int MAXG = AGLW > BGLW ? AGLW : BGLW;
-  static constexpr int RING = RS ? NA * ATILE + NBB * BTILE : NB * BUF;
-  // row rstd of the tile [BM]; RS: aliases the ring (only used after the main loop has drained)
-  static constexpr int RS_OFF = RS ? EPI_BYTES : (NB * BUF > EPI_BYTES ? NB * BUF : EPI_BYTES);
-  static constexpr int SMEM = RS ? (RING > RS_OFF + BM * 4 + 16 ? RING : RS_OFF + BM * 4 + 16) : RS_OFF + BM * 4 + 16;
+  static constexpr int RS_OFF = (NB * BUF > EPI_BYTES ? NB * BUF : EPI_BYTES);  // row rstd of the tile [BM]
+  static constexpr int SMEM = RS_OFF + BM * 4 + 16;
   static_assert(SMEM <= 160 * 1024, "LDS budget");
   static_assert(BHI_WAVES == 0 || BGL_LO == 0 || BHI_WAVES == 4, "B blocks per wave");
   static_assert(AGL >= 1 && TM % EROWS == 0 && FM % 2 == 0, "tile geometry");
-  static_assert(NB == 2 || NB == 4 || BHI_WAVES == 0, "3-buffer ring needs the same DMA count in every wave");
-  static_assert(!RS || (NBB >= 3 && BBLK % 4 == 0 && (AREG / 1024) % 4 == 0), "role-split ring geometry");
+  static_assert(NB == 2 || BHI_WAVES == 0, "3-buffer ring needs the same DMA count in every wave");
 };
 
 struct SkParams {
@@ -172,9 +152,6 @@ struct Kern {
                        NPT = G_::NPT, NPT_LO = G_::NPT_LO, BGL_LO = G_::BGL_LO, BHI_WAVES = G_::BHI_WAVES,
                        BBLK = G_::BBLK;
   static constexpr int HM = FM / 2, HN = FN / 2;  // quadrant size in 16x16 tiles
-  static constexpr bool RS = G_::RS;
-  static constexpr int NA = G_::NA, NBB = G_::NBB, ATILE = G_::ATILE, BTILE = G_::BTILE, AGLW = G_::AGLW,
-                       BGLW = G_::BGLW, MAXG = G_::MAXG;
 
   unsigned char* smem;
   const bf16_raw* A;
@@ -222,34 +199,6 @@ struct Kern {
     }
   }
 
-  // ---- role-split rings (NB == 4): per-role staging and counted waits ------------------------------
-  LSA_DEVICE void stage_a_rs(int slot, int mh, const unsigned (&off)[2][MAXG], int kt) {
-    unsigned char* dst = smem + slot * ATILE + mh * AREG;
-    const unsigned char* base = a_seg + (size_t)kt * (BK * 2);
-    if constexpr (LSA_SK_ABLATE == 6) return;
-#pragma unroll
-    for (int s = 0; s < AGLW; ++s) glds16(base + off[mh][s], dst + ((w - 4) * AGLW + s) * 1024);
-  }
-  LSA_DEVICE void stage_b_rs(int slot, int nh, const unsigned (&off)[2][MAXG], int kt) {
-    unsigned char* dst = smem + NA * ATILE + slot * BTILE + nh * BREG;
-    const unsigned char* base = b_seg + (size_t)kt * 2048;
-    if constexpr (LSA_SK_ABLATE == 7) return;
-#pragma unroll
-    for (int s = 0; s < BGLW; ++s) glds16_w<WNT>(base + off[nh][s], dst + (s * 4 + w) * 1024);
-  }
-  // wait until at most k K-tiles of this wave's own stream are still in flight
-  LSA_DEVICE void wait_rs(int k) {
-    if (w >= 4) {  // A-waves: 2 * AGLW instructions per K-tile
-      if (k >= 2) vm_wait<4 * AGLW>(); else if (k == 1) vm_wait<2 * AGLW>(); else vm_wait<0>();
-    } else {       // B-waves: 2 * BGLW instructions per K-tile
-      if (k >= 4) vm_wait<8 * BGLW>();
-      else if (k == 3) vm_wait<6 * BGLW>();
-      else if (k == 2) vm_wait<4 * BGLW>();
-      else if (k == 1) vm_wait<2 * BGLW>();
-      else vm_wait<0>();
-    }
-  }
-
   // ---- one segment: K-tiles [ka, kb) of output tile (mt, nt), accumulated into acc -------------
   int stamp_base = 0;
   LSA_DEVICE void run_segment(f32x4_t (&acc)[FM][FN], int mt, int nt, int ka, int kb) {
@@ -260,85 +209,53 @@ struct Kern {
     const int KT32 = P.K >> 5;
     a_seg = reinterpret_cast<const unsigned char*>(A + (size_t)m0 * P.lda + ka * BK);
     b_seg = reinterpret_cast<const unsigned char*>(W) + ((size_t)(n0 >> 4) * KT32 + ka * 2) * 1024;
-    unsigned aoff[2][AGL], boff[2][BGL], roff[2][MAXG];
-    const int nt16_last = (P.N >> 4) - 1 - (n0 >> 4);  // partial last column tile (BN = 192): clamp
-    // block b = 8 whole 128-B rows (full cache lines) of an A region's row-major image, rows
-    // ordered (wr', i, r16); lane -> row b*8 + lane/8, physical 16-B chunk lane%8 holding logical
-    // chunk (lane%8) ^ (row%8) (XOR swizzle: conflict-free fragment reads in rd_a)
-    auto a_block_off = [&](int mh, int b) -> unsigned {
-      const int wi = b >> 1, r16 = (b & 1) * 8 + (lane >> 3);
-      const int wr_ = wi / HM, i = wi % HM, ch = (lane & 7) ^ ((lane >> 3) & 7);
-      if constexpr (LSA_SK_ABLATE == 5) {  // (pre-swizzle fragment-order gather, half lines)
-        const int row = min(m0 + wr_ * TM + mh * (TM / 2) + i * 16 + (lane & 15), P.M - 1) - m0;
-        return (unsigned)((row * P.lda + (b & 1) * 32 + 8 * (lane >> 4)) * 2);
-      }
-      const int row = min(m0 + wr_ * TM + mh * (TM / 2) + i * 16 + r16, P.M - 1) - m0;
-      return (unsigned)((row * P.lda + ch * 8) * 2);
-    };
-    // block b of a B region: one packed 16-col x 32-k fragment (1 KiB, lane-linear)
-    auto b_block_off = [&](int nh, int b) -> unsigned {
-      const int kf = b & 1, wj = b >> 1;
-      const int wc_ = wj / HN, j = wj % HN;
-      const int ntl = min(wc_ * FN + nh * HN + j, nt16_last);
-      return (unsigned)(((ntl * KT32 + kf) * 64 + lane) * 16);
-    };
-    if constexpr (!RS) {
+    unsigned aoff[2][AGL], boff[2][BGL];
 #pragma unroll
-      for (int mh = 0; mh < 2; ++mh)
+    for (int mh = 0; mh < 2; ++mh)
 #pragma unroll
-        for (int s = 0; s < AGL; ++s) aoff[mh][s] = a_block_off(mh, w * AGL + s);
-#pragma unroll
-      for (int nh = 0; nh < 2; ++nh)
-#pragma unroll
-        for (int s = 0; s < BGL; ++s) boff[nh][s] = b_block_off(nh, (s * 8 + w) % BBLK);
-
-      // prologue. NB = 2: RA0(0) RB0(0) RB1(0) RA1(0) [RA0(1) RB0(1)];
-      //           NB = 3: all four regions of tiles 0 [and 1]
-      stage_a(0, 0, aoff, 0);
-      stage_b(0, 0, boff, 0);
-      stage_b(0, 1, boff, 0);
-      stage_a(0, 1, aoff, 0);
-      if (n > 1) {
-        stage_a(1, 0, aoff, 1);
-        stage_b(1, 0, boff, 1);
-        if (NB == 3) {
-          stage_b(1, 1, boff, 1);
-          stage_a(1, 1, aoff, 1);
-          vm_wait<BGL + AGL + NPT>();
-        } else {
-          wait_tile();
+      for (int s = 0; s < AGL; ++s) {
+        // block b = 8 whole 128-B rows (full cache lines) of the region's row-major image, rows
+        // ordered (wr', i, r16); lane -> row b*8 + lane/8, physical 16-B chunk lane%8 holding
+        // logical chunk (lane%8) ^ (row%8) (XOR swizzle: conflict-free fragment reads in rd_a)
+        const int b = w * AGL + s, wi = b >> 1, r16 = (b & 1) * 8 + (lane >> 3);
+        const int wr_ = wi / HM, i = wi % HM, ch = (lane & 7) ^ ((lane >> 3) & 7);
+        if constexpr (LSA_SK_ABLATE == 5) {  // (pre-swizzle fragment-order gather, half lines)
+          const int row = min(m0 + wr_ * TM + mh * (TM / 2) + i * 16 + (lane & 15), P.M - 1) - m0;
+          aoff[mh][s] = (unsigned)((row * P.lda + (b & 1) * 32 + 8 * (lane >> 4)) * 2);
+          continue;
         }
+        const int row = min(m0 + wr_ * TM + mh * (TM / 2) + i * 16 + r16, P.M - 1) - m0;
+        aoff[mh][s] = (unsigned)((row * P.lda + ch * 8) * 2);
+      }
+    const int nt16_last = (P.N >> 4) - 1 - (n0 >> 4);  // partial last column tile (BN = 192): clamp
+#pragma unroll
+    for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+      for (int s = 0; s < BGL; ++s) {
+        const int b = (s * 8 + w) % BBLK, kf = b & 1, wj = b >> 1;
+        const int wc_ = wj / HN, j = wj % HN;
+        const int ntl = min(wc_ * FN + nh * HN + j, nt16_last);
+        boff[nh][s] = (unsigned)(((ntl * KT32 + kf) * 64 + lane) * 16);
+      }
+
+    // prologue. NB = 2: RA0(0) RB0(0) RB1(0) RA1(0) [RA0(1) RB0(1)];
+    //           NB = 3: all four regions of tiles 0 [and 1]
+    stage_a(0, 0, aoff, 0);
+    stage_b(0, 0, boff, 0);
+    stage_b(0, 1, boff, 0);
+    stage_a(0, 1, aoff, 0);
+    if (n > 1) {
+      stage_a(1, 0, aoff, 1);
+      stage_b(1, 0, boff, 1);
+      if (NB == 3) {
+        stage_b(1, 1, boff, 1);
+        stage_a(1, 1, aoff, 1);
+        vm_wait<BGL + AGL + NPT>();
       } else {
-        wait_ab();
+        wait_tile();
       }
     } else {
-      // role-split rings: waves 4-7 stage A (blocks (w-4)*AGLW + s), waves 0-3 stage B (s*4 + w);
-      // prologue: A tiles 0 .. NA-2, B tiles 0 .. NBB-2, tile 0 of this wave's stream landed
-      if (w >= 4) {
-#pragma unroll
-        for (int mh = 0; mh < 2; ++mh)
-#pragma unroll
-          for (int s = 0; s < AGLW; ++s) roff[mh][s] = a_block_off(mh, (w - 4) * AGLW + s);
-#pragma unroll
-        for (int j = 0; j < NA - 1; ++j)
-          if (j < n) {
-            stage_a_rs(j, 0, roff, j);
-            stage_a_rs(j, 1, roff, j);
-          }
-        wait_rs(min(n, NA - 1) - 1);
-      } else {
-#pragma unroll
-        for (int nh = 0; nh < 2; ++nh)
-#pragma unroll
-          for (int s = 0; s < BGLW; ++s) roff[nh][s] = b_block_off(nh, s * 4 + w);
-#pragma unroll
-        for (int j = 0; j < NBB - 1; ++j)
-          if (j < n) {
-            stage_b_rs(j, 0, roff, j);
-            stage_b_rs(j, 1, roff, j);
-          }
-        wait_rs(min(n, NBB - 1) - 1);
-      }
+      wait_ab();
     }
     barrier();
     if (group) barrier();  // stagger: waves 4-7 run one barrier behind waves 0-3
@@ -389,58 +306,7 @@ struct Kern {
       __builtin_amdgcn_s_setprio(0);
     };
 
-    if constexpr (RS) {
-      auto rd_a_rs = [&](int slot, int mh) {
-        if constexpr (LSA_SK_ABLATE == 8 || LSA_SK_ABLATE == 10 || LSA_SK_ABLATE == 11) return;
-        const unsigned char* src = smem + slot * ATILE + mh * AREG;
-#pragma unroll
-        for (int i = 0; i < HM; ++i) {
-          a[i][0] = ld16(src + (wr * HM + i) * 2048 + roff0);
-          a[i][1] = ld16(src + (wr * HM + i) * 2048 + roff1);
-        }
-      };
-      auto rd_b_rs = [&](int slot, int nh, u32x4_t (&bb)[HN][2]) {
-        if constexpr (LSA_SK_ABLATE == 8 || LSA_SK_ABLATE == 10 || LSA_SK_ABLATE == 11) return;
-        const unsigned char* src = smem + NA * ATILE + slot * BTILE + nh * BREG + lane * 16;
-#pragma unroll
-        for (int j = 0; j < HN; ++j)
-#pragma unroll
-          for (int kf = 0; kf < 2; ++kf) bb[j][kf] = ld16(src + ((wc * HN + j) * 2 + kf) * 1024);
-      };
-      // per K-tile t (A slot t % NA, B slot t % NBB): B-waves restage B slot (t-1) % NBB with tile
-      // t+NBB-1 in phase 1, A-waves restage A slot (t-1) % NA with tile t+NA-1 in phases 2-3 (both
-      // slots were last read in tile t-1); in phase 4 each wave waits for ITS stream of tile t+1
-      // (read from the next phase on, after a barrier) - B keeps NBB-2 tiles in flight, A one
-      int sa = 0, sb = 0;
-      for (int t = 0; t < n; ++t) {
-        const int pa = sa == 0 ? NA - 1 : sa - 1, pb = sb == 0 ? NBB - 1 : sb - 1;
-        rd_a_rs(sa, 0);
-        rd_b_rs(sb, 0, b0);
-        if (w < 4 && t + NBB - 1 < n) {
-          stage_b_rs(pb, 0, roff, t + NBB - 1);
-          stage_b_rs(pb, 1, roff, t + NBB - 1);
-        }
-        loop_barrier();
-        mma(0, b0, 0);
-        loop_barrier();
-        rd_b_rs(sb, 1, b1);
-        if (w >= 4 && t + NA - 1 < n) stage_a_rs(pa, 0, roff, t + NA - 1);
-        loop_barrier();
-        mma(0, b1, 1);
-        loop_barrier();
-        rd_a_rs(sa, 1);
-        if (w >= 4 && t + NA - 1 < n) stage_a_rs(pa, 1, roff, t + NA - 1);
-        loop_barrier();
-        mma(1, b1, 1);
-        loop_barrier();
-        wait_rs(min(n - 1, t + (w >= 4 ? NA : NBB) - 1) - (t + 1));
-        loop_barrier();
-        mma(1, b0, 0);
-        loop_barrier();
-        sa = sa + 1 == NA ? 0 : sa + 1;
-        sb = sb + 1 == NBB ? 0 : sb + 1;
-      }
-    } else if (NB == 2) {
+    if (NB == 2) {
       // 2 buffers: RB1/RA1 of tile t+1 go into the other buffer, RA0/RB0 of tile t+2 into this
       // one right after their last reads; each region lands 5-6 phases after its DMA issue and
       // the counted wait keeps one K-tile of DMA in flight
@@ -851,16 +717,6 @@ int launch(const bf16_raw* A, const bf16_raw* W, const SkParams& prm, const EpiA
 template <int BM, int EPI>
 int dispatch(const bf16_raw* A, const bf16_raw* W, const SkParams& prm, const EpiArgs& ep, float* slab,
              unsigned* cnt, int bn, int nb, bool wnt, hipStream_t s) {
-  if (nb == 4) {  // role-split rings (geometries with an NBB >= 3 weight ring)
-    if constexpr (BM == 256) {
-      if (bn == 128) return launch<256, 128, EPI, 4>(A, W, prm, ep, slab, cnt, wnt, s);
-      return LSA_UNSUPPORTED;
-    } else {
-      if (bn == 256) return launch<128, 256, EPI, 4>(A, W, prm, ep, slab, cnt, wnt, s);
-      if (bn == 192) return launch<128, 192, EPI, 4>(A, W, prm, ep, slab, cnt, wnt, s);
-      return launch<128, 128, EPI, 4>(A, W, prm, ep, slab, cnt, wnt, s);
-    }
-  }
   if (bn == 256) {
     if constexpr (BM == 128) {
       if (nb == 3) return launch<BM, 256, EPI, 3>(A, W, prm, ep, slab, cnt, wnt, s);
@@ -876,7 +732,7 @@ int dispatch(const bf16_raw* A, const bf16_raw* W, const SkParams& prm, const Ep
 
 // bm: tile height 256 or 128. bn: tile width 256 / 192 (192: N % 16 == 0, partial last tile) / 128.
 // nb: DMA ring buffers, 2 or 3 (3 for bn 128, and bn 256 at bm 128; 0 = the default: 3 where
-// allowed); 4 = role-split rings (bm 256 with bn 128, or bm 128 with any bn). grid: workgroups (<= 1024); dp: 1 = whole tiles in data-parallel rounds first (0 =
+// allowed). grid: workgroups (<= 1024); dp: 1 = whole tiles in data-parallel rounds first (0 =
 // all tiles are remainder).
 // epi EPI_PARTIAL: every tile split into exactly `split` K ranges (tiles * split <= grid), fp32
 // partial k stored to ((float*)ep->out)[k][M][ldo], no slabs or tickets (lsa_resid_rmsnorm_partials sums them).
@@ -893,8 +749,7 @@ extern "C" int lsa_gemm_sk(const void* a, int lda, const void* wp, int M, int N,
   if (bm != 256 && bm != 128) return LSA_UNSUPPORTED;
   const int BM = bm;
   if (nb == 0) nb = (bn == 128 || (bm == 128 && bn == 256)) ? 3 : 2;
-  if (nb != 2 && !(nb == 3 && (bn == 128 || (bm == 128 && bn == 256))) && !(nb == 4 && (bm == 128 || bn == 128)))
-    return LSA_UNSUPPORTED;
+  if (nb != 2 && !(nb == 3 && (bn == 128 || (bm == 128 && bn == 256)))) return LSA_UNSUPPORTED;
   if (bn == 192 ? (N % 16 || (epi == EPI_SWIGLU && N % 32)) : N % bn) return LSA_BAD_SHAPE;
   if (grid < 1 || grid > 1024 || group_m < 1) return LSA_BAD_SHAPE;
   if (epi == EPI_RESID && !ep->resid) return LSA_BAD_SHAPE;

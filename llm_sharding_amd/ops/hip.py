@@ -397,9 +397,8 @@ def _sk_partial() -> dict:
 
 
 @functools.lru_cache(maxsize=4096)
-def gemm_sk_plan(M: int, N: int, K: int, tuned: bool = True, full: bool = False) -> tuple:
-    """(bn, grid, dp, split, bm) for ``gemm_sk`` (``full``: plus the DMA ring variant nb, 0 =
-    default rings, 4 = role-split rings where the tuner measured them faster). Grid = one workgroup per CU (the kernel holds
+def gemm_sk_plan(M: int, N: int, K: int, tuned: bool = True) -> tuple:
+    """(bn, grid, dp, split, bm) for ``gemm_sk``. Grid = one workgroup per CU (the kernel holds
     ~136-144 KiB of LDS). Whole tiles go out in data-parallel rounds; the remainder either as
     equal K splits (concurrent workgroups stream the same K offsets: L2 reuse) or by stream-K.
 
@@ -414,8 +413,7 @@ def gemm_sk_plan(M: int, N: int, K: int, tuned: bool = True, full: bool = False)
         if cands:
             cfg = min(cands)[1]
             if N % (16 if cfg[0] == 192 else cfg[0]) == 0:
-                p = (cfg[0], N_CU, cfg[2], cfg[3], cfg[4] if len(cfg) > 4 else SK_BM)
-                return p + (cfg[5] if len(cfg) > 5 else 0,) if full else p
+                return (cfg[0], N_CU, cfg[2], cfg[3], cfg[4] if len(cfg) > 4 else SK_BM)
     nkt = K // 64
     best = None
     # per 64-deep K step: 256 x bn tiles ~1.5 / 1.2 / 1.1 us; 128 x bn ~0.72x that (the step is bound
@@ -438,7 +436,7 @@ def gemm_sk_plan(M: int, N: int, K: int, tuned: bool = True, full: bool = False)
             for c in cands:
                 if best is None or c[0] < best[0] - 1e-9:
                     best = c
-    return best[1] + (0,) if full else best[1]
+    return best[1]
 
 
 def gemm_sk(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep: EpiArgs,
@@ -462,7 +460,7 @@ def gemm_sk(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int,
         _req(bn in (128, 192, 256) and split >= 1 and grid >= 1, "gemm_sk partial: explicit bn, grid and split required")
         _req(out_numel >= split * M * ep.ldo, f"gemm_sk partial: output holds {out_numel} floats, "
              f"split {split} x {M} rows x ldo {ep.ldo} needed")
-    pb, pg, pd, ps, pm, pn = gemm_sk_plan(M, N, K, full=True)
+    pb, pg, pd, ps, pm = gemm_sk_plan(M, N, K)
     if ep.ss_out and pb == 192:  # the fused-norm partials are per 64 columns of one wave (TN = 64)
         pb = 256 if N % 256 == 0 else 128
     if epi == EPI_ARGMAX:
@@ -474,8 +472,6 @@ def gemm_sk(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int,
     if not bn:
         bn, grid, split = pb, grid or pg, ps if split < 0 else split
         bm = bm or pm
-        # role-split rings (tuned nb = 4) need an NBB >= 3 weight ring (bn may have been adjusted)
-        nb = nb or (pn if (bm == 128 or bn == 128) else 0)
     bm = bm or SK_BM
     grid = grid or pg
     if split < 0:

@@ -7,10 +7,7 @@ against the fused EPI_RESID + rmsnorm pair; the winner goes in the entry's "part
 heights (bm 256 / 128) are swept. Writes the winners to
 llm_sharding_amd/ops/gemm_sk_tuning.json, which hip.gemm_sk_plan consults before its cost model.
 
-The DMA ring variant is swept too (--nbs: 0 = the default rings, 4 = role-split rings) and
-stored as the entry's sixth field.
-
-usage: tune_gemm_sk.py [--rows 256,512,...] [--models llama2-7b,...] [--out PATH] [--iters N] [--nbs 0,4]
+usage: tune_gemm_sk.py [--rows 256,512,...] [--models llama2-7b,...] [--out PATH] [--iters N]
 One JSON line per (model, shape, M) on stdout with every candidate's time."""
 import argparse
 import json
@@ -48,12 +45,10 @@ def main():
     ap.add_argument("--out", default=os.path.join(ROOT, "llm_sharding_amd", "ops", "gemm_sk_tuning.json"))
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--no-partial", action="store_true", help="skip the EPI_PARTIAL comparison")
-    ap.add_argument("--nbs", default="0,4", help="DMA ring variants: 0 = default rings, 4 = role-split rings")
     a = ap.parse_args()
     from llm_sharding_amd.config import llama2_7b
     from llm_sharding_amd.models.rope import rope_table
     rows = [int(r) for r in a.rows.split(",")]
-    nbs = [int(v) for v in a.nbs.split(",")]
     cos, sin = rope_table(llama2_7b(), 1024, DEV)
     sk_ws = hip.SkWorkspace(DEV)
     entries = []
@@ -90,17 +85,13 @@ def main():
                         if N % (16 if bn == 192 else bn):
                             continue
                         for sp in SPLITS:
-                            for nb in nbs:
-                                if nb == 4 and not (bm == 128 or bn == 128):
-                                    continue
-                                try:
-                                    us = timeit(lambda i: hip.gemm_sk(x, ws[i % nbuf], M, N, K, epi, ep, bn=bn,
-                                                                      grid=hip.N_CU, dp=1, split=sp, ws=sk_ws, bm=bm,
-                                                                      nb=nb), a.iters)
-                                except (RuntimeError, ValueError) as e:  # a config the host rejects for this shape
-                                    print(f"# skip bm={bm} bn={bn} split={sp} nb={nb}: {e}", file=sys.stderr)
-                                    continue
-                                res.append((round(us, 2), bn, sp, bm, nb))
+                            try:
+                                us = timeit(lambda i: hip.gemm_sk(x, ws[i % nbuf], M, N, K, epi, ep, bn=bn, grid=hip.N_CU,
+                                                                  dp=1, split=sp, ws=sk_ws, bm=bm), a.iters)
+                            except (RuntimeError, ValueError) as e:  # a config the host rejects for this shape
+                                print(f"# skip bm={bm} bn={bn} split={sp}: {e}", file=sys.stderr)
+                                continue
+                            res.append((round(us, 2), bn, sp, bm))
                 res.sort()
                 partial = None
                 if epi == hip.EPI_RESID and 128 < M <= hip.PARTIAL_MAX_ROWS and not a.no_partial:
@@ -108,11 +99,11 @@ def main():
                     # fused (EPI_RESID + rmsnorm) against EPI_PARTIAL + resid_rmsnorm_partials
                     xn = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
                     pbuf = torch.zeros(hip.PARTIAL_MAX_SPLIT, M, N, dtype=torch.float32, device=DEV)
-                    bbn, bsp, bbm, bnb = res[0][1], res[0][2], res[0][3], res[0][4]
+                    bbn, bsp, bbm = res[0][1], res[0][2], res[0][3]
 
                     def fused(i):
                         hip.gemm_sk(x, ws[i % nbuf], M, N, K, epi, ep, bn=bbn, grid=hip.N_CU, dp=1, split=bsp, ws=sk_ws,
-                                    bm=bbm, nb=bnb)
+                                    bm=bbm)
                         hip.rmsnorm(out, None, xn, M, 1e-5, N)
                     t_fused = timeit(fused, a.iters)
                     pres = []
@@ -133,10 +124,10 @@ def main():
                     pres.sort()
                     partial = {"fused_us": round(t_fused, 2), "best": pres[0] if pres else None, "all": pres}
                 plan = hip.gemm_sk_plan(M, N, K, tuned=False)
-                model_us = next((r[0] for r in res if (r[1], r[2], r[3], r[4]) == (plan[0], plan[3], plan[4], 0)), None)
+                model_us = next((r[0] for r in res if (r[1], r[2], r[3]) == (plan[0], plan[3], plan[4])), None)
                 fl = 2.0 * M * N * K
                 line = {"model": model, "shape": name, "N": N, "K": K, "M": M, "epi": epi,
-                        "best_us": res[0][0], "best": [res[0][1], hip.N_CU, 1, res[0][2], res[0][3], res[0][4]],
+                        "best_us": res[0][0], "best": [res[0][1], hip.N_CU, 1, res[0][2], res[0][3]],
                         "best_tflops": round(fl / res[0][0] / 1e6, 1), "cost_model_us": model_us,
                         "all": res, "partial": partial}
                 print(json.dumps(line), flush=True)

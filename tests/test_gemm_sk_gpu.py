@@ -75,38 +75,6 @@ def test_gemm_sk_store_resid(M, N, K, ws):
     assert int(ws.counters.abs().sum()) == 0  # every split tile's ticket was reset
 
 
-RS_GEOS = [(256, 128), (128, 128), (128, 192), (128, 256)]  # role-split rings (nb = 4)
-
-
-@pytest.mark.parametrize("M", [1, 200, 512])
-@pytest.mark.parametrize("N,K", [(1024, 512), (768, 1216), (512, 64), (512, 128), (1024, 4096)])
-def test_gemm_sk_role_split_rings(M, N, K, ws):
-    """nb = 4: weight-only / activation-only DMA waves with separate rings (short K: fewer tiles
-    than the ring depth; stream-K grids: segments of 1 .. n tiles)."""
-    h = hip()
-    a = _rnd(M, K)
-    w = _rnd(N, K, scale=0.02)
-    wp = packing.pack_b(w)
-    ref = a.float() @ w.float().T
-    r = _rnd(M, N)
-    for bm, bn in RS_GEOS:
-        if _skip(bn, N):
-            continue
-        for grid, dp, split in [(0, 1, -1), (256, 1, 0), (37, 0, 0), (512, 1, 4)]:
-            tiles = -(-M // bm) * -(-N // bn)
-            if split > 0 and (tiles * split > grid or split > K // 64):
-                continue
-            out = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
-            h.gemm_sk(a, wp, M, N, K, h.EPI_STORE, h.make_epi(out=out, ldo=N), bn=bn, grid=grid, dp=dp, split=split,
-                      nb=4, ws=ws, bm=bm)
-            assert rel_err(out, ref) < 8e-3, (bm, bn, grid, dp, split)
-            o2 = r.clone()
-            h.gemm_sk(a, wp, M, N, K, h.EPI_RESID, h.make_epi(out=o2, resid=o2, ldo=N, ldr=N), bn=bn, grid=grid, dp=dp,
-                      split=split, nb=4, ws=ws, bm=bm)
-            assert rel_err(o2, r.float() + ref) < 8e-3, (bm, bn, grid, dp, split)
-    assert int(ws.counters.abs().sum()) == 0
-
-
 def test_gemm_sk_strided_a_and_big_m(ws):
     """A with a row stride > K (a view into a wider buffer) and enough rows for several
     data-parallel rounds plus a stream-K tail."""
