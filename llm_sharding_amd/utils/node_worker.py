@@ -13,7 +13,9 @@ API parity with ``/root/reference/utils/node_worker.py``:
 
 MI355X-native underneath: the stage forward is a :class:`StageEngine` (fused HIP kernels,
 packed weights, static KV cache, fused final-norm/lm_head/argmax) instead of HF modules and a
-``DynamicCache``. Reference quirks fixed on purpose: causal prefill by
+``DynamicCache``; on the GPU every decode step (seq_len 1) replays a captured hipGraph of the
+stage (``use_graph=True``, one graph per batch size; the reference runs its HF modules eagerly,
+``:227-309``). Reference quirks fixed on purpose: causal prefill by
 default (Q1, ``noncausal_prefill=True`` restores the unmasked reference behaviour); batch > 1
 (Q2: next tokens embed to ``[B, 1, H]``); lm_head only on the last position (Q3); EOS by id as
 well as by string (Q4); no disk staging (Q5); blocking receive with timeout instead of a busy
@@ -48,7 +50,7 @@ from ..models.tokenizer import load_tokenizer
 from ..parallel import protocol
 from ..parallel.communicator import Again, Communicator
 from ..parallel.transport import PullSocket, PushSocket, local_ip, parse_addr
-from ..runtime.engine import ShardFolderSource, StageEngine, WeightSource
+from ..runtime.engine import DecodeGraph, ShardFolderSource, StageEngine, WeightSource
 from .forwarding_utils import build_position_ids
 
 
@@ -74,7 +76,7 @@ class NodeWorker:
                  device="cpu", dtype=torch.float16, backend: str = "tcp", max_batch: int = 8,
                  max_seq: int = 4096, noncausal_prefill: bool = False,
                  source: Optional[WeightSource] = None, verbose: bool = True,
-                 rccl_ranks: Optional[tuple] = None, ship_rope: bool = False):
+                 rccl_ranks: Optional[tuple] = None, ship_rope: bool = False, use_graph: bool = True):
         # backend "rccl": envelopes over TCP, tensors device-to-device over torch.distributed
         self.communicator = Communicator(src_addr=src_addr, dst_addr=dst_addr, backend=backend,
                                          device=torch.device(device), rccl_ranks=rccl_ranks)
@@ -93,6 +95,11 @@ class NodeWorker:
         self.source = source or ShardFolderSource(shards_path, self.config)
         self.verbose = verbose
         self.ship_rope = ship_rope  # send real cos/sin tables in next_state_info (reference wire parity)
+        # GPU decode steps (seq_len 1) replay a captured hipGraph of the stage (one per batch
+        # size) instead of launching every kernel from Python
+        self.use_graph = use_graph
+        self._graphs: dict = {}
+        self._graph_pos: dict = {}
 
         self.tokenizer = None
         self.embed_tokens = None   # embedding table [V, H] (ingress / head stage)
@@ -125,6 +132,7 @@ class NodeWorker:
             raise ValueError("[ERROR] start or end is invalid")
         self.start, self.end = start, end
         self.engine = self.shard = self.lm_head = None
+        self._graphs, self._graph_pos = {}, {}
         if self.device.type == "cuda":
             torch.cuda.empty_cache()
         if self.verbose:
@@ -198,12 +206,16 @@ class NodeWorker:
         eng = self.engine
         past = eng.seq_len[0]
         slots = list(range(B))
-        slot, pos = eng.prefill_rows(slots, [S] * B)
-        kv_len = [past + S] * (B * S) if (self.noncausal_prefill and S > 1) else None
-        h = eng.forward(hs.reshape(B * S, H).to(self.device, eng.dtype), slot, pos, kv_len=kv_len)
-        eng.advance(slots, [S] * B)
+        if S == 1 and self.use_graph and eng.gpu:
+            out = self._graph_step(hs, B, H)
+        else:
+            slot, pos = eng.prefill_rows(slots, [S] * B)
+            kv_len = [past + S] * (B * S) if (self.noncausal_prefill and S > 1) else None
+            h = eng.forward(hs.reshape(B * S, H).to(self.device, eng.dtype), slot, pos, kv_len=kv_len)
+            eng.advance(slots, [S] * B)
+            out = eng.head(h, [b * S + S - 1 for b in range(B)]) if self.end == self.layer_num else h
         if self.end == self.layer_num:
-            return eng.head(h, [b * S + S - 1 for b in range(B)]).to("cpu", torch.long)
+            return out.to("cpu", torch.long)
         if eng.cos is None or not self.ship_rope:
             # every stage derives its positions from its own KV length (the reference ships the
             # first stage's tables down the chain, node_worker.py:267-271): keep the message
@@ -213,7 +225,28 @@ class NodeWorker:
             position_ids = torch.arange(0, S, dtype=torch.long)[None].expand(B, S)
             cos, sin = full_cos_sin(eng.cos[past:past + S].cpu(), eng.sin[past:past + S].cpu(), position_ids,
                                     dtype=eng.dtype)
-        return {"hidden_states": h.reshape(B, S, H).clone(), "cos": cos, "sin": sin}
+        return {"hidden_states": out.reshape(B, S, H).clone(), "cos": cos, "sin": sin}
+
+    def _graph_step(self, hs: torch.Tensor, B: int, H: int) -> torch.Tensor:
+        """One decode step of rows 0..B-1 by hipGraph replay (DecodeGraph "mid", or "last" with
+        the fused head + argmax): the hidden state goes into the graph's input buffer, the
+        positions live on the device and advance inside the graph; they are re-uploaded only
+        when the host's KV lengths moved without the graph (prefill, clear_KV_cache)."""
+        eng = self.engine
+        last = self.end == self.layer_num
+        g = self._graphs.get(B)
+        if g is None:
+            g = DecodeGraph(eng, B, "last" if last else "mid").capture()
+            self._graphs[B] = g
+            self._graph_pos[B] = None
+        want = [int(eng.seq_len[r]) for r in range(B)]
+        if self._graph_pos[B] != want:
+            g.set_positions()
+        g.h_in.copy_(hs.reshape(B, H).to(self.device, eng.dtype))
+        g.replay()
+        eng.advance(list(range(B)), [1] * B)
+        self._graph_pos[B] = [p + 1 for p in want]
+        return g.tokens if last else g.out_hidden
 
     # ------------------------------------------------------------------ autoregression
     @torch.inference_mode()

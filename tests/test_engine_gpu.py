@@ -234,8 +234,11 @@ def test_multistage_concurrent_streams_7b_shapes():
     assert multi.tolist() == single.tolist()
 
 
-def test_node_worker_chain_on_gpu(tiny_shards_bf16):
-    """Reference-API NodeWorkers on the GPU (tcp hand-off on loopback) == single-stage engine."""
+@pytest.mark.parametrize("use_graph", [True, False])
+def test_node_worker_chain_on_gpu(tiny_shards_bf16, use_graph):
+    """Reference-API NodeWorkers on the GPU (tcp hand-off on loopback) == single-stage engine,
+    with the decode steps replayed from hipGraphs (use_graph) or launched eagerly; a second
+    request after clear_KV_cache re-uploads the graphs' positions."""
     import socket
     from llm_sharding_amd.utils.node_worker import NodeWorker
     socks = [socket.socket() for _ in range(2)]
@@ -245,22 +248,29 @@ def test_node_worker_chain_on_gpu(tiny_shards_bf16):
     for s in socks:
         s.close()
     a = NodeWorker(f"tcp://*:{ports[0]}", f"tcp://127.0.0.1:{ports[1]}", True, tiny_shards_bf16, device=DEV,
-                   dtype=torch.float16, verbose=False)
+                   dtype=torch.float16, verbose=False, use_graph=use_graph)
     b = NodeWorker(f"tcp://*:{ports[1]}", f"tcp://127.0.0.1:{ports[0]}", False, tiny_shards_bf16, device=DEV,
-                   dtype=torch.float16, verbose=False)
+                   dtype=torch.float16, verbose=False, use_graph=use_graph)
     a.load_shards(0, 2)
     b.load_shards(2, 4)
     prompt = torch.tensor([[1, 33, 44, 55, 66, 77]])
-    d = a.receive_user_request(input_ids=prompt)
-    for _ in range(6):
-        a.communicator.transfer_data(a.pass_through_shard(d))
-        x = b.communicator.receive_data(timeout_ms=10000)
-        b.communicator.transfer_data(b.pass_through_shard(x))
-        tok = a.communicator.receive_data(timeout_ms=10000)
-        end, d = a.receive_next_token(tok, max_new_tokens=6)
-        if end:
-            break
-    got = a.output_ids()[0, 6:].tolist()
+
+    def run():
+        d = a.receive_user_request(input_ids=prompt)
+        for _ in range(6):
+            a.communicator.transfer_data(a.pass_through_shard(d))
+            x = b.communicator.receive_data(timeout_ms=10000)
+            b.communicator.transfer_data(b.pass_through_shard(x))
+            tok = a.communicator.receive_data(timeout_ms=10000)
+            end, d = a.receive_next_token(tok, max_new_tokens=6)
+            if end:
+                break
+        return a.output_ids()[0, 6:].tolist()
+    got = run()
+    assert bool(a._graphs) == use_graph and bool(b._graphs) == use_graph
+    a.clear_KV_cache()
+    b.clear_KV_cache()
+    assert run() == got
     from llm_sharding_amd.runtime.engine import ShardFolderSource
     cfg = a.config
     eng = StageEngine(cfg, 0, 4, DEV, torch.bfloat16, has_embed=True, has_head=True,
