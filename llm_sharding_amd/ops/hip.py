@@ -63,8 +63,6 @@ def lib() -> ctypes.CDLL:
     L.lsa_dequant_fp8_packed.argtypes = [vp, vp, vp, i, i, vp]
     L.lsa_gemv_coop_fp8.argtypes = [vp, i, vp, vp, vp, i, i, i, i, f, i, ctypes.POINTER(EpiArgs), i, i, i, i, vp, vp, vp]
     L.lsa_gemm.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(EpiArgs), i, i, vp, vp, vp]
-    L.lsa_skinny.argtypes = [vp, i, vp, vp, i, i, i, i, f, i, ctypes.POINTER(EpiArgs), i, i, i, i, vp, ctypes.c_longlong,
-                             vp, i, vp]
     L.lsa_attn_decode.argtypes = [vp, i, vp, vp, vp, vp, vp, i, i, i, i, i, f, i, i, vp, vp, vp, i, vp, vp]
     L.lsa_attn_prefill.argtypes = [vp, i, vp, vp, vp, i, i, i, i, i, f, i, vp, i, vp]
     L.lsa_attn_decode_mfma.argtypes = [vp, i, vp, vp, vp, vp, vp, i, i, i, i, i, f, vp, i, i, vp]
@@ -77,7 +75,7 @@ def lib() -> ctypes.CDLL:
     L.lsa_pos_advance.argtypes = [vp, i, i, vp]
     L.lsa_gemm_sk.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(EpiArgs), i, i, i, i, i, i, i, vp, vp, ctypes.c_longlong, i,
                               i, vp]
-    for name in ("lsa_gemv", "lsa_gemv_coop", "lsa_skinny", "lsa_gemv_fp8", "lsa_dequant_fp8_packed", "lsa_gemv_coop_fp8", "lsa_gemm",
+    for name in ("lsa_gemv", "lsa_gemv_coop", "lsa_gemv_fp8", "lsa_dequant_fp8_packed", "lsa_gemv_coop_fp8", "lsa_gemm",
                  "lsa_gemm_sk", "lsa_attn_decode", "lsa_attn_prefill", "lsa_embed", "lsa_rmsnorm", "lsa_layernorm",
                  "lsa_resid_rmsnorm_partials", "lsa_row_ss",
                  "lsa_argmax_finalize", "lsa_pos_advance", "lsa_version"):
@@ -172,16 +170,14 @@ def _check_epi(epi: int, ep: EpiArgs, N: int) -> None:
 def gemv(x: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep: EpiArgs,
          norm: bool = False, eps: float = 1e-5, a_rows: Optional[torch.Tensor] = None,
          tn: int = 0, nw: int = 0, u: int = 0, coop: Optional[tuple] = None,
-         ws: Optional[CoopWorkspace] = None, skinny: Optional[tuple] = None) -> None:
+         ws: Optional[CoopWorkspace] = None) -> None:
     """Decode / short-prefill projection, M <= 128 rows (> 64: coop kernel only). ``wp`` is ``pack_b(W)`` (``pack_b(fold_norm(W, g))``
     when ``norm``: RMSNorm of the A rows is then applied in-kernel), W: [N, K].
 
     Kernel choice: explicit ``tn/nw/u`` -> streaming GEMV (gemv.hip); explicit
-    ``coop=(tnw, nw, kf, sk[, kw])`` -> cooperative split-K (gemv_coop.hip); explicit
-    ``skinny=(tn, nwv, depth, sk)`` -> register-direct MFMA split-K (skinny_gemm.hip, 17..128
-    rows, no argmax epilogue); none -> the tuned choice of :func:`packing.proj_config`."""
-    from .packing import (GEMV_CONFIGS, coop_candidates, coop_slab_floats, proj_config, row_blocks,
-                          skinny_candidates, skinny_slab_floats)
+    ``coop=(tnw, nw, kf, sk[, kw])`` -> cooperative split-K (gemv_coop.hip); neither -> the tuned
+    choice of :func:`packing.proj_config`."""
+    from .packing import GEMV_CONFIGS, coop_candidates, coop_slab_floats, proj_config, row_blocks
     _req(1 <= M <= 128, f"gemv supports 1..128 rows, got {M}")
     _check_epi(epi, ep, N)
     _req(_is_bf16_cuda(x, wp), "gemv: bf16 cuda tensors required")
@@ -191,31 +187,12 @@ def gemv(x: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep
         _req(x.shape[0] >= M, "gemv: x has fewer rows than M")
     else:
         _req(a_rows.dtype == torch.int32 and a_rows.is_cuda and a_rows.numel() >= M, "gemv: a_rows")
-    if tn == 0 and coop is None and skinny is None:
+    if tn == 0 and coop is None:
         algo, cfg = proj_config(N // 16, M, need_even=(epi == EPI_SWIGLU), k=K)
-        if algo == "skinny" and epi == EPI_ARGMAX:  # (tuned per shape; the head reduces by atomics)
-            algo, cfg = "coop", coop_candidates(N // 16, K, M)[-1]
         if algo == "coop":
             coop = cfg
-        elif algo == "skinny":
-            skinny = cfg
         else:
             tn, nw, u = cfg
-    if skinny is not None:
-        stn, snw, sd, ssk = skinny = tuple(skinny)
-        _req(epi != EPI_ARGMAX, "gemv: the skinny kernel has no argmax epilogue")
-        _req(skinny in skinny_candidates(N // 16, K, M, epi == EPI_SWIGLU),
-             f"gemv: skinny config {skinny} invalid for N={N} K={K} M={M}")
-        _req(x.stride(0) % 8 == 0, "gemv skinny: x rows must be 16-byte aligned")
-        if ws is None:
-            ws = default_workspace(x.device)
-        need = skinny_slab_floats(N, M, stn, ssk)
-        _req(ws.slab.numel() >= need, f"gemv: skinny workspace too small ({ws.slab.numel()} < {need} floats)")
-        rc = lib().lsa_skinny(_p(x), x.stride(0), _p(a_rows), _p(wp), M, N, K, int(norm), float(eps), epi,
-                              ctypes.byref(ep), stn, snw, sd, ssk, _p(ws.slab), ws.slab.numel(), _p(ws.counters),
-                              ws.counters.numel(), _stream())
-        _check(rc, "lsa_skinny")
-        return
     if coop is not None:
         coop = tuple(coop) if len(coop) == 5 else tuple(coop) + (1,)
         tnw, cnw, kf, sk, kw = coop

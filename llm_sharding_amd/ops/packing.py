@@ -200,37 +200,6 @@ def coop_candidates(n_tiles: int, k: int, rows: int) -> list:
     return out
 
 
-# (mb, tn, nwv, depth) instantiated in csrc/kernels/skinny_gemm.hip (LSA_SKINNY_CONFIGS) - keep in sync.
-SKINNY_CONFIGS = [(2, 4, 4, 4), (2, 8, 4, 4), (2, 4, 8, 4), (2, 2, 8, 4), (2, 6, 4, 4), (4, 4, 4, 4), (4, 2, 8, 4),
-                  (4, 4, 8, 3), (4, 8, 4, 3), (4, 3, 4, 4), (4, 6, 4, 3), (8, 4, 4, 3), (8, 2, 4, 4), (8, 2, 8, 3),
-                  (8, 4, 4, 2), (8, 3, 4, 3), (8, 6, 4, 2)]
-SKINNY_SPLITS = (1, 2, 3, 4, 6, 8)
-
-
-def skinny_candidates(n_tiles: int, k: int, rows: int, need_even: bool = False) -> list:
-    """(tn, nwv, depth, sk) for the skinny MFMA projection (skinny_gemm.hip, rows 17..128):
-    every wave of every split keeps at least one 32-k step; at most 4 workgroups per CU."""
-    if rows <= 16 or rows > 128:
-        return []
-    mb = row_blocks(rows)
-    out = []
-    for (b, tn, nwv, depth) in SKINNY_CONFIGS:
-        if b != mb or n_tiles % tn or (need_even and tn % 2):
-            continue
-        for sk in SKINNY_SPLITS:
-            if (k // 32) >= sk * nwv and (n_tiles // tn) * sk <= 4 * N_CU:
-                out.append((tn, nwv, depth, sk))
-    return out
-
-
-def skinny_slab_floats(n: int, rows: int, tn: int, sk: int) -> int:
-    """fp32 workspace a skinny launch needs (0 when sk == 1)."""
-    if sk == 1:
-        return 0
-    mr = 16 * row_blocks(rows)
-    return sk * n * mr + sk * (n // 16 // tn) * mr
-
-
 # (mb, tnw, nw, kf) with fp8 weights (LSA_COOP_FP8_CONFIGS in gemv_coop.hip) - keep in sync.
 COOP_FP8_CONFIGS = [(2, 1, 8, 4), (4, 1, 8, 4), (2, 1, 4, 4), (4, 1, 4, 4), (8, 1, 8, 4), (8, 1, 4, 2), (2, 1, 8, 8),
                     (4, 1, 8, 8)]
@@ -271,10 +240,6 @@ def coop_workspace_need(shapes, max_rows: int = 64, even_n=()) -> tuple:
                 tnw, nw, kf, sk = cfg[:4]
                 floats = max(floats, coop_slab_floats(n, rows, tnw, nw, kf, sk))
                 groups = max(groups, n // 16 // (tnw * nw))
-            elif algo == "skinny":
-                tn, _, _, sk = cfg
-                floats = max(floats, skinny_slab_floats(n, rows, tn, sk))
-                groups = max(groups, n // 16 // tn)
     return floats, groups
 
 
@@ -296,15 +261,14 @@ def _tuned() -> dict:
 
 
 def proj_config(n_tiles: int, rows: int, need_even: bool = False, k: int = 4096) -> tuple:
-    """("gemv", (tn, nw, u)), ("coop", (tnw, nw, kf, sk, kw)) or ("skinny", (tn, nwv, depth, sk))
-    for a decode projection of ``rows`` rows. The tuning table (measured on MI355X) wins; otherwise rows <= 16 use the
+    """("gemv", (tn, nw, u)) or ("coop", (tnw, nw, kf, sk, kw)) for a decode projection of ``rows``
+    rows. The tuning table (measured on MI355X) wins; otherwise rows <= 16 use the
     weight-streaming GEMV and larger row counts the cooperative split-K kernel with the
     smallest split that fills the 256 CUs."""
     t = _tuned().get((n_tiles * 16, k, row_blocks(rows), bool(need_even)))
     if t is not None:
         algo, cfg = t
         if (algo == "coop" and cfg in coop_candidates(n_tiles, k, rows)) or \
-           (algo == "skinny" and cfg in skinny_candidates(n_tiles, k, rows, need_even)) or \
            (algo == "gemv" and cfg in gemv_candidates(n_tiles, k, rows, need_even)):
             return t
     if rows > 16:

@@ -96,9 +96,6 @@ def gemv_sweep(out_rows, models, rows_list, tune_entries, fp8=False):
                 for cfg in packing.coop_candidates(N // 16, K, M):
                     us = timeit(lambda i: hip.gemv(x, ws[i % nbuf], M, N, K, epi, ep, norm=norm, coop=cfg, ws=cws))
                     res.append((us, "coop", cfg, N * K * 2 / us / 1e6))
-                for cfg in packing.skinny_candidates(N // 16, K, M, even) if epi != hip.EPI_ARGMAX else []:
-                    us = timeit(lambda i: hip.gemv(x, ws[i % nbuf], M, N, K, epi, ep, norm=norm, skinny=cfg, ws=cws))
-                    res.append((us, "skinny", cfg, N * K * 2 / us / 1e6))
                 if fp8:
                     r8 = []
                     for cfg in packing.fp8_gemv_candidates(N // 16, K, M, even) if M <= 64 else []:
