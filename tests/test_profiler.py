@@ -152,7 +152,8 @@ def test_stage_cost_profile_predicts_deployed_stages():
     for st in plan.stages:
         want = predict_stage_ms(prof, st.n_layers, st.has_embed, st.has_head)
         assert abs(st.est_time - want) < 1e-9
-        got = _measure_stage(cfg, src, st.start, st.end, st.has_embed, st.has_head, 8, 64)
+        # best of 3 medians: a shared CPU host inflates single measurements, never deflates them
+        got = min(_measure_stage(cfg, src, st.start, st.end, st.has_embed, st.has_head, 8, 64) for _ in range(3))
         assert abs(st.est_time - got) / got < 0.15, (st.start, st.end, st.est_time, got, prof)
     # a device measured 2x slower per layer gets fewer layers
     slow = dict(prof, layer_decode_ms=2 * prof["layer_decode_ms"])
