@@ -16,6 +16,13 @@
 //    is reset by the last arriver, so the kernel is replay-safe inside hipGraphs.
 #include "epilogue.h"
 
+// Timing-only builds (scripts/coop_phases.py; outputs garbage): 1 = exit after the main loop,
+// 2 = exit after the k-group / split reduction (no epilogue), 3 = epilogue without its global
+// stores, 4 = epilogue stores of constants (no LDS reads, no math).
+#ifndef LSA_COOP_ABLATE
+#define LSA_COOP_ABLATE 0
+#endif
+
 namespace {
 
 // A tile [MR][KC] bf16 in LDS, 16-B chunks XOR-swizzled so that the 16 lanes of one
@@ -236,6 +243,15 @@ __global__ __launch_bounds__(NW * KW * 64) void gemv_coop_kernel(
     }
   }
   __syncthreads();  // all waves done with the A buffers: smem becomes the reduction tile
+  if constexpr (LSA_COOP_ABLATE == 1) {
+    float t = 0.f;
+#pragma unroll
+    for (int rb = 0; rb < MB; ++rb)
+#pragma unroll
+      for (int q = 0; q < TNW; ++q) t += acc[rb][q][0] + acc[rb][q][1] + acc[rb][q][2] + acc[rb][q][3];
+    if (t == 1.2345f) ep.out[tid] = 0;  // keep the loop live
+    return;
+  }
   if constexpr (KW > 1) {
     // k-groups 1..KW-1 hand their partial tiles to group 0 (fragment-native, 16 B per lane)
     f32x4_t* xp = reinterpret_cast<f32x4_t*>(smem);  // [KW-1][TG][MB][64]
@@ -257,7 +273,7 @@ __global__ __launch_bounds__(NW * KW * 64) void gemv_coop_kernel(
     __syncthreads();
   }
   float* red = reinterpret_cast<float*>(smem);  // [TG][MR][16]
-  if (SK == 1) {
+  if (SK == 1 || EPI == EPI_PARTIAL) {  // EPI_PARTIAL: every split stores its own fp32 tile
     if (kg == 0)
 #pragma unroll
     for (int rb = 0; rb < MB; ++rb)
@@ -345,6 +361,11 @@ __global__ __launch_bounds__(NW * KW * 64) void gemv_coop_kernel(
     }
     if (tid == 0) __hip_atomic_store(&counters[g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  if constexpr (LSA_COOP_ABLATE == 2) {
+    __syncthreads();
+    if (red[tid] == 1.2345f) ep.out[tid] = 0;
+    return;
+  }
   if (EPI == EPI_ARGMAX)
     for (int r = tid; r < MR; r += NTHR) s_key[r] = 0ull;
   __syncthreads();
@@ -391,6 +412,12 @@ __global__ __launch_bounds__(NW * KW * 64) void gemv_coop_kernel(
     for (int e = tid; e < TG * MR; e += NTHR) {
       const int t = e / MR, mm = e % MR;
       if (mm >= M) continue;
+      if constexpr (LSA_COOP_ABLATE == 4) {
+        bf16_raw* o = ep.out + (size_t)mm * ep.ldo + (ntg0 + t) * 16;
+        st16(o, u32x4_t{0u, 0u, 0u, 0u});
+        st16(o + 8, u32x4_t{0u, 0u, 0u, 0u});
+        continue;
+      }
       const float r = rstd(mm);
       const int c0 = (ntg0 + t) * 16;
       float v[16];
@@ -398,6 +425,17 @@ __global__ __launch_bounds__(NW * KW * 64) void gemv_coop_kernel(
       if (EPI == EPI_ARGMAX) {
         epi_bias16(ep, c0, v);
         atomicMax(&s_key[mm], argmax_key16(v, (unsigned)(c0 + ep.col_offset)));
+      } else if constexpr (EPI == EPI_PARTIAL) {
+        // fp32 partial of split s at ((float*)out)[s][M][ldo] (lsa_resid_rmsnorm_partials adds
+        // the splits to the residual stream in fixed order)
+        float* po = reinterpret_cast<float*>(ep.out) + ((size_t)s * M + mm) * ep.ldo + c0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) *reinterpret_cast<f32x4_t*>(po + 4 * q) = f32x4_t{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
+      } else if constexpr (LSA_COOP_ABLATE == 3) {
+        float t = 0.f;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) t += v[j];
+        if (t == 1.2345f) ep.out[mm] = 0;
       } else {
         epi_row16<EPI>(ep, mm, c0, v);
       }
@@ -475,6 +513,7 @@ int coop_entry(const void* x, int ldx, const int* a_rows, const void* wp, int M,
     case EPI_SWIGLU: return LSA_D(EPI_SWIGLU);
     case EPI_QKV: return LSA_D(EPI_QKV);
     case EPI_ARGMAX: return LSA_D(EPI_ARGMAX);
+    case EPI_PARTIAL: return LSA_D(EPI_PARTIAL);
     default: return LSA_UNSUPPORTED;
   }
 #undef LSA_D
@@ -483,7 +522,9 @@ int coop_entry(const void* x, int ldx, const int* a_rows, const void* wp, int M,
 }  // namespace
 
 // K is split into 32*kf-k chunks, spread over the SK splits as evenly as possible; each split
-// over kw k-groups of nw waves (kw > 1: (K/(32*kf)) % (sk*kw) == 0).
+// over kw k-groups of nw waves (kw > 1: (K/(32*kf)) % (sk*kw) == 0). EPI_PARTIAL: no in-kernel
+// split reduction - split s stores its fp32 tile to ((float*)ep->out)[s][M][ldo] for
+// lsa_resid_rmsnorm_partials.
 // Workspace: slab >= SK*N*16*MB*4 + SK*(N/16/(nw*tnw))*16*MB*4 bytes (only when SK > 1);
 // counters: N/16/(nw*tnw) zero-initialised uint32 (reset by the kernel itself).
 extern "C" int lsa_gemv_coop(const void* x, int ldx, const int* a_rows, const void* wp, int M, int N, int K, int norm, float eps,

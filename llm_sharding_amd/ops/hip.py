@@ -170,13 +170,15 @@ def _check_epi(epi: int, ep: EpiArgs, N: int) -> None:
 def gemv(x: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep: EpiArgs,
          norm: bool = False, eps: float = 1e-5, a_rows: Optional[torch.Tensor] = None,
          tn: int = 0, nw: int = 0, u: int = 0, coop: Optional[tuple] = None,
-         ws: Optional[CoopWorkspace] = None) -> None:
+         ws: Optional[CoopWorkspace] = None, out_numel: int = 0) -> None:
     """Decode / short-prefill projection, M <= 128 rows (> 64: coop kernel only). ``wp`` is ``pack_b(W)`` (``pack_b(fold_norm(W, g))``
     when ``norm``: RMSNorm of the A rows is then applied in-kernel), W: [N, K].
 
     Kernel choice: explicit ``tn/nw/u`` -> streaming GEMV (gemv.hip); explicit
     ``coop=(tnw, nw, kf, sk[, kw])`` -> cooperative split-K (gemv_coop.hip); neither -> the tuned
-    choice of :func:`packing.proj_config`."""
+    choice of :func:`packing.proj_config`. EPI_PARTIAL (coop only): split s writes its fp32 tile
+    to ``ep.out`` viewed as [sk][M][ldo] (``out_numel`` = its capacity in floats, checked) for
+    :func:`resid_rmsnorm_partials`."""
     from .packing import GEMV_CONFIGS, coop_candidates, coop_slab_floats, proj_config, row_blocks
     _req(1 <= M <= 128, f"gemv supports 1..128 rows, got {M}")
     _check_epi(epi, ep, N)
@@ -193,9 +195,13 @@ def gemv(x: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep
             coop = cfg
         else:
             tn, nw, u = cfg
+    _req(epi != EPI_PARTIAL or coop is not None, "gemv: EPI_PARTIAL needs an explicit coop config")
     if coop is not None:
         coop = tuple(coop) if len(coop) == 5 else tuple(coop) + (1,)
         tnw, cnw, kf, sk, kw = coop
+        if epi == EPI_PARTIAL:
+            _req(out_numel >= sk * M * ep.ldo, f"gemv partial: output holds {out_numel} floats, "
+                 f"{sk} splits x {M} rows x ldo {ep.ldo} needed")
         _req(coop in coop_candidates(N // 16, K, M), f"gemv: coop config {coop} invalid for N={N} K={K} M={M}")
         if ws is None:
             ws = default_workspace(x.device)

@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import json
 import os
+from typing import Optional
 
 import torch
 
@@ -252,12 +253,25 @@ def _tuned() -> dict:
                 for e in json.load(f).get("entries", []):
                     if e.get("algo") in ("fp8", "coop_fp8"):
                         _TUNED[(e["N"], e["K"], e["mb"], bool(e["even"]), "fp8")] = (e["algo"], tuple(e["cfg"]))
+                    elif e.get("algo") == "coop_partial":
+                        _TUNED[(e["N"], e["K"], e["mb"], False, "partial")] = (e["algo"], tuple(e["cfg"]))
                     else:
                         cfg = tuple(e["cfg"])
                         if e.get("algo") == "coop" and len(cfg) == 4:
                             cfg = cfg + (1,)  # tables written before k-groups existed
                         _TUNED[(e["N"], e["K"], e["mb"], bool(e["even"]))] = (e.get("algo", "gemv"), cfg)
     return _TUNED
+
+
+def partial_config(n_tiles: int, rows: int, k: int = 4096) -> Optional[tuple]:
+    """(tnw, nw, kf, sk, kw) when a residual decode projection of ``rows`` rows is measured
+    faster as coop EPI_PARTIAL (splits store fp32 tiles) + lsa_resid_rmsnorm_partials than with
+    the in-kernel split reduction + residual epilogue (scripts/tune_coop_partial.py), else None."""
+    t = _tuned().get((n_tiles * 16, k, row_blocks(rows), False, "partial"))
+    if t is None or rows <= 16:
+        return None
+    cfg = tuple(t[1])
+    return cfg if cfg in coop_candidates(n_tiles, k, rows) and cfg[3] <= 8 else None
 
 
 def proj_config(n_tiles: int, rows: int, need_even: bool = False, k: int = 4096) -> tuple:

@@ -656,6 +656,19 @@ class StageEngine:
             else:
                 hip.gemv(x, wbf(w, s, N, K), rows, N, K, epi, ep, norm=norm, eps=eps, ws=ws)
 
+        def dec_resid(x, w, s, N, K, ep):
+            # 17..128 rows: split-K partials + one residual-add kernel where measured faster than
+            # the coop kernel's in-kernel split reduction (ops/gemv_tuning.json "coop_partial")
+            pc = None if (native_fp8 or s is not None or cfg.is_gpt2 or N not in (2048, 4096, 6144, 8192)) \
+                else packing.partial_config(N // 16, rows, k=K)
+            if pc is None or ws.slab.numel() < pc[3] * rows * N:
+                dec(x, w, s, N, K, hip.EPI_RESID, ep)
+                return
+            part = ws.slab[:pc[3] * rows * N].view(pc[3], rows, N)
+            hip.gemv(x, w, rows, N, K, hip.EPI_PARTIAL, hip.make_epi(out=part, ldo=N), coop=pc, ws=ws,
+                     out_numel=part.numel())
+            hip.resid_rmsnorm_partials(hbuf, part, pc[3], rows, eps)
+
         def pre(x, w, s, N, K, epi, ep):
             hip.gemm(x, wbf(w, s, N, K), rows, N, K, epi, ep, ws=ws, sk_ws=self.sk_ws)
 
@@ -716,9 +729,9 @@ class StageEngine:
             ep_o = hip.make_epi(out=hbuf, resid=hbuf, ldo=hbuf.stride(0), ldr=hbuf.stride(0))
             ep_gu = hip.make_epi(out=act, ldo=act.stride(0))
             if decode:
-                dec(attn_o, lw.o, lw.o_s, H, cfg.q_size, hip.EPI_RESID, ep_o)
+                dec_resid(attn_o, lw.o, lw.o_s, H, cfg.q_size, ep_o)
                 dec(hbuf, lw.gate_up, lw.gate_up_s, 2 * I, H, hip.EPI_SWIGLU, ep_gu, norm=True)
-                dec(act, lw.down, lw.down_s, H, I, hip.EPI_RESID, ep_o)
+                dec_resid(act, lw.down, lw.down_s, H, I, ep_o)
             else:
                 ep_r = hip.make_epi(out=hbuf, resid=hbuf, ldo=hbuf.stride(0), ldr=hbuf.stride(0), ss_out=ss) \
                     if fuse else ep_o

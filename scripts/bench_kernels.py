@@ -194,6 +194,8 @@ def main():
                     key = (e["N"], e["K"], e["mb"], bool(e["even"]))
                     if e.get("algo") in ("fp8", "coop_fp8"):
                         key = key + ("fp8",)
+                    elif e.get("algo") == "coop_partial":
+                        key = key + ("partial",)
                     old[key] = (e.get("algo", "gemv"), e["cfg"])
             old.update(tune)
             ents = [{"N": k[0], "K": k[1], "mb": k[2], "even": k[3], "algo": v[0], "cfg": v[1]}

@@ -106,6 +106,20 @@ def test_big_batch_decode_graph_vs_golden(rows, partial):
             _big_batch_vs_golden(rows)
 
 
+@pytest.mark.parametrize("rows", [40, 100])
+def test_decode_coop_partials_vs_golden(rows, monkeypatch):
+    """17..128-row decode with the residual projections as coop EPI_PARTIAL +
+    resid_rmsnorm_partials (packing.partial_config forced to a 4-split config) against the fp32
+    golden model, captured in a decode graph."""
+    from llm_sharding_amd.ops import packing
+
+    def forced(n_tiles, r, k=4096):
+        c = [c for c in packing.coop_candidates(n_tiles, k, r) if c[3] == 4]
+        return c[0] if c else None
+    monkeypatch.setattr(packing, "partial_config", forced)
+    _big_batch_vs_golden(rows)
+
+
 def _big_batch_vs_golden(rows):
     cfg = _mid_cfg()
     seed, P = 13, 5

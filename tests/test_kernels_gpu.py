@@ -119,6 +119,35 @@ def test_gemv_coop_every_config(cfg):
     assert tested > 0, cfg
 
 
+@pytest.mark.parametrize("M", [17, 40, 64, 100, 128])
+@pytest.mark.parametrize("N,K", [(4096, 4096), (4096, 11008)])
+def test_gemv_coop_partials_resid(M, N, K):
+    """coop EPI_PARTIAL (each split stores its fp32 tile, no in-kernel reduction) followed by
+    lsa_resid_rmsnorm_partials == resid + x @ W^T, for every coop config with <= 8 splits."""
+    h = hip()
+    x = _rnd(M, K)
+    w = _rnd(N, K, scale=0.02)
+    wp = packing.pack_b(w)
+    resid = _rnd(M, N)
+    ref = resid.float() + x.float() @ w.float().T
+    ws = h.CoopWorkspace(DEV, slab_floats=1 << 23)
+    part = torch.empty(8 * M * N, dtype=torch.float32, device=DEV)
+    tested = 0
+    for c in packing.coop_candidates(N // 16, K, M):
+        if c[3] > 8:
+            continue
+        out = resid.clone()
+        p3 = part[:c[3] * M * N].view(c[3], M, N)
+        h.gemv(x, wp, M, N, K, h.EPI_PARTIAL, h.make_epi(out=p3, ldo=N), coop=c, ws=ws, out_numel=p3.numel())
+        h.resid_rmsnorm_partials(out, p3, c[3], M, 1e-5)
+        assert rel_err(out, ref) < 8e-3, c
+        tested += 1
+    assert tested > 0
+    with pytest.raises(Exception):  # the capacity check runs before the launch
+        h.gemv(x, wp, M, N, K, h.EPI_PARTIAL, h.make_epi(out=part, ldo=N), coop=(1, 4, 4, 8, 1), ws=ws,
+               out_numel=M * N)
+
+
 @pytest.mark.parametrize("M", [20, 64])
 def test_gemv_coop_swiglu_argmax_graph(M):
     """SwiGLU and argmax epilogues through the coop kernel, replayed in a hipGraph (the
