@@ -236,7 +236,11 @@ class NodeWorker:
         last = self.end == self.layer_num
         g = self._graphs.get(B)
         if g is None:
-            g = DecodeGraph(eng, B, "last" if last else "mid").capture()
+            # captured outside inference mode: the graph's own tensors (and the CUDA generator's
+            # graph-safe RNG state, created at the process's first capture) stay normal tensors
+            # that later captures elsewhere may update in place
+            with torch.inference_mode(False):
+                g = DecodeGraph(eng, B, "last" if last else "mid").capture()
             self._graphs[B] = g
             self._graph_pos[B] = None
         want = [int(eng.seq_len[r]) for r in range(B)]
