@@ -64,6 +64,9 @@ def parse():
     ap.add_argument("--latency-steps", type=int, default=32,
                     help="after the throughput pass, time this many batch-1 decode steps through the same "
                          "pipeline (b1_p50_tpot_ms / b1_tok_s in the JSON line); 0 = skip")
+    ap.add_argument("--mid-batch", type=int, default=128,
+                    help="after the batch-1 pass, time --latency-steps decode steps of this many sequences "
+                         "(<= 128, the fused-GEMV regime; mid_p50_tpot_ms / mid_tok_s); 0 = skip")
     ap.add_argument("--stage-layers", type=int, default=0,
                     help="profile one pipeline stage: the model cut to this many layers (NOT the headline metric)")
     ap.add_argument("--transport", default="rccl", choices=("rccl", "ipc"),
@@ -132,7 +135,7 @@ def main():
                                microbatches=a.microbatches, seed=a.seed, use_graph=not a.no_graph,
                                weight_dtype=a.weight_dtype, streams=a.streams, dp=a.dp,
                                latency_steps=a.latency_steps, device=a.device, stage_layers=a.stage_layers,
-                               transport=a.transport)
+                               transport=a.transport, mid_batch=a.mid_batch)
     if res is None:  # non-zero ranks
         return
     line = {
@@ -160,6 +163,9 @@ def main():
         "ttft_ms": round(res["ttft_ms"], 3),
         "b1_p50_tpot_ms": None if res["b1_p50_tpot_ms"] is None else round(res["b1_p50_tpot_ms"], 4),
         "b1_tok_s": None if res["b1_tok_s"] is None else round(res["b1_tok_s"], 2),
+        "mid_batch": res["mid_batch"],
+        "mid_p50_tpot_ms": None if res["mid_p50_tpot_ms"] is None else round(res["mid_p50_tpot_ms"], 4),
+        "mid_tok_s": None if res["mid_tok_s"] is None else round(res["mid_tok_s"], 2),
         "mem_pred_gb": res["mem_pred_gb"], "mem_peak_gb": res["mem_peak_gb"],
         "reference_anecdote_tok_s": BASELINE_TOK_S,
     }

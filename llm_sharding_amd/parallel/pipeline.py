@@ -551,16 +551,17 @@ def _tpot_from_events(events: list) -> list:
 
 
 def _latency_pass(cfg, stage: "PipelineStage", srank: int, pp: int, st, dev, max_seq: int, prompts,
-                  prompt_len: int, steps: int, dist, sync, p2p) -> tuple:
-    """Batch-1 decode through the pipeline on the already loaded stage engine (KV slot 0 is
-    reused): prefill one prompt, LAT_WARMUP untimed steps, ``steps`` timed ones. Returns (p50
-    per-token latency in ms on the last stage - 0.0 elsewhere -, timed wall seconds)."""
+                  prompt_len: int, steps: int, dist, sync, p2p, rows: int = 1) -> tuple:
+    """Batch-``rows`` decode through the pipeline on the already loaded stage engine (KV slots
+    0..rows-1 are reused): prefill ``rows`` prompts, LAT_WARMUP untimed steps, ``steps`` timed
+    ones. Returns (p50 per-token latency in ms on the last stage - 0.0 elsewhere -, timed wall
+    seconds)."""
     eng = stage.eng
-    eng.reset([0])
-    b1 = PipelineStage(cfg, srank, pp, st.start, st.end, dev, 1, 1, max_seq, None,
+    eng.reset(list(range(rows)))
+    b1 = PipelineStage(cfg, srank, pp, st.start, st.end, dev, rows, 1, max_seq, None,
                        use_graph=stage.use_graph, dtype=stage.dtype, p2p=p2p, engine=eng)
     b1.tl = stage.tl
-    p1 = prompts[:1, :1].contiguous() if prompts is not None else None
+    p1 = prompts[:1, :rows].contiguous() if prompts is not None else None
     firsts = b1.prefill(p1, prompt_len)
     b1.build_graphs(firsts, history_len=LAT_WARMUP + steps)
     for s in range(LAT_WARMUP):
@@ -589,7 +590,7 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
                          microbatches: int = 0, seed: int = 0, use_graph: bool = True,
                          verbose: bool = True, weight_dtype: str = "bf16", streams: int = 1,
                          device: str = "cuda", dp: int = 1, latency_steps: int = 0,
-                         stage_layers: int = 0, transport: str = "rccl") -> Optional[dict]:
+                         stage_layers: int = 0, transport: str = "rccl", mid_batch: int = 0) -> Optional[dict]:
     """``microbatches`` 0 = ``streams`` x stages (every GPU holds ``streams`` micro-batches of
     ``batch`` sequences: weak scaling); ``max_seq`` 0 = what the run needs, rounded up to 64.
 
@@ -599,6 +600,10 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
     rank's time). The pipelines share no communicator, so a replica's ring stays on its own
     xGMI links (adjacent ranks) and a 7B model fits one GPU many times over: dp8 trades the
     pipeline's per-token latency for none of its bubbles.
+
+    ``mid_batch`` > 0: after the batch-1 pass, the same latency pass with ``mid_batch`` sequences
+    (<= 128: the fused-GEMV decode regime of a latency-oriented serving batch or a pipeline
+    micro-batch) -> ``mid_p50_tpot_ms`` / ``mid_tok_s``.
 
     ``stage_layers`` > 0: a STAGE PROFILE, not the headline number - the model's architecture
     cut to that many decoder layers (embedding and lm_head kept), e.g. one 10-layer stage of
@@ -739,13 +744,18 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
     if latency_steps > 0:
         lat_p50, lat_el = _latency_pass(cfg, stage, srank, pp, st, dev, max_seq, prompts, prompt_len,
                                         latency_steps, dist, sync, p2p)
+    mid_p50 = mid_el = 0.0
+    mid_batch = mid_batch if 0 < mid_batch <= min(batch, 128) else 0
+    if mid_batch and latency_steps > 0:
+        mid_p50, mid_el = _latency_pass(cfg, stage, srank, pp, st, dev, max_seq, prompts, prompt_len,
+                                        latency_steps, dist, sync, p2p, rows=mid_batch)
     mem_peak = float(torch.cuda.max_memory_allocated(dev)) if gpu else 0.0
     chk = getattr(p2p, "check", None)
     if chk is not None:
         chk()  # a timed-out IPC hand-off ends the run with an error, never with poisoned tokens
     stats = torch.tensor([elapsed, ttft_ms, _percentile(tpot, 0.5) if tpot else 0.0,
                           _percentile(tpot, 0.9) if tpot else 0.0, load_s, lat_el, lat_p50,
-                          mem_pred["total"], mem_peak], dtype=torch.float64,
+                          mem_pred["total"], mem_peak, mid_el, mid_p50], dtype=torch.float64,
                          device="cpu" if ipc_only else dev)  # gloo gathers host tensors
     if not gpu and stage.last:  # no device events on CPU: wall-clock step time stands in for TPOT
         stats[2] = stats[3] = elapsed * 1e3 / steps
@@ -759,12 +769,15 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
         load_s = float(allst[:, 4].max())
         lat_el, lat_p50 = float(allst[:, 5].max()), float(allst[pp - 1, 6])
         mem_pred_max, mem_peak_max = float(allst[:, 7].max()), float(allst[:, 8].max())
+        mid_el, mid_p50 = float(allst[:, 9].max()), float(allst[pp - 1, 10])
     else:
         mem_pred_max, mem_peak_max = float(stats[7]), float(stats[8])
         p50, p90 = float(stats[2]), float(stats[3])
         lat_el, lat_p50 = float(stats[5]), float(stats[6])
+        mid_el, mid_p50 = float(stats[9]), float(stats[10])
     if latency_steps > 0 and not gpu:
         lat_p50 = lat_el * 1e3 / latency_steps
+        mid_p50 = mid_el * 1e3 / latency_steps if mid_batch else 0.0
     tokens = dp * steps * M * batch
     res = {
         "tok_s": tokens / elapsed,
@@ -786,6 +799,10 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
         "transport": transport if pp > 1 else None,
         "b1_p50_tpot_ms": lat_p50 if latency_steps > 0 else None,
         "b1_tok_s": (dp * latency_steps / lat_el) if latency_steps > 0 and lat_el > 0 else None,
+        "mid_batch": mid_batch or None,
+        "mid_p50_tpot_ms": mid_p50 if mid_batch and latency_steps > 0 else None,
+        "mid_tok_s": (dp * mid_batch * latency_steps / mid_el) if mid_batch and latency_steps > 0 and mid_el > 0
+        else None,
         # max over ranks: the memory model's stage bytes and torch's measured peak allocation
         "mem_pred_gb": round(mem_pred_max / 1e9, 2),
         "mem_peak_gb": round(mem_peak_max / 1e9, 2) if gpu else None,
