@@ -176,7 +176,13 @@ class IpcRingP2P:
         cur, cs = torch.cuda.current_stream(self.dev), self.streams[e]
         cs.wait_stream(cur)
         L = _lib()
-        for off, nb in self._chunks(n):
+        chunks = self._chunks(n)
+        # a message of more chunks than slots needs its receiver running concurrently; the two
+        # streams of a loopback edge (one process) may share a hardware queue, so there the
+        # receive could sit behind a send that waits for it
+        hip._req(e[0] != e[1] or len(chunks) <= self.R,
+                 f"ipc ring: a loopback message may span at most {self.R} slots ({len(chunks)} needed)")
+        for off, nb in chunks:
             _ok(L.lsa_ipc_send(src.data_ptr() + off, nb, base + _FLAG_BYTES, self.slot_bytes, base, self.ackbox[e],
                                self.R, self._state(e, True), self.err.data_ptr(), self.timeout_us, self.grid,
                                cs.cuda_stream), "lsa_ipc_send")

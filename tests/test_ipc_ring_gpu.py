@@ -69,7 +69,7 @@ def test_ipc_ring_loopback_chunked_and_staged():
     """Loopback edge in one process: messages larger than a slot go as chunks, non-contiguous /
     misaligned tensors through a private copy; every byte arrives, in order, and no error."""
     import torch
-    ring = _loopback(slot_bytes=4096, slots=3, timeout_s=5.0)
+    ring = _loopback(slot_bytes=4096, slots=8, timeout_s=5.0)
     g = torch.Generator(device="cuda").manual_seed(0)
     msgs = [torch.randint(-2**31, 2**31 - 1, (n,), dtype=torch.int32, device="cuda", generator=g)
             for n in (1, 3, 1024, 1025, 5000, 3 * 1024)]
@@ -83,8 +83,12 @@ def test_ipc_ring_loopback_chunked_and_staged():
         w.wait()
         torch.cuda.synchronize()
         assert torch.equal(out, m), (m.shape, m.dtype)
+    # more chunks than slots on a loopback edge is refused up front (its receive could queue
+    # behind the send on a shared hardware queue)
+    with pytest.raises(Exception):
+        ring.isend(torch.zeros(9 * 1024, dtype=torch.int32, device="cuda"), 0)
     # a burst of R single-slot messages queued before any receive
-    burst = [torch.full((512,), i, dtype=torch.int32, device="cuda") for i in range(3)]
+    burst = [torch.full((512,), i, dtype=torch.int32, device="cuda") for i in range(8)]
     works = [ring.isend(m, 0) for m in burst]
     outs = [torch.zeros_like(m) for m in burst]
     for o in outs:
