@@ -23,6 +23,22 @@
 #define LSA_COOP_ABLATE 0
 #endif
 
+// Diagnostic build only (-DLSA_COOP_STAMPS, scripts/coop_stamps.py): per-workgroup
+// s_memrealtime stamps (100 MHz) at the phase boundaries, written by thread 0 to a buffer nothing
+// else reads: 0 start, 1 main loop done (wave 0), 2 all waves done, 3 k-group sum done, 4 slab
+// stored, 5 ticket drawn, 6 (last arriver) slabs summed, 7 tile in LDS, 8 epilogue done.
+#ifdef LSA_COOP_STAMPS
+__device__ unsigned long long* g_coop_stamps;
+#define LSA_CSTAMP(slot)                                                                                      \
+  do {                                                                                                       \
+    if (threadIdx.x == 0 && g_coop_stamps) g_coop_stamps[blockIdx.x * 16 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define LSA_CSTAMP(slot) \
+  do {                   \
+  } while (0)
+#endif
+
 namespace {
 
 // A tile [MR][KC] bf16 in LDS, 16-B chunks XOR-swizzled so that the 16 lanes of one
@@ -64,7 +80,8 @@ __global__ __launch_bounds__(NW * KW * 64) void gemv_coop_kernel(
   constexpr int TG = NW * TNW;                  // 16-col tiles per workgroup
   constexpr int ABUF = MR * KC * 2;             // bytes per A chunk of one k-group
   constexpr int ABUFT = KW * ABUF;              // bytes per A buffer (all k-groups)
-  constexpr int RED = TG * MR * 16 * 4;         // fp32 reduction tile
+  constexpr int RS = 20;                        // reduction tile row stride (floats): 16 + 4 pad
+  constexpr int RED = TG * MR * RS * 4;         // fp32 reduction tile [TG][MR][RS]
   constexpr int XRED = (KW - 1) * TG * MB * 64 * 16;  // k-group partials, fragment-native
   constexpr int SMEM0 = (2 * ABUFT > RED ? 2 * ABUFT : RED);
   constexpr int SMEM = (SMEM0 > XRED ? SMEM0 : XRED);
@@ -74,6 +91,7 @@ __global__ __launch_bounds__(NW * KW * 64) void gemv_coop_kernel(
   __shared__ unsigned long long s_key[MR];
 
   const int tid = threadIdx.x, lane = tid & 63;
+  LSA_CSTAMP(0);
   const int wt = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int w = wt % NW, kg = wt / NW;          // tile wave within the k-group, k-group
   const int KT = K >> 5;
@@ -242,7 +260,9 @@ __global__ __launch_bounds__(NW * KW * 64) void gemv_coop_kernel(
       for (int o = 1; o < C16; o <<= 1) ss[i] += __shfl_xor(ss[i], o, 64);
     }
   }
+  LSA_CSTAMP(1);
   __syncthreads();  // all waves done with the A buffers: smem becomes the reduction tile
+  LSA_CSTAMP(2);
   if constexpr (LSA_COOP_ABLATE == 1) {
     float t = 0.f;
 #pragma unroll
@@ -272,7 +292,8 @@ __global__ __launch_bounds__(NW * KW * 64) void gemv_coop_kernel(
     }
     __syncthreads();
   }
-  float* red = reinterpret_cast<float*>(smem);  // [TG][MR][16]
+  LSA_CSTAMP(3);
+  float* red = reinterpret_cast<float*>(smem);  // [TG][MR][RS]
   if (SK == 1 || EPI == EPI_PARTIAL) {  // EPI_PARTIAL: every split stores its own fp32 tile
     if (kg == 0)
 #pragma unroll
@@ -281,7 +302,7 @@ __global__ __launch_bounds__(NW * KW * 64) void gemv_coop_kernel(
       for (int t = 0; t < TNW; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          red[((w * TNW + t) * MR + rb * 16 + (lane >> 4) * 4 + r) * 16 + (lane & 15)] = acc[rb][t][r];
+          red[((w * TNW + t) * MR + rb * 16 + (lane >> 4) * 4 + r) * RS + (lane & 15)] = acc[rb][t][r];
     if (NORM && ac16 == 0) {
 #pragma unroll
       for (int i = 0; i < LPT; ++i) s_ss[arow + i * RSTEP] = ss[i];
@@ -313,11 +334,13 @@ __global__ __launch_bounds__(NW * KW * 64) void gemv_coop_kernel(
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    LSA_CSTAMP(4);
     if (tid == 0) {
       const unsigned old = __hip_atomic_fetch_add(&counters[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       s_last = old == (unsigned)(SK - 1);
     }
     __syncthreads();
+    LSA_CSTAMP(5);
     if (!s_last) return;
     // Last arriver: sum the SK slabs in fixed split order (deterministic). The group's region
     // is one contiguous run of TG*MB*256 floats per split; every thread keeps E4 16-B loads x
@@ -349,7 +372,7 @@ __global__ __launch_bounds__(NW * KW * 64) void gemv_coop_kernel(
       const int u = j * NTHR + tid;
       const int tl = u / (MB * 64), rb = (u >> 6) % MB, ln = u & 63;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) red[(tl * MR + rb * 16 + (ln >> 4) * 4 + r) * 16 + (ln & 15)] = sum[j][r];
+      for (int r = 0; r < 4; ++r) red[(tl * MR + rb * 16 + (ln >> 4) * 4 + r) * RS + (ln & 15)] = sum[j][r];
     }
     if (NORM) {
       for (int r = tid; r < MR; r += NTHR) {  // NTHR may be < MR (single-wave workgroups)
@@ -359,6 +382,7 @@ __global__ __launch_bounds__(NW * KW * 64) void gemv_coop_kernel(
         s_ss[r] = t2;
       }
     }
+    LSA_CSTAMP(6);
     if (tid == 0) __hip_atomic_store(&counters[g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if constexpr (LSA_COOP_ABLATE == 2) {
@@ -370,16 +394,19 @@ __global__ __launch_bounds__(NW * KW * 64) void gemv_coop_kernel(
     for (int r = tid; r < MR; r += NTHR) s_key[r] = 0ull;
   __syncthreads();
 
+  LSA_CSTAMP(7);
   auto rstd = [&](int mm) -> float { return NORM ? rsqrtf(s_ss[mm] / (float)K + eps) : 1.f; };
   const int ntg0 = g * TG;
-  auto load16 = [&](int t, int mm, float r, float* v) {  // row-rotated quads (LDS banks)
-    const float* rp = red + (t * MR + mm) * 16;
+  // rows RS = 20 floats apart: the 16 rows one ds_read_b128 lane group reads start 20 banks
+  // apart (all 64 banks, conflict-free) with the quads in static order - a row-dependent quad
+  // rotation made v[] dynamically indexed (~1,200 v_cndmask per epilogue, 2.5-5.5 us per launch)
+  auto load16 = [&](int t, int mm, float r, float* v) {
+    const float* rp = red + (t * MR + mm) * RS;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int qq = (q + mm) & 3;
-      const f32x4_t x4 = *reinterpret_cast<const f32x4_t*>(rp + 4 * qq);
+      const f32x4_t x4 = *reinterpret_cast<const f32x4_t*>(rp + 4 * q);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v[4 * qq + j] = x4[j] * r;
+      for (int j = 0; j < 4; ++j) v[4 * q + j] = x4[j] * r;
     }
     if (FP8) {
       const float* sp = wscale + (ntg0 + t) * 16;
@@ -407,8 +434,7 @@ __global__ __launch_bounds__(NW * KW * 64) void gemv_coop_kernel(
       st16(o + 8, pack8(gg + 8));
     }
   } else {
-    // one thread per finished 16-column tile row (epilogue.h epi_row16); the 4 quad reads
-    // start at a row-rotated quad so neighbouring lanes hit different LDS banks
+    // one thread per finished 16-column tile row (epilogue.h epi_row16)
     for (int e = tid; e < TG * MR; e += NTHR) {
       const int t = e / MR, mm = e % MR;
       if (mm >= M) continue;
@@ -445,6 +471,7 @@ __global__ __launch_bounds__(NW * KW * 64) void gemv_coop_kernel(
       for (int r = tid; r < M; r += NTHR) atomicMax(&ep.keys[r], s_key[r]);
     }
   }
+  LSA_CSTAMP(8);
 }
 
 template <int MB, int TNW, int NW, int KF, int KW, int EPI, bool FP8>
@@ -533,6 +560,12 @@ extern "C" int lsa_gemv_coop(const void* x, int ldx, const int* a_rows, const vo
   return coop_entry<false>(x, ldx, a_rows, wp, M, N, K, norm, eps, epi, ep, tnw, nw, kf, sk, kw, slab, counters, nullptr,
                            stream);
 }
+
+#ifdef LSA_COOP_STAMPS
+extern "C" int lsa_coop_set_stamps(unsigned long long* buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_coop_stamps), &buf, sizeof(buf)) == hipSuccess ? LSA_OK : LSA_LAUNCH_FAILED;
+}
+#endif
 
 // Same with OCP fp8 e4m3 weights packed as in gemv_fp8.hip and fp32 per-row scales.
 extern "C" int lsa_gemv_coop_fp8(const void* x, int ldx, const int* a_rows, const void* wq, const float* wscale, int M,
