@@ -7,10 +7,12 @@ export TMPDIR=/tmp
 timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread -k "coop or gemv or qkv" \
     > gpurun_out/r3_epi_test.log 2>&1 || { tail -30 gpurun_out/r3_epi_test.log; exit 3; }
 tail -1 gpurun_out/r3_epi_test.log
-timeout -k 10 300 python scripts/coop_stamps.py 64 128 > gpurun_out/r3_coop_stamps2.txt 2>&1 || { tail -20 gpurun_out/r3_coop_stamps2.txt; exit 4; }
-grep -E "M=|tile|epi " gpurun_out/r3_coop_stamps2.txt
+if [ -f llm_sharding_amd/_native/liblsa_coop_stamps.so ]; then
+  timeout -k 10 300 python scripts/coop_stamps.py 64 128 > gpurun_out/r3_coop_stamps2.txt 2>&1 || { tail -20 gpurun_out/r3_coop_stamps2.txt; exit 4; }
+  grep -E "M=|tile|epi " gpurun_out/r3_coop_stamps2.txt
+fi
 cp llm_sharding_amd/ops/gemv_tuning.json gpurun_out/r3_gemv_tuning_epi.json
-timeout -k 10 600 python scripts/bench_kernels.py --only gemv --models llama2-7b --rows 32,64,128 --tune \
+timeout -k 10 600 python scripts/bench_kernels.py --only gemv --models llama2-7b --rows ${ROWS:-32,64,128} --tune \
     --tune-file gpurun_out/r3_gemv_tuning_epi.json --out gpurun_out/r3_epi_sweep.json > gpurun_out/r3_epi_sweep.jsonl 2>&1 \
     || { tail -20 gpurun_out/r3_epi_sweep.jsonl; exit 5; }
 python - << 'PY'
