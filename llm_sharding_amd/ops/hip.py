@@ -73,10 +73,11 @@ def lib() -> ctypes.CDLL:
     L.lsa_row_ss.argtypes = [vp, i, i, i, vp, vp]
     L.lsa_argmax_finalize.argtypes = [vp, i, vp, vp, i, vp, i, i, vp, vp]
     L.lsa_pos_advance.argtypes = [vp, i, i, vp]
+    L.lsa_gemm_wr.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(EpiArgs), i, i, vp]
     L.lsa_gemm_sk.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(EpiArgs), i, i, i, i, i, i, i, vp, vp, ctypes.c_longlong, i,
                               i, vp]
     for name in ("lsa_gemv", "lsa_gemv_coop", "lsa_gemv_fp8", "lsa_dequant_fp8_packed", "lsa_gemv_coop_fp8", "lsa_gemm",
-                 "lsa_gemm_sk", "lsa_attn_decode", "lsa_attn_prefill", "lsa_embed", "lsa_rmsnorm", "lsa_layernorm",
+                 "lsa_gemm_sk", "lsa_gemm_wr", "lsa_attn_decode", "lsa_attn_prefill", "lsa_embed", "lsa_rmsnorm", "lsa_layernorm",
                  "lsa_resid_rmsnorm_partials", "lsa_row_ss",
                  "lsa_argmax_finalize", "lsa_pos_advance", "lsa_version"):
         getattr(L, name).restype = ctypes.c_int
@@ -308,7 +309,11 @@ def gemm(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep
     ``sk`` its split-K factor (0 = :func:`gemm_split`; > 1 uses ``ws``)."""
     if not legacy and N % 128 == 0 and K % 64 == 0 and epi != EPI_ARGMAX and a.stride(0) % 8 == 0 \
             and a.data_ptr() % 16 == 0:
-        gemm_sk(a, wp, M, N, K, epi, ep, ws=sk_ws)
+        bn = gemm_wr_plan(M, N, K, epi, ep)
+        if bn:
+            gemm_wr(a, wp, M, N, K, epi, ep, bn=bn)
+        else:
+            gemm_sk(a, wp, M, N, K, epi, ep, ws=sk_ws)
         return
     _req(not (ep.ss_out or ep.ss_in), "gemm: the fused-norm epilogue fields need the gemm_sk path")
     _req(_is_bf16_cuda(a, wp), "gemm: bf16 cuda tensors required")
@@ -338,6 +343,37 @@ def gemm(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep
 
 
 SK_BM = 256  # gemm_sk.hip row tile (default; 128-row tiles for small / odd M: plan field bm)
+
+# gemm_wr.hip (weights streamed into MFMA registers, 128 x bn tiles, one round of whole-K tiles)
+# where it measured faster than gemm_sk's best plan: one round of 224-256 whole 128 x 192 tiles,
+# i.e. the 7B qkv projection at 449-512 rows (54-55 us vs 68-81 us, profiles/r3_gemm_wr.md).
+# LSA_GEMM_WR=0 turns it off (A/B runs).
+WR_TILES = (224, 256)
+
+
+def gemm_wr_plan(M: int, N: int, K: int, epi: int, ep: "EpiArgs") -> int:
+    """bn for :func:`gemm_wr`, or 0 when gemm_sk takes the shape."""
+    if os.environ.get("LSA_GEMM_WR", "1") == "0" or epi not in (EPI_STORE, EPI_QKV) or ep.ss_out or ep.act \
+            or ep.bias or K % 256 or N % 192:
+        return 0
+    tiles = -(-M // 128) * (N // 192)
+    return 192 if WR_TILES[0] <= tiles <= WR_TILES[1] else 0
+
+
+def gemm_wr(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep: EpiArgs, bn: int = 192,
+            grid: int = 0) -> None:
+    """Projection GEMM with the weights fetched straight into MFMA B registers (gemm_wr.hip):
+    128 x ``bn`` tiles, one per workgroup per round, A staged by LDS-DMA, EPI_STORE / EPI_QKV
+    (with the fused RMSNorm row scale, ``ep.ss_in``). K % 256 == 0, N % bn == 0."""
+    _req(_is_bf16_cuda(a, wp), "gemm_wr: bf16 cuda tensors required")
+    _req(wp.numel() == N * K and K % 256 == 0, "gemm_wr: packed weight shape (K % 256 == 0)")
+    _req(a.dim() == 2 and a.shape[0] >= M >= 1 and a.shape[1] >= K and a.stride(1) == 1 and a.stride(0) % 8 == 0
+         and a.data_ptr() % 16 == 0, "gemm_wr: A must be [>=M, >=K] row-major with 16-B aligned rows")
+    _req(bn in (128, 192, 256) and N % bn == 0, f"gemm_wr: N={N} does not tile by bn={bn}")
+    _req(epi in (EPI_STORE, EPI_QKV) and not ep.ss_out, "gemm_wr: EPI_STORE / EPI_QKV only")
+    _check_epi(epi, ep, N)
+    rc = lib().lsa_gemm_wr(_p(a), a.stride(0), _p(wp), M, N, K, epi, ctypes.byref(ep), bn, grid or N_CU, _stream())
+    _check(rc, "lsa_gemm_wr")
 
 
 class SkWorkspace:
