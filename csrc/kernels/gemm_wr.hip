@@ -74,7 +74,7 @@ struct WrGeo {
 template <int FN, int EPI>
 LSA_DEVICE void gemm_wr_body(unsigned char* smem, const bf16_raw* __restrict__ A, int lda,
                              const bf16_raw* __restrict__ Wp, int M, int N, int K, const EpiArgs& ep, int MT,
-                             int NT) {
+                             int NT, int S) {
   using G_ = WrGeo<FN>;
   constexpr int TN = G_::TN, BN = G_::BN, NS = G_::NS, ADMA = G_::ADMA, PER = G_::PER;
   const int lane = threadIdx.x & 63;
@@ -85,14 +85,19 @@ LSA_DEVICE void gemm_wr_body(unsigned char* smem, const bf16_raw* __restrict__ A
     const int hw = blockIdx.x, q = G / 8, r = G % 8, x = hw % 8;
     g = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + hw / 8;
   }
-  const int nsteps = K / WR_BK, KT32 = K >> 5;
+  const int n4 = K / (NS * WR_BK), KT32 = K >> 5;  // K in groups of NS 64-deep steps
   // A fragment read offsets inside one ring buffer (row lane%16 of a 16-row tile, 16-B chunk
   // kf*4 + lane/16 stored at chunk ^ (row % 8))
   const unsigned roff0 = (lane & 15) * 128 + (((lane >> 4) ^ (lane & 7)) * 16);
   const unsigned roff1 = (lane & 15) * 128 + (((4 + (lane >> 4)) ^ (lane & 7)) * 16);
 
-  for (int tile = g; tile < MT * NT; tile += G) {
+  // work item = (tile, K split sp): row tiles fastest, then column tiles, then splits (the items
+  // running together share weight panels and K offsets); split sp covers the 64-deep steps
+  // [k0, k1), both multiples of NS. S == 1 unless EPI_PARTIAL.
+  for (int item = g; item < MT * NT * S; item += G) {
+    const int tile = item % (MT * NT), sp = item / (MT * NT);
     const int mt = tile % MT, nt = tile / MT;
+    const int k0 = (sp * n4 / S) * NS, nsteps = ((sp + 1) * n4 / S) * NS;  // steps [k0, nsteps)
     const int m0 = mt * WR_BM, n16 = (nt * BN + w * TN) >> 4;  // this wave's first 16-col tile
     // A DMA: wave w fills blocks w*ADMA + s (8 rows x 128 B each) of every ring buffer
     unsigned aoff[ADMA];
@@ -137,17 +142,17 @@ LSA_DEVICE void gemm_wr_body(unsigned char* smem, const bf16_raw* __restrict__ A
     // prologue: steps 0 .. NS-2 in flight (per step: W then A), A(0) kf0 frags read
     static_assert(NS == 4, "prologue issues steps 0, 1, 2");
 #pragma unroll
-    for (int v = 0; v < 2 * FN; ++v) wload(wr[0], v, 0);
+    for (int v = 0; v < 2 * FN; ++v) wload(wr[0], v, k0);
 #pragma unroll
-    for (int s = 0; s < ADMA; ++s) aload(0, s, 0);
+    for (int s = 0; s < ADMA; ++s) aload(0, s, k0);
 #pragma unroll
-    for (int v = 0; v < 2 * FN; ++v) wload(wr[1], v, min(1, nsteps - 1));
+    for (int v = 0; v < 2 * FN; ++v) wload(wr[1], v, min(k0 + 1, nsteps - 1));
 #pragma unroll
-    for (int s = 0; s < ADMA; ++s) aload(1, s, min(1, nsteps - 1));
+    for (int s = 0; s < ADMA; ++s) aload(1, s, min(k0 + 1, nsteps - 1));
 #pragma unroll
-    for (int v = 0; v < 2 * FN; ++v) wload(wr[2], v, min(2, nsteps - 1));
+    for (int v = 0; v < 2 * FN; ++v) wload(wr[2], v, min(k0 + 2, nsteps - 1));
 #pragma unroll
-    for (int s = 0; s < ADMA; ++s) aload(2, s, min(2, nsteps - 1));
+    for (int s = 0; s < ADMA; ++s) aload(2, s, min(k0 + 2, nsteps - 1));
     wr_vm_wait<(NS - 2) * PER>();
     wr_barrier();
 #pragma unroll
@@ -186,7 +191,7 @@ LSA_DEVICE void gemm_wr_body(unsigned char* smem, const bf16_raw* __restrict__ A
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       }
     };
-    for (int t = 0; t < nsteps; t += NS) {  // nsteps % NS == 0 (launcher)
+    for (int t = k0; t < nsteps; t += NS) {  // k0, nsteps multiples of NS
       step(t, std::integral_constant<int, 0>{});
       step(t + 1, std::integral_constant<int, 1>{});
       step(t + 2, std::integral_constant<int, 2>{});
@@ -240,7 +245,13 @@ LSA_DEVICE void gemm_wr_body(unsigned char* smem, const bf16_raw* __restrict__ A
 #pragma unroll
           for (int q = 0; q < 16; ++q) v[q] *= rsc;
         }
-        epi_row16<EPI>(ep, m, col_base + j * 16, v);
+        if (EPI == EPI_PARTIAL) {  // fp32 partial of split sp: ((float*)out)[sp][M][ldo]
+          float* o = reinterpret_cast<float*>(ep.out) + ((size_t)sp * M + m) * ep.ldo + col_base + j * 16;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) st16(o + 4 * q, __builtin_bit_cast(u32x4_t, *reinterpret_cast<const f32x4_t*>(v + 4 * q)));
+        } else {
+          epi_row16<EPI>(ep, m, col_base + j * 16, v);
+        }
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -251,18 +262,18 @@ LSA_DEVICE void gemm_wr_body(unsigned char* smem, const bf16_raw* __restrict__ A
 template <int FN, int EPI>
 __global__ __launch_bounds__(WR_NTHR) void gemm_wr_kernel(const bf16_raw* __restrict__ A, int lda,
                                                           const bf16_raw* __restrict__ Wp, int M, int N, int K,
-                                                          EpiArgs ep, int MT, int NT) {
+                                                          EpiArgs ep, int MT, int NT, int S) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[WrGeo<FN>::SMEM];
-  gemm_wr_body<FN, EPI>(smem, A, lda, Wp, M, N, K, ep, MT, NT);
+  gemm_wr_body<FN, EPI>(smem, A, lda, Wp, M, N, K, ep, MT, NT, S);
 }
 
 template <int FN, int EPI>
 int wr_launch(const bf16_raw* A, int lda, const bf16_raw* W, int M, int N, int K, const EpiArgs& ep, int grid,
-              hipStream_t s) {
+              int split, hipStream_t s) {
   constexpr int BN = WrGeo<FN>::BN;
   const int MT = (M + WR_BM - 1) / WR_BM, NT = N / BN;
-  const int tiles = MT * NT;
-  gemm_wr_kernel<FN, EPI><<<grid < tiles ? grid : tiles, WR_NTHR, 0, s>>>(A, lda, W, M, N, K, ep, MT, NT);
+  const int items = MT * NT * split;
+  gemm_wr_kernel<FN, EPI><<<grid < items ? grid : items, WR_NTHR, 0, s>>>(A, lda, W, M, N, K, ep, MT, NT, split);
   LSA_CHECK_LAUNCH();
   return LSA_OK;
 }
@@ -270,24 +281,30 @@ int wr_launch(const bf16_raw* A, int lda, const bf16_raw* W, int M, int N, int K
 }  // namespace
 
 // 128-row x bn tiles, weights straight into MFMA registers (see the header comment). epi:
-// EPI_STORE or EPI_QKV (with the fused-RMSNorm row scale when ep->ss_in is set: K == 64 ss_n).
-// bn: 128 / 192 / 256 with N % bn == 0; K % 256 == 0; grid: workgroups (tiles beyond it loop).
-// Returns LSA_BAD_SHAPE on any shape the kernel's indexing cannot take.
+// EPI_STORE, EPI_QKV (with the fused-RMSNorm row scale when ep->ss_in is set: K == 64 ss_n) or
+// EPI_PARTIAL: every tile split into exactly `split` K ranges (multiples of 256), fp32 partial
+// k to ((float*)ep->out)[k][M][ldo] (lsa_resid_rmsnorm_partials sums them); the caller checks
+// the buffer holds split * M * ldo floats. bn: 128 / 192 / 256 with N % bn == 0; K % 256 == 0;
+// grid: workgroups (work items beyond it loop). Returns LSA_BAD_SHAPE on any shape the
+// kernel's indexing cannot take.
 extern "C" int lsa_gemm_wr(const void* a, int lda, const void* wp, int M, int N, int K, int epi, const EpiArgs* ep,
-                           int bn, int grid, hipStream_t stream) {
+                           int bn, int grid, int split, hipStream_t stream) {
   if (M < 1 || K < 4 * WR_BK || K % (4 * WR_BK) || lda < K || lda % 8 || grid < 1 || !ep) return LSA_BAD_SHAPE;
   if (bn != 128 && bn != 192 && bn != 256) return LSA_UNSUPPORTED;
   if (N % bn) return LSA_BAD_SHAPE;
-  if (epi != EPI_STORE && epi != EPI_QKV) return LSA_UNSUPPORTED;
+  if (epi != EPI_STORE && epi != EPI_QKV && epi != EPI_PARTIAL) return LSA_UNSUPPORTED;
+  if (split < 1 || (split > 1 && epi != EPI_PARTIAL) || split > K / (4 * WR_BK)) return LSA_BAD_SHAPE;
+  if (epi == EPI_PARTIAL && (!ep->out || ep->ldo < N || ep->ldo % 4)) return LSA_BAD_SHAPE;
   if (epi == EPI_STORE && (!ep->out || ep->ldo < N || ep->ldo % 8)) return LSA_BAD_SHAPE;
   if (epi == EPI_QKV && (!ep->k_cache || !ep->v_cache || !ep->slot || !ep->pos || !ep->out)) return LSA_BAD_SHAPE;
   if (ep->ss_out) return LSA_UNSUPPORTED;
   if (ep->ss_in && (epi != EPI_QKV || ep->ss_n < 4 || ep->ss_n % 4 || K != 64 * ep->ss_n)) return LSA_BAD_SHAPE;
   const bf16_raw* A = static_cast<const bf16_raw*>(a);
   const bf16_raw* W = static_cast<const bf16_raw*>(wp);
-#define LSA_WR(FN) \
-  return epi == EPI_QKV ? wr_launch<FN, EPI_QKV>(A, lda, W, M, N, K, *ep, grid, stream) \
-                        : wr_launch<FN, EPI_STORE>(A, lda, W, M, N, K, *ep, grid, stream);
+#define LSA_WR(FN)                                                                                     \
+  return epi == EPI_QKV     ? wr_launch<FN, EPI_QKV>(A, lda, W, M, N, K, *ep, grid, split, stream)     \
+         : epi == EPI_PARTIAL ? wr_launch<FN, EPI_PARTIAL>(A, lda, W, M, N, K, *ep, grid, split, stream) \
+                              : wr_launch<FN, EPI_STORE>(A, lda, W, M, N, K, *ep, grid, split, stream);
   if (bn == 128) { LSA_WR(2) }
   if (bn == 192) { LSA_WR(3) }
   LSA_WR(4)

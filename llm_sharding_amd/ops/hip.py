@@ -73,7 +73,7 @@ def lib() -> ctypes.CDLL:
     L.lsa_row_ss.argtypes = [vp, i, i, i, vp, vp]
     L.lsa_argmax_finalize.argtypes = [vp, i, vp, vp, i, vp, i, i, vp, vp]
     L.lsa_pos_advance.argtypes = [vp, i, i, vp]
-    L.lsa_gemm_wr.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(EpiArgs), i, i, vp]
+    L.lsa_gemm_wr.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(EpiArgs), i, i, i, vp]
     L.lsa_gemm_sk.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(EpiArgs), i, i, i, i, i, i, i, vp, vp, ctypes.c_longlong, i,
                               i, vp]
     for name in ("lsa_gemv", "lsa_gemv_coop", "lsa_gemv_fp8", "lsa_dequant_fp8_packed", "lsa_gemv_coop_fp8", "lsa_gemm",
@@ -361,18 +361,26 @@ def gemm_wr_plan(M: int, N: int, K: int, epi: int, ep: "EpiArgs") -> int:
 
 
 def gemm_wr(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep: EpiArgs, bn: int = 192,
-            grid: int = 0) -> None:
+            grid: int = 0, split: int = 1, out_numel: int = 0) -> None:
     """Projection GEMM with the weights fetched straight into MFMA B registers (gemm_wr.hip):
     128 x ``bn`` tiles, one per workgroup per round, A staged by LDS-DMA, EPI_STORE / EPI_QKV
-    (with the fused RMSNorm row scale, ``ep.ss_in``). K % 256 == 0, N % bn == 0."""
+    (with the fused RMSNorm row scale, ``ep.ss_in``) / EPI_PARTIAL (every tile split into
+    ``split`` K ranges of multiples of 256; fp32 partial k to ``ep.out`` [k][M][ldo], summed by
+    :func:`resid_rmsnorm_partials`; ``out_numel`` = the buffer's capacity in floats, checked).
+    K % 256 == 0, N % bn == 0."""
     _req(_is_bf16_cuda(a, wp), "gemm_wr: bf16 cuda tensors required")
     _req(wp.numel() == N * K and K % 256 == 0, "gemm_wr: packed weight shape (K % 256 == 0)")
     _req(a.dim() == 2 and a.shape[0] >= M >= 1 and a.shape[1] >= K and a.stride(1) == 1 and a.stride(0) % 8 == 0
          and a.data_ptr() % 16 == 0, "gemm_wr: A must be [>=M, >=K] row-major with 16-B aligned rows")
     _req(bn in (128, 192, 256) and N % bn == 0, f"gemm_wr: N={N} does not tile by bn={bn}")
-    _req(epi in (EPI_STORE, EPI_QKV) and not ep.ss_out, "gemm_wr: EPI_STORE / EPI_QKV only")
+    _req(epi in (EPI_STORE, EPI_QKV, EPI_PARTIAL) and not ep.ss_out, "gemm_wr: EPI_STORE / EPI_QKV / EPI_PARTIAL")
+    _req(split == 1 or (epi == EPI_PARTIAL and 1 <= split <= K // 256), f"gemm_wr: split {split}")
+    if epi == EPI_PARTIAL:
+        _req(out_numel >= split * M * ep.ldo, f"gemm_wr partial: output holds {out_numel} floats, "
+             f"split {split} x {M} rows x ldo {ep.ldo} needed")
     _check_epi(epi, ep, N)
-    rc = lib().lsa_gemm_wr(_p(a), a.stride(0), _p(wp), M, N, K, epi, ctypes.byref(ep), bn, grid or N_CU, _stream())
+    rc = lib().lsa_gemm_wr(_p(a), a.stride(0), _p(wp), M, N, K, epi, ctypes.byref(ep), bn, grid or N_CU, split,
+                           _stream())
     _check(rc, "lsa_gemm_wr")
 
 

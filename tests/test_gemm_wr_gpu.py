@@ -116,3 +116,27 @@ def test_gemm_dispatches_wr_for_one_round_of_192_tiles(monkeypatch):
     out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
     h.gemm(a, packing.pack_b(w), M, N, K, h.EPI_STORE, h.make_epi(out=out, ldo=N))
     assert calls and rel_err(out, a.float() @ w.float().T) < 8e-3
+
+
+@pytest.mark.parametrize("M,N,K,bn,S", [(512, 4096, 4096, 128, 2), (300, 1024, 2816, 256, 3), (129, 768, 1024, 128, 4),
+                                        (512, 4096, 11008, 128, 2)])
+def test_gemm_wr_partials_resid_rmsnorm(M, N, K, bn, S):
+    """EPI_PARTIAL: S K-range partials (multiples of 256) summed with the residual by
+    lsa_resid_rmsnorm_partials, then RMSNorm - against fp32."""
+    h = hip()
+    a, w, r = _rnd(M, K), _rnd(N, K, scale=0.02), _rnd(M, N)
+    part = torch.full((S, M, N), float("nan"), device=DEV)
+    with pytest.raises(RuntimeError):  # capacity is checked before the launch
+        h.gemm_wr(a, packing.pack_b(w), M, N, K, h.EPI_PARTIAL, h.make_epi(out=part, ldo=N), bn=bn, split=S,
+                  out_numel=part.numel() - 1)
+    h.gemm_wr(a, packing.pack_b(w), M, N, K, h.EPI_PARTIAL, h.make_epi(out=part, ldo=N), bn=bn, split=S,
+              out_numel=part.numel())
+    ref = a.float() @ w.float().T
+    assert rel_err(part.sum(0), ref) < 1e-4  # fp32 partials, fp32 sums
+    hb = r.clone()
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    h.resid_rmsnorm_partials(hb, part, S, M, 1e-5, out=out)
+    hr = r.float() + ref
+    assert rel_err(hb, hr) < 8e-3
+    hf = hb.float()
+    assert rel_err(out, hf * torch.rsqrt(hf.pow(2).mean(-1, keepdim=True) + 1e-5)) < 8e-3
