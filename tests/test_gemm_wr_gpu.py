@@ -118,7 +118,7 @@ def test_gemm_dispatches_wr_for_one_round_of_192_tiles(monkeypatch):
     assert calls and rel_err(out, a.float() @ w.float().T) < 8e-3
 
 
-@pytest.mark.parametrize("M,N,K,bn,S", [(512, 4096, 4096, 128, 2), (300, 1024, 2816, 256, 3), (129, 768, 1024, 128, 4),
+@pytest.mark.parametrize("M,N,K,bn,S", [(512, 4096, 4096, 128, 2), (300, 2048, 2816, 256, 3), (129, 2048, 1024, 128, 4),
                                         (512, 4096, 11008, 128, 2)])
 def test_gemm_wr_partials_resid_rmsnorm(M, N, K, bn, S):
     """EPI_PARTIAL: S K-range partials (multiples of 256) summed with the residual by
@@ -126,7 +126,7 @@ def test_gemm_wr_partials_resid_rmsnorm(M, N, K, bn, S):
     h = hip()
     a, w, r = _rnd(M, K), _rnd(N, K, scale=0.02), _rnd(M, N)
     part = torch.full((S, M, N), float("nan"), device=DEV)
-    with pytest.raises(RuntimeError):  # capacity is checked before the launch
+    with pytest.raises(ValueError):  # capacity is checked before the launch
         h.gemm_wr(a, packing.pack_b(w), M, N, K, h.EPI_PARTIAL, h.make_epi(out=part, ldo=N), bn=bn, split=S,
                   out_numel=part.numel() - 1)
     h.gemm_wr(a, packing.pack_b(w), M, N, K, h.EPI_PARTIAL, h.make_epi(out=part, ldo=N), bn=bn, split=S,
