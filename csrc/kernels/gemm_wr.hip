@@ -198,6 +198,13 @@ LSA_DEVICE void gemm_wr_body(unsigned char* smem, const bf16_raw* __restrict__ A
       step(t + 3, std::integral_constant<int, 3>{});
     }
     wr_vm_wait<0>();  // the dead prefetches land before the LDS is reused
+    // ... and before their destination registers are: the compiler sees the last group's weight
+    // prefetches as dead values and could hand their registers to epilogue values while the
+    // loads are still in flight - keeping them live up to here (after the wait) rules that out
+#pragma unroll
+    for (int sl = 0; sl < NS; ++sl)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) asm volatile("" ::"v"(wr[sl][j][0]), "v"(wr[sl][j][1]));
     wr_barrier();
 
     // epilogue: fp32 tile through a wave-private LDS image; one lane per (row, 16 columns)
