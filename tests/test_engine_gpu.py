@@ -106,6 +106,18 @@ def test_big_batch_decode_graph_vs_golden(rows, partial):
             _big_batch_vs_golden(rows)
 
 
+def test_512_row_decode_qkv_on_gemm_wr_vs_golden(monkeypatch):
+    """The headline decode shape (512 sequences, 7B layers): the qkv projection inside the
+    captured graph runs on gemm_wr.hip (weights straight into MFMA registers, fused-RMSNorm row
+    scale + RoPE/KV append) - asserted - and the step matches the fp32 golden model."""
+    from llm_sharding_amd.ops import hip
+    calls = []
+    real = hip.gemm_wr
+    monkeypatch.setattr(hip, "gemm_wr", lambda *a, **k: (calls.append(a[2:5]), real(*a, **k)))
+    _big_batch_vs_golden(512)
+    assert (512, 12288, 4096) in calls
+
+
 @pytest.mark.parametrize("rows", [40, 100])
 def test_decode_coop_partials_vs_golden(rows, monkeypatch):
     """17..128-row decode with the residual projections as coop EPI_PARTIAL +
