@@ -262,7 +262,8 @@ LSA_DEVICE void gemm_wr_body(unsigned char* smem, const bf16_raw* __restrict__ A
       }
       __builtin_amdgcn_sched_barrier(0);
     }
-    wr_barrier();  // the image is dead before the next tile's DMA reuses the LDS
+    wr_vm_wait<0>();  // this tile's stores retired: the next item's counted waits see only its own loads
+    wr_barrier();     // the image is dead before the next tile's DMA reuses the LDS
   }
 }
 
