@@ -34,7 +34,7 @@ def main():
     if os.environ.get("WR_LIB"):  # an ablation build of gemm_wr.hip (-DLSA_WR_ABLATE=n)
         L = ctypes.CDLL(os.environ["WR_LIB"])
     vp, i = ctypes.c_void_p, ctypes.c_int
-    L.lsa_gemm_wr.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(hip.EpiArgs), i, i, vp]
+    L.lsa_gemm_wr.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(hip.EpiArgs), i, i, i, vp]
     shapes = [tuple(int(v) for v in a.split(",")) for a in sys.argv[1:]] or [
         (512, 12288, 4096), (512, 22016, 4096), (512, 4096, 11008), (512, 4096, 4096), (16384, 4096, 4096)]
     for M, N, K in shapes:
@@ -59,7 +59,7 @@ def main():
 
                     def run(r=0, bn=bn, grid=grid, epw=epw):
                         rc = L.lsa_gemm_wr(vp(x.data_ptr()), K, vp(wps[r % nbuf].data_ptr()), M, N, K, hip.EPI_STORE,
-                                           ctypes.byref(epw), bn, grid, stream)
+                                           ctypes.byref(epw), bn, grid, 1, stream)
                         assert rc == 0, rc
                     run(0)
                     torch.cuda.synchronize()
