@@ -346,7 +346,7 @@ SK_BM = 256  # gemm_sk.hip row tile (default; 128-row tiles for small / odd M: p
 
 # gemm_wr.hip (weights streamed into MFMA registers, 128 x bn tiles, one round of whole-K tiles)
 # where it measured faster than gemm_sk's best plan: one round of 224-256 whole 128 x 192 tiles,
-# i.e. the 7B qkv projection at 449-512 rows (54-55 us vs 68-81 us, profiles/r3_gemm_wr.md).
+# i.e. the 7B qkv projection at 385-512 rows (54-55 us vs 68-81 us, profiles/r3_gemm_wr.md).
 # LSA_GEMM_WR=0 turns it off (A/B runs).
 WR_TILES = (224, 256)
 

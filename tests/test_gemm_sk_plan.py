@@ -27,3 +27,22 @@ def test_cost_model_for_untuned_shapes():
         assert bn in (128, 192, 256) and N % (16 if bn == 192 else bn) == 0 and grid == hip.N_CU and split >= 0
         assert bm in (128, 256)
         assert hip.gemm_sk_plan(M, N, K, tuned=False) == (bn, grid, dp, split, bm) or (N, K) in hip._sk_tuned()
+
+
+def test_gemm_wr_route(monkeypatch):
+    """hip.gemm sends a projection to gemm_wr.hip only where it measured faster than gemm_sk: one
+    round of 224-256 whole 128 x 192 tiles with a store / QKV epilogue (the 7B qkv projection at
+    385-512 rows); everything else, and LSA_GEMM_WR=0, stays on gemm_sk."""
+    monkeypatch.delenv("LSA_GEMM_WR", raising=False)
+    ep = hip.EpiArgs()
+    assert hip.gemm_wr_plan(512, 12288, 4096, hip.EPI_QKV, ep) == 192
+    assert hip.gemm_wr_plan(385, 12288, 4096, hip.EPI_STORE, ep) == 192
+    for M, N, K, epi in [(384, 12288, 4096, hip.EPI_QKV),   # 3 row tiles: 192 tiles
+                         (513, 12288, 4096, hip.EPI_QKV),   # 5 row tiles: 320 tiles
+                         (512, 12288, 4096, hip.EPI_SWIGLU),
+                         (512, 4096, 4096, hip.EPI_RESID),
+                         (512, 22016, 4096, hip.EPI_SWIGLU),
+                         (512, 12288, 4160, hip.EPI_QKV)]:  # K % 256 != 0
+        assert hip.gemm_wr_plan(M, N, K, epi, ep) == 0, (M, N, K, epi)
+    monkeypatch.setenv("LSA_GEMM_WR", "0")
+    assert hip.gemm_wr_plan(512, 12288, 4096, hip.EPI_QKV, ep) == 0
