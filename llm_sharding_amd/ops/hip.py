@@ -346,7 +346,7 @@ SK_BM = 256  # gemm_sk.hip row tile (default; 128-row tiles for small / odd M: p
 
 # gemm_wr.hip (weights streamed into MFMA registers, 128 x bn tiles, one round of whole-K tiles)
 # where it measured faster than gemm_sk's best plan: one round of 224-256 whole 128 x 192 tiles,
-# i.e. the 7B qkv projection at 385-512 rows (54-55 us vs 68-81 us, profiles/r3_gemm_wr.md).
+# i.e. the 7B qkv projection at 448-512 rows (54-55 us vs 59-81 us, profiles/r3_gemm_wr.md).
 # LSA_GEMM_WR=0 turns it off (A/B runs).
 WR_TILES = (224, 256)
 
@@ -356,8 +356,11 @@ def gemm_wr_plan(M: int, N: int, K: int, epi: int, ep: "EpiArgs") -> int:
     if os.environ.get("LSA_GEMM_WR", "1") == "0" or epi not in (EPI_STORE, EPI_QKV) or ep.ss_out or ep.act \
             or ep.bias or K % 256 or N % 192:
         return 0
-    tiles = -(-M // 128) * (N // 192)
-    return 192 if WR_TILES[0] <= tiles <= WR_TILES[1] else 0
+    mt = -(-M // 128)
+    tiles = mt * (N // 192)
+    # the last row tile at least half full: the kernel computes whole 128-row tiles, gemm_sk's
+    # 128-row plans do not (measured at 448 and 512 rows)
+    return 192 if WR_TILES[0] <= tiles <= WR_TILES[1] and M - (mt - 1) * 128 >= 64 else 0
 
 
 def gemm_wr(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep: EpiArgs, bn: int = 192,
