@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""Projection GEMMs at decode-batch and prompt-sized M: the hand-written stream-K MFMA GEMM
-(gemm_sk.hip, plain-store epilogue, the plan the engine uses) against torch.matmul
+"""Projection GEMMs at decode-batch and prompt-sized M: the engine's hand-written GEMM dispatch
+(hip.gemm: gemm_wr.hip where its route applies, else gemm_sk.hip with the plan the engine uses;
+plain-store epilogue) against torch.matmul
 (hipBLASLt on ROCm, plain GEMM, no epilogue). Weights rotate over > 600 MB of copies so they
 stream from HBM (beyond the 256 MB Infinity Cache) as in a decode step; both timed as
 20 launches captured in one hipGraph (no host overhead).
@@ -32,14 +33,15 @@ def main():
             out = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
             ref = torch.empty_like(out)
             ep = hip.make_epi(out=out, ldo=N)
-            plan = hip.gemm_sk_plan(M, N, K)
-            t_ours = timeit(lambda i: hip.gemm_sk(x, wps[i % nbuf], M, N, K, hip.EPI_STORE, ep, ws=sk_ws))
+            wr = hip.gemm_wr_plan(M, N, K, hip.EPI_STORE, ep)
+            plan = ["gemm_wr", wr] if wr else list(hip.gemm_sk_plan(M, N, K))
+            t_ours = timeit(lambda i: hip.gemm(x, wps[i % nbuf], M, N, K, hip.EPI_STORE, ep, sk_ws=sk_ws))
             t_blas = timeit(lambda i: torch.matmul(x, ws_[i % nbuf].t(), out=ref))
-            hip.gemm_sk(x, wps[0], M, N, K, hip.EPI_STORE, ep, ws=sk_ws)
+            hip.gemm(x, wps[0], M, N, K, hip.EPI_STORE, ep, sk_ws=sk_ws)
             torch.matmul(x, ws_[0].t(), out=ref)
             err = ((out.float() - ref.float()).norm() / ref.float().norm()).item()
             fl = 2.0 * M * N * K
-            print(json.dumps({"shape": name, "M": M, "N": N, "K": K, "cold_weights": True, "plan": list(plan),
+            print(json.dumps({"shape": name, "M": M, "N": N, "K": K, "cold_weights": True, "plan": plan,
                               "ours_us": round(t_ours, 2), "ours_tflops": round(fl / t_ours / 1e6, 1),
                               "hipblaslt_us": round(t_blas, 2), "hipblaslt_tflops": round(fl / t_blas / 1e6, 1),
                               "speedup": round(t_blas / t_ours, 3), "relerr_vs_hipblaslt": float(f"{err:.2e}")}),
