@@ -1,4 +1,7 @@
-// Projection GEMM with the weights streamed straight into MFMA B registers (experimental).
+// Projection GEMM with the weights streamed straight into MFMA B registers.
+// hip.gemm routes it one round of 224-256 whole 128 x 192 tiles (the 7B qkv projection at
+// 448-512 rows: 57.9 vs 68.1 us per layer in the headline decode step, profiles/r3_gemm_wr.md);
+// gemm_sk.hip stays faster on every other measured shape.
 //
 //   C[M, N] = A[M, K] @ W^T, bf16 in, fp32 accumulate.
 //
@@ -9,9 +12,9 @@
 //  * 4 waves (one per SIMD), 128-row x BN tile, each wave owns ALL 128 rows x BN/4 columns, so
 //    every weight fragment is used by exactly one wave: it is fetched with ONE
 //    global_load_dwordx4 per lane (the packed-16x32 layout of common.h is already lane-linear
-//    1 KiB per fragment) into registers, prefetched P K-steps ahead - no LDS for W at all.
+//    1 KiB per fragment) into registers, prefetched 3 K-steps ahead - no LDS for W at all.
 //  * only A goes through LDS (LDS-DMA, whole 128-B rows, XOR-swizzled 16-B chunks as in
-//    gemm_sk: conflict-free ds_read_b128 fragment reads), an NBUF-deep ring.
+//    gemm_sk: conflict-free ds_read_b128 fragment reads), a 4-deep ring.
 //  * LDS traffic per K-step: 16 KiB of DMA writes + 4 x 16 KiB of fragment reads, against
 //    8 x FN x 2 MFMAs per wave: 37.5 % (BN 256) / 50 % (BN 192) of the MFMA time, where
 //    gemm_sk's 256 x 128 tile is at ~87 %.
@@ -25,8 +28,8 @@ namespace {
 constexpr int WR_BM = 128, WR_BK = 64, WR_NTHR = 256;
 constexpr int WR_ABUF = WR_BM * WR_BK * 2;  // one A K-step image: 16 KiB
 
-// Diagnostic ablation builds only (-DLSA_WR_ABLATE=n, scripts/gemm_wr_probe.py --ablate; results
-// are garbage): 1 = no VMEM in the loop, 2 = no barriers in the loop, 3 = no LDS reads in the
+// Diagnostic ablation builds only (-DLSA_WR_ABLATE=n into a separate .so, timed by
+// scripts/gemm_wr_probe.py with WR_LIB=<that .so>; scripts/gpu_r3_wr_abl.sh; results are garbage): 1 = no VMEM in the loop, 2 = no barriers in the loop, 3 = no LDS reads in the
 // loop, 4 = no MFMAs (faults: the unused asm load targets get reused), 5 = MFMAs only.
 // The production library never defines it.
 #ifndef LSA_WR_ABLATE
@@ -63,12 +66,13 @@ struct WrGeo {
 // MT row tiles sharing a weight panel run together (and on one XCD after the block remap).
 // Pipeline of one 64-deep K-step t (two 32-deep MFMA fragments kf0 / kf1):
 //   phase A: MFMAs of kf0 (A frags a0, read during step t-1) interleaved with the reads of
-//            kf1's frags (a1) and with this step's prefetches (W(t+3) into register slot
-//            (t+3)%4, A(t+3) into ring slot (t+3)%4: 2*FN + 4 VMEM instructions spread over
-//            the MFMAs - issued as one burst they stall the single wave on the texture path)
-//   lgkmcnt(0) + vmcnt(2 steps in flight) + barrier: A(t+1) complete in LDS for every wave,
-//            and every wave's reads of ring slot t%4 retired (slot t%4 is refilled at step t+1)
-//   phase B: MFMAs of kf1 interleaved with the reads of step t+1's kf0 frags.
+//            kf1's frags (a1) and the weight prefetch W(t+3) into register slot (t+3)%4 (2*FN
+//            loads spread over the MFMAs - issued as one burst they stall the single wave on
+//            the texture path)
+//   vmcnt (W(t+2), A(t+2), W(t+3) may stay in flight) + barrier: A(t+1) is in LDS for every
+//            wave, and every wave has consumed its reads of ring slot (t-1)%4
+//   phase B: MFMAs of kf1 interleaved with the reads of step t+1's kf0 frags and the A DMA of
+//            step t+3 into ring slot (t+3)%4 = (t-1)%4.
 // (the body is a __device__ function: lambdas directly inside a __global__ template kept the
 // host pass from emitting the kernel's launch stub)
 template <int FN, int EPI>
