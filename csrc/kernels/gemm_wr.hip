@@ -112,7 +112,13 @@ LSA_DEVICE void gemm_wr_body(unsigned char* smem, const bf16_raw* __restrict__ A
       aoff[s] = (unsigned)((min(m0 + row, M - 1) * lda + ch * 8) * 2);
     }
     const unsigned char* abase = reinterpret_cast<const unsigned char*>(A);
-    const bf16_raw* wbase = Wp + ((size_t)n16 * KT32 * 64 + lane) * 8;  // + (j*KT32 + kt)*512
+    // weights: wave-uniform base of this wave's column panel (SGPRs; + 2 KiB per K-step) and a
+    // per-lane offset per 16-column tile j (lane * 16 + j * KT32 KiB): the loads use the saddr
+    // form, no per-load 64-bit address VALU (the single wave is issue-bound, profiles/r3_gemm_wr.md)
+    const unsigned char* wsb = reinterpret_cast<const unsigned char*>(Wp) + (size_t)n16 * KT32 * 1024;
+    unsigned wvo[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) wvo[j] = (unsigned)(lane * 16 + j * KT32 * 1024);
 
     f32x4_t acc[8][FN];
 #pragma unroll
@@ -128,9 +134,12 @@ LSA_DEVICE void gemm_wr_body(unsigned char* smem, const bf16_raw* __restrict__ A
     // step covers these loads.
     auto wload = [&](u32x4_t (&dst)[FN][2], int v, int ts) {
       if constexpr (LSA_WR_ABLATE == 1 || LSA_WR_ABLATE == 5) if (ts > 2) return;
-      const int j = v >> 1, kf = v & 1;
-      const bf16_raw* p = wbase + ((size_t)j * KT32 + 2 * ts + kf) * 512;
-      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(dst[j][kf]) : "v"(p) : "memory");
+      const int j = v >> 1;
+      const unsigned char* sb = wsb + (size_t)ts * 2048;
+      if (v & 1)
+        asm volatile("global_load_dwordx4 %0, %1, %2 offset:1024" : "=v"(dst[j][1]) : "v"(wvo[j]), "s"(sb) : "memory");
+      else
+        asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(dst[j][0]) : "v"(wvo[j]), "s"(sb) : "memory");
     };
     // A DMA block s of step ts into ring slot `ring`
     auto aload = [&](int ring, int s, int ts) {
