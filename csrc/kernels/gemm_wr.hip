@@ -47,15 +47,15 @@ LSA_DEVICE void wr_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <int FN>
+template <int FN, int NG = 1>
 struct WrGeo {
   static constexpr int TN = FN * 16, BN = 4 * TN;
   static constexpr int NS = 4;                        // W register slots = A ring slots (distance 3)
   static constexpr int ADMA = WR_ABUF / 1024 / 4;     // A DMA instructions per wave per step (4)
   static constexpr int PER = 2 * FN + ADMA;           // VMEM instructions per wave per step
   static constexpr int ELD = TN + 4;                  // fp32 row stride of the epilogue image
-  static constexpr int EPI_BYTES = 4 * WR_BM * ELD * 4;
-  static constexpr int RS_OFF = (NS * WR_ABUF > EPI_BYTES ? NS * WR_ABUF : EPI_BYTES);  // row rstd [128]
+  static constexpr int EPI_BYTES = NG * 4 * WR_BM * ELD * 4;  // NG = 2: group 1's partial image too
+  static constexpr int RS_OFF = (NG * NS * WR_ABUF > EPI_BYTES ? NG * NS * WR_ABUF : EPI_BYTES);  // row rstd [128]
   static constexpr int SMEM = RS_OFF + WR_BM * 4;
   static_assert(SMEM <= 160 * 1024, "LDS budget");
   static_assert(2 * PER <= 63, "vmcnt range");
@@ -75,14 +75,21 @@ struct WrGeo {
 //            step t+3 into ring slot (t+3)%4 = (t-1)%4.
 // (the body is a __device__ function: lambdas directly inside a __global__ template kept the
 // host pass from emitting the kernel's launch stub)
-template <int FN, int EPI>
-LSA_DEVICE void gemm_wr_body(unsigned char* smem, const bf16_raw* __restrict__ A, int lda,
+// NG = 2 (experimental, scripts/gemm_wr_probe.py): two wave groups of 4 waves split every tile's
+// K range in halves (two waves per SIMD, one from each group: while one waits, the other
+// issues), each group with its own A ring; group 1 hands its partial accumulators to group 0
+// through LDS before the epilogue. Both groups run the same number of steps, so every barrier
+// pairs up.
+template <int FN, int EPI, int NG>
+LSA_DEVICE void gemm_wr_body(unsigned char* smem_all, const bf16_raw* __restrict__ A, int lda,
                              const bf16_raw* __restrict__ Wp, int M, int N, int K, const EpiArgs& ep, int MT,
                              int NT, int S) {
-  using G_ = WrGeo<FN>;
+  using G_ = WrGeo<FN, NG>;
   constexpr int TN = G_::TN, BN = G_::BN, NS = G_::NS, ADMA = G_::ADMA, PER = G_::PER;
   const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wg = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int grp = wg >> 2, w = wg & 3;  // wave group, column owner within the group
+  unsigned char* smem = smem_all + grp * (NS * WR_ABUF);  // this group's A ring
   const int G = gridDim.x;
   int g;
   {  // XCD-aware remap (bijective): blocks of one XCD get consecutive work ids
@@ -101,7 +108,12 @@ LSA_DEVICE void gemm_wr_body(unsigned char* smem, const bf16_raw* __restrict__ A
   for (int item = g; item < MT * NT * S; item += G) {
     const int tile = item % (MT * NT), sp = item / (MT * NT);
     const int mt = tile % MT, nt = tile / MT;
-    const int k0 = (sp * n4 / S) * NS, nsteps = ((sp + 1) * n4 / S) * NS;  // steps [k0, nsteps)
+    int k0 = (sp * n4 / S) * NS, nsteps = ((sp + 1) * n4 / S) * NS;  // steps [k0, nsteps)
+    if (NG == 2) {  // halves of the range, both multiples of NS (host: K % (2 NS 64) == 0)
+      const int half = (nsteps - k0) / 2;
+      k0 += grp * half;
+      nsteps = k0 + half;
+    }
     const int m0 = mt * WR_BM, n16 = (nt * BN + w * TN) >> 4;  // this wave's first 16-col tile
     // A DMA: wave w fills blocks w*ADMA + s (8 rows x 128 B each) of every ring buffer
     unsigned aoff[ADMA];
@@ -220,13 +232,33 @@ LSA_DEVICE void gemm_wr_body(unsigned char* smem, const bf16_raw* __restrict__ A
       for (int j = 0; j < FN; ++j) asm volatile("" ::"v"(wr[sl][j][0]), "v"(wr[sl][j][1]));
     wr_barrier();
 
+    if (NG == 2) {  // group 1's partial sums -> LDS -> added into group 0's accumulators
+      float* part = reinterpret_cast<float*>(smem_all) + (4 + w) * (WR_BM * G_::ELD);
+      if (grp == 1) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) part[(i * 16 + 4 * (lane >> 4) + r) * G_::ELD + j * 16 + (lane & 15)] = acc[i][j][r];
+      }
+      __syncthreads();
+      if (grp == 0) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[i][j][r] += part[(i * 16 + 4 * (lane >> 4) + r) * G_::ELD + j * 16 + (lane & 15)];
+      }
+    }
     // epilogue: fp32 tile through a wave-private LDS image; one lane per (row, 16 columns)
     // unit runs the row16 epilogues of epilogue.h (EPI_QKV: RoPE + KV-cache append; with
     // ss_in, the fused RMSNorm's row scale first, computed once per workgroup in gemm_sk's
     // summation order so both GEMMs produce the same bits)
-    float* s_rs = reinterpret_cast<float*>(smem + G_::RS_OFF);
+    float* s_rs = reinterpret_cast<float*>(smem_all + G_::RS_OFF);
     if (EPI == EPI_QKV && ep.ss_in) {
-      for (int r = threadIdx.x; r < WR_BM; r += WR_NTHR) {
+      for (int r = threadIdx.x; r < WR_BM; r += WR_NTHR * NG) {
         const int m = min(m0 + r, M - 1);
         const float* sp = ep.ss_in + (size_t)m * ep.ss_n;
         float tsum = 0.f;
@@ -243,17 +275,20 @@ LSA_DEVICE void gemm_wr_body(unsigned char* smem, const bf16_raw* __restrict__ A
         s_rs[r] = rsqrtf(tsum / (float)(64 * ep.ss_n) + ep.ss_eps);
       }
     }
-    float* img = reinterpret_cast<float*>(smem) + w * (WR_BM * G_::ELD);
+    float* img = reinterpret_cast<float*>(smem_all) + w * (WR_BM * G_::ELD);
+    if (grp == 0) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+      for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int j = 0; j < FN; ++j)
+        for (int j = 0; j < FN; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) img[(i * 16 + 4 * (lane >> 4) + r) * G_::ELD + j * 16 + (lane & 15)] = acc[i][j][r];
+          for (int r = 0; r < 4; ++r) img[(i * 16 + 4 * (lane >> 4) + r) * G_::ELD + j * 16 + (lane & 15)] = acc[i][j][r];
+    }
     __syncthreads();  // the image and the row scales are complete
     const int col_base = nt * BN + w * TN;
 #pragma unroll
     for (int s2 = 0; s2 < (WR_BM * FN) / 64; ++s2) {
+      if (grp != 0) break;  // NG = 2: group 0 owns the epilogue
       const int u = lane + 64 * s2, row = u / FN, j = u % FN;
       const int m = m0 + row;
       float v[16];
@@ -280,21 +315,22 @@ LSA_DEVICE void gemm_wr_body(unsigned char* smem, const bf16_raw* __restrict__ A
   }
 }
 
-template <int FN, int EPI>
-__global__ __launch_bounds__(WR_NTHR) void gemm_wr_kernel(const bf16_raw* __restrict__ A, int lda,
-                                                          const bf16_raw* __restrict__ Wp, int M, int N, int K,
-                                                          EpiArgs ep, int MT, int NT, int S) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[WrGeo<FN>::SMEM];
-  gemm_wr_body<FN, EPI>(smem, A, lda, Wp, M, N, K, ep, MT, NT, S);
+template <int FN, int EPI, int NG>
+__global__ __launch_bounds__(WR_NTHR * NG) void gemm_wr_kernel(const bf16_raw* __restrict__ A, int lda,
+                                                               const bf16_raw* __restrict__ Wp, int M, int N, int K,
+                                                               EpiArgs ep, int MT, int NT, int S) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[WrGeo<FN, NG>::SMEM];
+  gemm_wr_body<FN, EPI, NG>(smem, A, lda, Wp, M, N, K, ep, MT, NT, S);
 }
 
-template <int FN, int EPI>
+template <int FN, int EPI, int NG = 1>
 int wr_launch(const bf16_raw* A, int lda, const bf16_raw* W, int M, int N, int K, const EpiArgs& ep, int grid,
               int split, hipStream_t s) {
-  constexpr int BN = WrGeo<FN>::BN;
+  constexpr int BN = WrGeo<FN, NG>::BN;
   const int MT = (M + WR_BM - 1) / WR_BM, NT = N / BN;
   const int items = MT * NT * split;
-  gemm_wr_kernel<FN, EPI><<<grid < items ? grid : items, WR_NTHR, 0, s>>>(A, lda, W, M, N, K, ep, MT, NT, split);
+  gemm_wr_kernel<FN, EPI, NG><<<grid < items ? grid : items, WR_NTHR * NG, 0, s>>>(A, lda, W, M, N, K, ep, MT, NT,
+                                                                                   split);
   LSA_CHECK_LAUNCH();
   return LSA_OK;
 }
@@ -306,10 +342,11 @@ int wr_launch(const bf16_raw* A, int lda, const bf16_raw* W, int M, int N, int K
 // EPI_PARTIAL: every tile split into exactly `split` K ranges (multiples of 256), fp32 partial
 // k to ((float*)ep->out)[k][M][ldo] (lsa_resid_rmsnorm_partials sums them); the caller checks
 // the buffer holds split * M * ldo floats. bn: 128 / 192 / 256 with N % bn == 0; K % 256 == 0;
-// grid: workgroups (work items beyond it loop). Returns LSA_BAD_SHAPE on any shape the
-// kernel's indexing cannot take.
+// grid: workgroups (work items beyond it loop). ng = 2 (experimental: two wave groups split
+// each tile's K range; bn 128, EPI_STORE, split 1, K % 512 == 0). Returns LSA_BAD_SHAPE on any
+// shape the kernel's indexing cannot take.
 extern "C" int lsa_gemm_wr(const void* a, int lda, const void* wp, int M, int N, int K, int epi, const EpiArgs* ep,
-                           int bn, int grid, int split, hipStream_t stream) {
+                           int bn, int grid, int split, int ng, hipStream_t stream) {
   if (M < 1 || K < 4 * WR_BK || K % (4 * WR_BK) || lda < K || lda % 8 || grid < 1 || !ep) return LSA_BAD_SHAPE;
   if (bn != 128 && bn != 192 && bn != 256) return LSA_UNSUPPORTED;
   if (N % bn) return LSA_BAD_SHAPE;
@@ -320,8 +357,14 @@ extern "C" int lsa_gemm_wr(const void* a, int lda, const void* wp, int M, int N,
   if (epi == EPI_QKV && (!ep->k_cache || !ep->v_cache || !ep->slot || !ep->pos || !ep->out)) return LSA_BAD_SHAPE;
   if (ep->ss_out) return LSA_UNSUPPORTED;
   if (ep->ss_in && (epi != EPI_QKV || ep->ss_n < 4 || ep->ss_n % 4 || K != 64 * ep->ss_n)) return LSA_BAD_SHAPE;
+  if (ng != 1 && ng != 2) return LSA_UNSUPPORTED;
   const bf16_raw* A = static_cast<const bf16_raw*>(a);
   const bf16_raw* W = static_cast<const bf16_raw*>(wp);
+  if (ng == 2) {
+    if (bn != 128 || epi != EPI_STORE || split != 1) return LSA_UNSUPPORTED;
+    if (K % (8 * WR_BK)) return LSA_BAD_SHAPE;
+    return wr_launch<2, EPI_STORE, 2>(A, lda, W, M, N, K, *ep, grid, 1, stream);
+  }
 #define LSA_WR(FN)                                                                                     \
   return epi == EPI_QKV     ? wr_launch<FN, EPI_QKV>(A, lda, W, M, N, K, *ep, grid, split, stream)     \
          : epi == EPI_PARTIAL ? wr_launch<FN, EPI_PARTIAL>(A, lda, W, M, N, K, *ep, grid, split, stream) \

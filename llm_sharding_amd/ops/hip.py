@@ -73,7 +73,7 @@ def lib() -> ctypes.CDLL:
     L.lsa_row_ss.argtypes = [vp, i, i, i, vp, vp]
     L.lsa_argmax_finalize.argtypes = [vp, i, vp, vp, i, vp, i, i, vp, vp]
     L.lsa_pos_advance.argtypes = [vp, i, i, vp]
-    L.lsa_gemm_wr.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(EpiArgs), i, i, i, vp]
+    L.lsa_gemm_wr.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(EpiArgs), i, i, i, i, vp]
     L.lsa_gemm_sk.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(EpiArgs), i, i, i, i, i, i, i, vp, vp, ctypes.c_longlong, i,
                               i, vp]
     for name in ("lsa_gemv", "lsa_gemv_coop", "lsa_gemv_fp8", "lsa_dequant_fp8_packed", "lsa_gemv_coop_fp8", "lsa_gemm",
@@ -382,7 +382,7 @@ def gemm_wr(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int,
         _req(out_numel >= split * M * ep.ldo, f"gemm_wr partial: output holds {out_numel} floats, "
              f"split {split} x {M} rows x ldo {ep.ldo} needed")
     _check_epi(epi, ep, N)
-    rc = lib().lsa_gemm_wr(_p(a), a.stride(0), _p(wp), M, N, K, epi, ctypes.byref(ep), bn, grid or N_CU, split,
+    rc = lib().lsa_gemm_wr(_p(a), a.stride(0), _p(wp), M, N, K, epi, ctypes.byref(ep), bn, grid or N_CU, split, 1,
                            _stream())
     _check(rc, "lsa_gemm_wr")
 

@@ -34,7 +34,7 @@ def main():
     if os.environ.get("WR_LIB"):  # an ablation build of gemm_wr.hip (-DLSA_WR_ABLATE=n)
         L = ctypes.CDLL(os.environ["WR_LIB"])
     vp, i = ctypes.c_void_p, ctypes.c_int
-    L.lsa_gemm_wr.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(hip.EpiArgs), i, i, i, vp]
+    L.lsa_gemm_wr.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(hip.EpiArgs), i, i, i, i, vp]
     shapes = [tuple(int(v) for v in a.split(",")) for a in sys.argv[1:]] or [
         (512, 12288, 4096), (512, 22016, 4096), (512, 4096, 11008), (512, 4096, 4096), (16384, 4096, 4096)]
     for M, N, K in shapes:
@@ -45,10 +45,12 @@ def main():
         ref = (x.float() @ ws[0].float().T)
         stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
         res = {"M": M, "N": N, "K": K}
-        only = os.environ.get("WR_ONLY")  # "bn,p,grid": one configuration (profiling)
+        only = os.environ.get("WR_ONLY")  # "bn,ng,grid": one configuration (profiling)
         cfgs = [tuple(int(v) for v in only.split(","))] if only else [
-            (bn, p, g) for bn in (128, 192, 256) for p in (2,) for g in (256, 512)]
-        for bn, p, grid in cfgs:
+            (bn, ng, g) for bn in (128, 192, 256) for ng in ((1, 2) if bn == 128 else (1,)) for g in (256, 512)]
+        for bn, ng, grid in cfgs:
+            if ng == 2 and K % 512:
+                continue
             if N % bn:
                 continue
             if True:
@@ -57,15 +59,15 @@ def main():
 
                     epw = hip.make_epi(out=out, ldo=N)
 
-                    def run(r=0, bn=bn, grid=grid, epw=epw):
+                    def run(r=0, bn=bn, grid=grid, epw=epw, ng=ng):
                         rc = L.lsa_gemm_wr(vp(x.data_ptr()), K, vp(wps[r % nbuf].data_ptr()), M, N, K, hip.EPI_STORE,
-                                           ctypes.byref(epw), bn, grid, 1, stream)
+                                           ctypes.byref(epw), bn, grid, 1, ng, stream)
                         assert rc == 0, rc
                     run(0)
                     torch.cuda.synchronize()
                     err = ((out.float() - ref).norm() / ref.norm()).item()
                     us = timeit(run)
-                    res[f"bn{bn}_p{p}_g{grid}"] = [round(us, 2), round(2 * M * N * K / us / 1e6, 1), f"{err:.1e}"]
+                    res[f"bn{bn}_ng{ng}_g{grid}"] = [round(us, 2), round(2 * M * N * K / us / 1e6, 1), f"{err:.1e}"]
         if os.environ.get("WR_ONLY"):
             print(json.dumps(res), flush=True)
             continue

@@ -4,7 +4,7 @@ set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out/wrpmc
 export TMPDIR=/tmp
-export WR_ONLY=256,2,512
+export WR_ONLY=256,1,512
 i=0
 for pmc in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_MFMA SQ_WAIT_INST_LDS" \
            "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_INSTS_VALU SQ_INSTS_MFMA"; do

@@ -4,7 +4,7 @@ set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out/wrpmc2
 export TMPDIR=/tmp
-export WR_ONLY=192,2,256
+export WR_ONLY=192,1,256
 i=0
 for pmc in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA" \
            "GRBM_GUI_ACTIVE TA_BUSY_avr SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VMEM"; do

@@ -140,3 +140,20 @@ def test_gemm_wr_partials_resid_rmsnorm(M, N, K, bn, S):
     assert rel_err(hb, hr) < 8e-3
     hf = hb.float()
     assert rel_err(out, hf * torch.rsqrt(hf.pow(2).mean(-1, keepdim=True) + 1e-5)) < 8e-3
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 4096, 4096), (300, 1024, 1536), (129, 768, 512)])
+def test_gemm_wr_two_wave_groups(M, N, K):
+    """ng = 2 (two wave groups split each tile's K range, partials combined through LDS; bn 128,
+    store epilogue) against fp32."""
+    import ctypes
+    h = hip()
+    a = _rnd(M, K)
+    w = _rnd(N, K, scale=0.02)
+    out = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=DEV)
+    ep = h.make_epi(out=out, ldo=N)
+    rc = h.lib().lsa_gemm_wr(h._p(a), K, h._p(packing.pack_b(w)), M, N, K, h.EPI_STORE, ctypes.byref(ep), 128, 256, 1, 2,
+                             h._stream())
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert rel_err(out, a.float() @ w.float().T) < 8e-3
