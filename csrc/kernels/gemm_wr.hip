@@ -56,7 +56,8 @@ struct WrGeo {
   static constexpr int ELD = TN + 4;                  // fp32 row stride of the epilogue image
   static constexpr int EPI_BYTES = NG * 4 * WR_BM * ELD * 4;  // NG = 2: group 1's partial image too
   static constexpr int RS_OFF = (NG * NS * WR_ABUF > EPI_BYTES ? NG * NS * WR_ABUF : EPI_BYTES);  // row rstd [128]
-  static constexpr int SMEM = RS_OFF + WR_BM * 4;
+  static constexpr int SS_OFF = RS_OFF + WR_BM * 4;  // EPI_RESID + ss_out: 16-column sums of squares [128][BN / 16]
+  static constexpr int SMEM = SS_OFF + WR_BM * (BN / 16) * 4;
   static_assert(SMEM <= 160 * 1024, "LDS budget");
   static_assert(2 * PER <= 63, "vmcnt range");
   static_assert(ADMA == 4, "one A DMA block per two rows of phase B");
@@ -286,15 +287,41 @@ LSA_DEVICE void gemm_wr_body(unsigned char* smem_all, const bf16_raw* __restrict
     }
     __syncthreads();  // the image and the row scales are complete
     const int col_base = nt * BN + w * TN;
+    float* s_ss = reinterpret_cast<float*>(smem_all + G_::SS_OFF);
+    constexpr int NU = (WR_BM * FN) / 64 / NG;  // unit passes per wave (NG = 2: the groups share each image)
 #pragma unroll
-    for (int s2 = 0; s2 < (WR_BM * FN) / 64; ++s2) {
-      if (grp != 0) break;  // NG = 2: group 0 owns the epilogue
-      const int u = lane + 64 * s2, row = u / FN, j = u % FN;
+    for (int s2 = 0; s2 < NU; ++s2) {
+      const int u = lane + 64 * (grp * NU + s2), row = u / FN, j = u % FN;
       const int m = m0 + row;
       float v[16];
 #pragma unroll
       for (int q = 0; q < 4; ++q) *reinterpret_cast<f32x4_t*>(v + 4 * q) = *reinterpret_cast<const f32x4_t*>(img + row * G_::ELD + j * 16 + 4 * q);
-      if (m < M) {
+      if (EPI == EPI_RESID) {
+        // residual add (+ bias); with ss_out, the sum of squares of the ROUNDED outputs of this
+        // 16-column unit, combined per 64-column block below in lsa_row_ss's order
+        float ssq = 0.f;
+        if (m < M) {
+          const int c0 = col_base + j * 16;
+          epi_bias16(ep, c0, v);
+          const bf16_raw* rr = ep.resid + (size_t)m * ep.ldr + c0;
+          float x0[8], x1[8];
+          unpack8(ld16(rr), x0);
+          unpack8(ld16(rr + 8), x1);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            x0[q] += v[q];
+            x1[q] += v[q + 8];
+          }
+          const u32x4_t p0 = pack8(x0), p1 = pack8(x1);
+          bf16_raw* o = ep.out + (size_t)m * ep.ldo + c0;
+          st16(o, p0);
+          st16(o + 8, p1);
+          unpack8(p0, x0);
+          unpack8(p1, x1);
+          ssq = ss16(x0, x1);
+        }
+        if (ep.ss_out) s_ss[row * (BN / 16) + w * FN + j] = ssq;
+      } else if (m < M) {
         if (EPI == EPI_QKV && ep.ss_in) {
           const float rsc = s_rs[row];
 #pragma unroll
@@ -309,6 +336,17 @@ LSA_DEVICE void gemm_wr_body(unsigned char* smem_all, const bf16_raw* __restrict
         }
       }
       __builtin_amdgcn_sched_barrier(0);
+    }
+    if (EPI == EPI_RESID && ep.ss_out) {  // per 64-column block: (s0 + s1) + (s2 + s3)
+      __syncthreads();
+      for (int r = threadIdx.x; r < WR_BM * (BN / 64); r += WR_NTHR * NG) {
+        const int row = r / (BN / 64), b = r % (BN / 64);
+        if (m0 + row < M) {
+          const float* sq = s_ss + row * (BN / 16) + 4 * b;
+          ep.ss_out[(size_t)(m0 + row) * ep.ss_n + ((nt * BN) >> 6) + b] =
+              __fadd_rn(__fadd_rn(sq[0], sq[1]), __fadd_rn(sq[2], sq[3]));
+        }
+      }
     }
     wr_vm_wait<0>();  // this tile's stores retired: the next item's counted waits see only its own loads
     wr_barrier();     // the image is dead before the next tile's DMA reuses the LDS
@@ -338,34 +376,40 @@ int wr_launch(const bf16_raw* A, int lda, const bf16_raw* W, int M, int N, int K
 }  // namespace
 
 // 128-row x bn tiles, weights straight into MFMA registers (see the header comment). epi:
-// EPI_STORE, EPI_QKV (with the fused-RMSNorm row scale when ep->ss_in is set: K == 64 ss_n) or
+// EPI_STORE, EPI_RESID (out = resid + y; with ep->ss_out, the fused RMSNorm's per-64-column sums of
+// squares of the rounded outputs, as gemm_sk), EPI_QKV (with the fused-RMSNorm row scale when
+// ep->ss_in is set: K == 64 ss_n) or
 // EPI_PARTIAL: every tile split into exactly `split` K ranges (multiples of 256), fp32 partial
 // k to ((float*)ep->out)[k][M][ldo] (lsa_resid_rmsnorm_partials sums them); the caller checks
 // the buffer holds split * M * ldo floats. bn: 128 / 192 / 256 with N % bn == 0; K % 256 == 0;
 // grid: workgroups (work items beyond it loop). ng = 2 (experimental: two wave groups split
-// each tile's K range; bn 128, EPI_STORE, split 1, K % 512 == 0). Returns LSA_BAD_SHAPE on any
+// each tile's K range; bn 128, EPI_STORE / EPI_RESID, split 1, K % 512 == 0). Returns LSA_BAD_SHAPE on any
 // shape the kernel's indexing cannot take.
 extern "C" int lsa_gemm_wr(const void* a, int lda, const void* wp, int M, int N, int K, int epi, const EpiArgs* ep,
                            int bn, int grid, int split, int ng, hipStream_t stream) {
   if (M < 1 || K < 4 * WR_BK || K % (4 * WR_BK) || lda < K || lda % 8 || grid < 1 || !ep) return LSA_BAD_SHAPE;
   if (bn != 128 && bn != 192 && bn != 256) return LSA_UNSUPPORTED;
   if (N % bn) return LSA_BAD_SHAPE;
-  if (epi != EPI_STORE && epi != EPI_QKV && epi != EPI_PARTIAL) return LSA_UNSUPPORTED;
+  if (epi != EPI_STORE && epi != EPI_QKV && epi != EPI_PARTIAL && epi != EPI_RESID) return LSA_UNSUPPORTED;
   if (split < 1 || (split > 1 && epi != EPI_PARTIAL) || split > K / (4 * WR_BK)) return LSA_BAD_SHAPE;
   if (epi == EPI_PARTIAL && (!ep->out || ep->ldo < N || ep->ldo % 4)) return LSA_BAD_SHAPE;
   if (epi == EPI_STORE && (!ep->out || ep->ldo < N || ep->ldo % 8)) return LSA_BAD_SHAPE;
   if (epi == EPI_QKV && (!ep->k_cache || !ep->v_cache || !ep->slot || !ep->pos || !ep->out)) return LSA_BAD_SHAPE;
-  if (ep->ss_out) return LSA_UNSUPPORTED;
+  if (epi == EPI_RESID && (!ep->out || !ep->resid || ep->ldo < N || ep->ldo % 8 || ep->ldr < N || ep->ldr % 8))
+    return LSA_BAD_SHAPE;
+  if (ep->ss_out && (epi != EPI_RESID || N % 64 || ep->ss_n != N / 64)) return LSA_BAD_SHAPE;
   if (ep->ss_in && (epi != EPI_QKV || ep->ss_n < 4 || ep->ss_n % 4 || K != 64 * ep->ss_n)) return LSA_BAD_SHAPE;
   if (ng != 1 && ng != 2) return LSA_UNSUPPORTED;
   const bf16_raw* A = static_cast<const bf16_raw*>(a);
   const bf16_raw* W = static_cast<const bf16_raw*>(wp);
   if (ng == 2) {
-    if (bn != 128 || epi != EPI_STORE || split != 1) return LSA_UNSUPPORTED;
+    if (bn != 128 || (epi != EPI_STORE && epi != EPI_RESID) || split != 1) return LSA_UNSUPPORTED;
     if (K % (8 * WR_BK)) return LSA_BAD_SHAPE;
-    return wr_launch<2, EPI_STORE, 2>(A, lda, W, M, N, K, *ep, grid, 1, stream);
+    return epi == EPI_RESID ? wr_launch<2, EPI_RESID, 2>(A, lda, W, M, N, K, *ep, grid, 1, stream)
+                            : wr_launch<2, EPI_STORE, 2>(A, lda, W, M, N, K, *ep, grid, 1, stream);
   }
 #define LSA_WR(FN)                                                                                     \
+  if (epi == EPI_RESID) return wr_launch<FN, EPI_RESID>(A, lda, W, M, N, K, *ep, grid, split, stream); \
   return epi == EPI_QKV     ? wr_launch<FN, EPI_QKV>(A, lda, W, M, N, K, *ep, grid, split, stream)     \
          : epi == EPI_PARTIAL ? wr_launch<FN, EPI_PARTIAL>(A, lda, W, M, N, K, *ep, grid, split, stream) \
                               : wr_launch<FN, EPI_STORE>(A, lda, W, M, N, K, *ep, grid, split, stream);

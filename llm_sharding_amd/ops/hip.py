@@ -16,7 +16,7 @@ import functools
 import json
 import os
 from contextlib import contextmanager
-from typing import Optional
+from typing import Optional, Tuple
 
 import torch
 
@@ -309,9 +309,9 @@ def gemm(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep
     ``sk`` its split-K factor (0 = :func:`gemm_split`; > 1 uses ``ws``)."""
     if not legacy and N % 128 == 0 and K % 64 == 0 and epi != EPI_ARGMAX and a.stride(0) % 8 == 0 \
             and a.data_ptr() % 16 == 0:
-        bn = gemm_wr_plan(M, N, K, epi, ep)
-        if bn:
-            gemm_wr(a, wp, M, N, K, epi, ep, bn=bn)
+        wr = gemm_wr_plan(M, N, K, epi, ep)
+        if wr:
+            gemm_wr(a, wp, M, N, K, epi, ep, bn=wr[0], ng=wr[1])
         else:
             gemm_sk(a, wp, M, N, K, epi, ep, ws=sk_ws)
         return
@@ -345,44 +345,61 @@ def gemm(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep
 SK_BM = 256  # gemm_sk.hip row tile (default; 128-row tiles for small / odd M: plan field bm)
 
 # gemm_wr.hip (weights streamed into MFMA registers, 128 x bn tiles, one round of whole-K tiles)
-# where it measured faster than gemm_sk's best plan: one round of 224-256 whole 128 x 192 tiles,
-# i.e. the 7B qkv projection at 448-512 rows (54-55 us vs 59-81 us, profiles/r3_gemm_wr.md).
-# LSA_GEMM_WR=0 turns it off (A/B runs).
+# where it measured faster than gemm_sk's best plan (profiles/r3_gemm_wr.md):
+# * one round of 224-256 whole 128 x 192 tiles with a store / QKV epilogue, i.e. the 7B qkv
+#   projection at 448-512 rows (54-55 us vs 59-81 us);
+# * opt-in (LSA_GEMM_WR_RESID=1): the residual projection with 4 row tiles x 28-32 128-column
+#   tiles (the 7B o projection at 448-512 rows) on two wave groups per tile (ng = 2), fused-RMSNorm
+#   sums of squares included - faster than gemm_sk in isolation with cold weights (39.4 vs 45.8
+#   us) but 1.5 % slower per headline step in the engine (13.59-13.63 vs 13.38-13.40 ms), so off.
+# LSA_GEMM_WR=0 turns both off (A/B runs).
 WR_TILES = (224, 256)
+WR_RESID_TILES = (112, 128)
 
 
-def gemm_wr_plan(M: int, N: int, K: int, epi: int, ep: "EpiArgs") -> int:
-    """bn for :func:`gemm_wr`, or 0 when gemm_sk takes the shape."""
-    if os.environ.get("LSA_GEMM_WR", "1") == "0" or epi not in (EPI_STORE, EPI_QKV) or ep.ss_out or ep.act \
-            or ep.bias or K % 256 or N % 192:
-        return 0
+def gemm_wr_plan(M: int, N: int, K: int, epi: int, ep: "EpiArgs") -> Optional[Tuple[int, int]]:
+    """(bn, ng) for :func:`gemm_wr`, or None when gemm_sk takes the shape."""
+    if os.environ.get("LSA_GEMM_WR", "1") == "0" or ep.act or ep.bias:
+        return None
     mt = -(-M // 128)
-    tiles = mt * (N // 192)
     # the last row tile at least half full: the kernel computes whole 128-row tiles, gemm_sk's
     # 128-row plans do not (measured at 448 and 512 rows)
-    return 192 if WR_TILES[0] <= tiles <= WR_TILES[1] and M - (mt - 1) * 128 >= 64 else 0
+    if M - (mt - 1) * 128 < 64:
+        return None
+    if epi in (EPI_STORE, EPI_QKV) and not ep.ss_out and K % 256 == 0 and N % 192 == 0 \
+            and WR_TILES[0] <= mt * (N // 192) <= WR_TILES[1]:
+        return 192, 1
+    if epi == EPI_RESID and os.environ.get("LSA_GEMM_WR_RESID", "0") == "1" and K % 512 == 0 and N % 128 == 0 \
+            and mt == 4 and WR_RESID_TILES[0] <= mt * (N // 128) <= WR_RESID_TILES[1]:
+        return 128, 2
+    return None
 
 
 def gemm_wr(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep: EpiArgs, bn: int = 192,
-            grid: int = 0, split: int = 1, out_numel: int = 0) -> None:
+            grid: int = 0, split: int = 1, out_numel: int = 0, ng: int = 1) -> None:
     """Projection GEMM with the weights fetched straight into MFMA B registers (gemm_wr.hip):
-    128 x ``bn`` tiles, one per workgroup per round, A staged by LDS-DMA, EPI_STORE / EPI_QKV
-    (with the fused RMSNorm row scale, ``ep.ss_in``) / EPI_PARTIAL (every tile split into
-    ``split`` K ranges of multiples of 256; fp32 partial k to ``ep.out`` [k][M][ldo], summed by
-    :func:`resid_rmsnorm_partials`; ``out_numel`` = the buffer's capacity in floats, checked).
-    K % 256 == 0, N % bn == 0."""
+    128 x ``bn`` tiles, one per workgroup per round, A staged by LDS-DMA, EPI_STORE / EPI_RESID
+    (with the fused-RMSNorm sums of squares, ``ep.ss_out``) / EPI_QKV (with the fused RMSNorm row
+    scale, ``ep.ss_in``) / EPI_PARTIAL (every tile split into ``split`` K ranges of multiples of
+    256; fp32 partial k to ``ep.out`` [k][M][ldo], summed by :func:`resid_rmsnorm_partials`;
+    ``out_numel`` = the buffer's capacity in floats, checked). K % 256 == 0, N % bn == 0.
+    ``ng`` = 2: two wave groups per tile, each over half the K range (bn 128, EPI_STORE /
+    EPI_RESID, K % 512 == 0)."""
     _req(_is_bf16_cuda(a, wp), "gemm_wr: bf16 cuda tensors required")
     _req(wp.numel() == N * K and K % 256 == 0, "gemm_wr: packed weight shape (K % 256 == 0)")
     _req(a.dim() == 2 and a.shape[0] >= M >= 1 and a.shape[1] >= K and a.stride(1) == 1 and a.stride(0) % 8 == 0
          and a.data_ptr() % 16 == 0, "gemm_wr: A must be [>=M, >=K] row-major with 16-B aligned rows")
     _req(bn in (128, 192, 256) and N % bn == 0, f"gemm_wr: N={N} does not tile by bn={bn}")
-    _req(epi in (EPI_STORE, EPI_QKV, EPI_PARTIAL) and not ep.ss_out, "gemm_wr: EPI_STORE / EPI_QKV / EPI_PARTIAL")
+    _req(epi in (EPI_STORE, EPI_QKV, EPI_PARTIAL, EPI_RESID), "gemm_wr: EPI_STORE / EPI_RESID / EPI_QKV / EPI_PARTIAL")
+    _req(not ep.ss_out or (epi == EPI_RESID and N % 64 == 0 and ep.ss_n == N // 64), "gemm_wr: ss_out shape")
     _req(split == 1 or (epi == EPI_PARTIAL and 1 <= split <= K // 256), f"gemm_wr: split {split}")
+    _req(ng == 1 or (ng == 2 and bn == 128 and epi in (EPI_STORE, EPI_RESID) and split == 1 and K % 512 == 0),
+         f"gemm_wr: ng {ng} (2: bn 128, store / resid, K % 512 == 0)")
     if epi == EPI_PARTIAL:
         _req(out_numel >= split * M * ep.ldo, f"gemm_wr partial: output holds {out_numel} floats, "
              f"split {split} x {M} rows x ldo {ep.ldo} needed")
     _check_epi(epi, ep, N)
-    rc = lib().lsa_gemm_wr(_p(a), a.stride(0), _p(wp), M, N, K, epi, ctypes.byref(ep), bn, grid or N_CU, split, 1,
+    rc = lib().lsa_gemm_wr(_p(a), a.stride(0), _p(wp), M, N, K, epi, ctypes.byref(ep), bn, grid or N_CU, split, ng,
                            _stream())
     _check(rc, "lsa_gemm_wr")
 

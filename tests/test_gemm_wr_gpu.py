@@ -101,12 +101,12 @@ def test_gemm_dispatches_wr_for_one_round_of_192_tiles(monkeypatch):
     everything else to gemm_sk; LSA_GEMM_WR=0 turns it off."""
     h = hip()
     ep = h.make_epi(out=torch.empty(1, 1, device=DEV))
-    assert h.gemm_wr_plan(512, 12288, 4096, h.EPI_QKV, ep) == 192
-    assert h.gemm_wr_plan(512, 12288, 4096, h.EPI_SWIGLU, ep) == 0
-    assert h.gemm_wr_plan(2048, 12288, 4096, h.EPI_QKV, ep) == 0
-    assert h.gemm_wr_plan(512, 4096, 4096, h.EPI_STORE, ep) == 0
+    assert h.gemm_wr_plan(512, 12288, 4096, h.EPI_QKV, ep) == (192, 1)
+    assert h.gemm_wr_plan(512, 12288, 4096, h.EPI_SWIGLU, ep) is None
+    assert h.gemm_wr_plan(2048, 12288, 4096, h.EPI_QKV, ep) is None
+    assert h.gemm_wr_plan(512, 4096, 4096, h.EPI_STORE, ep) is None
     monkeypatch.setenv("LSA_GEMM_WR", "0")
-    assert h.gemm_wr_plan(512, 12288, 4096, h.EPI_QKV, ep) == 0
+    assert h.gemm_wr_plan(512, 12288, 4096, h.EPI_QKV, ep) is None
     monkeypatch.delenv("LSA_GEMM_WR")
     calls = []
     real = h.gemm_wr
@@ -146,14 +146,36 @@ def test_gemm_wr_partials_resid_rmsnorm(M, N, K, bn, S):
 def test_gemm_wr_two_wave_groups(M, N, K):
     """ng = 2 (two wave groups split each tile's K range, partials combined through LDS; bn 128,
     store epilogue) against fp32."""
-    import ctypes
     h = hip()
     a = _rnd(M, K)
     w = _rnd(N, K, scale=0.02)
     out = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=DEV)
-    ep = h.make_epi(out=out, ldo=N)
-    rc = h.lib().lsa_gemm_wr(h._p(a), K, h._p(packing.pack_b(w)), M, N, K, h.EPI_STORE, ctypes.byref(ep), 128, 256, 1, 2,
-                             h._stream())
-    assert rc == 0
+    h.gemm_wr(a, packing.pack_b(w), M, N, K, h.EPI_STORE, h.make_epi(out=out, ldo=N), bn=128, ng=2)
     torch.cuda.synchronize()
     assert rel_err(out, a.float() @ w.float().T) < 8e-3
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 4096, 4096), (450, 4096, 4096), (300, 1024, 1536), (129, 768, 512)])
+@pytest.mark.parametrize("bn,ng", [(128, 2), (128, 1), (192, 1), (256, 1)])
+@pytest.mark.parametrize("ss", [False, True])
+def test_gemm_wr_resid_ss_out(M, N, K, bn, ng, ss):
+    """EPI_RESID in place on the residual stream (out = resid = h) against fp32; with ss_out, the
+    per-64-column sums of squares equal lsa_row_ss over the rounded outputs bit for bit (the
+    fused RMSNorm of the next projection sees the same bits either way)."""
+    if N % bn or (ng == 2 and K % 512):
+        pytest.skip("shape does not tile")
+    h = hip()
+    a = _rnd(M, K)
+    w = _rnd(N, K, scale=0.02)
+    hbuf = _rnd(M, N)
+    want = hbuf.float() + a.float() @ w.float().T
+    ssb = torch.full((M, N // 64), float("nan"), device=DEV) if ss else None
+    ep = h.make_epi(out=hbuf, resid=hbuf, ldo=N, ldr=N, ss_out=ssb)
+    h.gemm_wr(a, packing.pack_b(w), M, N, K, h.EPI_RESID, ep, bn=bn, ng=ng)
+    torch.cuda.synchronize()
+    assert rel_err(hbuf, want) < 8e-3
+    if ss:
+        ref = torch.empty_like(ssb)
+        h.row_ss(hbuf, M, ref)
+        torch.cuda.synchronize()
+        assert torch.equal(ssb, ref)
