@@ -14,7 +14,9 @@ the master that calls ``ConfigSender``; the repository only ships a hand-written
 4. failure detection / elastic recovery: :meth:`health` pings every
    controller's config port (``ping`` -> ``pong`` with its status); :meth:`failover` drops
    the devices that stopped answering, re-plans the layers over the survivors and hot
-   re-configures them (the reference's live re-shard path, ``node_worker.py:445-474``);
+   re-configures them (the reference's live re-shard path, ``node_worker.py:445-474``); a
+   deployed pipeline (item 5) that lost a rank is first dropped by its survivors, which then
+   serve as a ZMQ chain (a torchrun world cannot shrink);
 5. the RCCL deployment on one node (BASELINE north star: "the master_node scheduler places
    shards on the 8 GPUs of one node"): :meth:`deploy_pipeline` plans the stages over the
    controllers of a torchrun job (``start_node.py --backend rccl``: controller i = rank i =
@@ -174,19 +176,18 @@ class MasterNode:
 
     def failover(self, timeout_ms: int = 2000) -> list:
         """Ping the deployed chain; if any controller is dead, re-plan over the devices that
-        answered and redeploy. Returns the list of dropped devices (empty if all alive)."""
+        answered and redeploy. Returns the list of dropped devices (empty if all alive). A
+        deployed pipeline that lost a rank is dropped by its survivors first
+        (:meth:`_drop_pipeline`) and they are re-deployed as a chain."""
         status = self.health(timeout_ms)
         dead = [d for d, st in status if st is None]
         if not dead:
             return []
-        if self.mode == "pipeline":
-            # an RCCL job cannot lose a rank and continue: the torchrun world is fixed (a slow
-            # but live rank is re-balanced with replan(speeds=...) instead)
-            raise RuntimeError(f"[ERROR] pipeline ranks unreachable: {[(d.host, d.config_port) for d in dead]}; "
-                               "restart the torchrun job and redeploy")
         alive = [d for d, st in status if st is not None]
         if not alive:
             raise RuntimeError("[ERROR] every controller is unreachable")
+        if self.mode == "pipeline":
+            self._drop_pipeline(alive, timeout_ms)
         self.devices = [d for d in self.devices if d not in dead]
         self.plan = None
         for s in self.senders:
@@ -194,6 +195,28 @@ class MasterNode:
         self.senders = []
         self.deploy(timeout_ms=max(timeout_ms, 10000))
         return dead
+
+    def _drop_pipeline(self, alive: list, timeout_ms: int, drop_timeout_s: float = 120.0) -> None:
+        """A torchrun world cannot lose a rank and go on (a slow but live rank is re-balanced with
+        :meth:`replan` instead), so the survivors leave it: ``abort_pipeline`` to every live rank
+        (the others first, acknowledged, then rank 0, which stops scheduling), each rank drops its
+        stage and process groups (NodeController._drop_pipeline) and waits; the caller then
+        re-deploys them as a ZMQ chain. Ranks blocked on the dead one fail on its closed
+        connections and drop out the same way."""
+        ing = self.plan.stages[0].device if self.plan is not None else self.devices[0]
+        for d in [d for d in alive if d is not ing] + [d for d in alive if d is ing]:
+            if ping_node(d.host, d.config_port, timeout_ms, command="abort_pipeline") is None:
+                raise RuntimeError(f"[ERROR] pipeline rank {d.host}:{d.config_port} did not acknowledge the abort; "
+                                   "restart the torchrun job and redeploy")
+        deadline = time.monotonic() + drop_timeout_s
+        while True:
+            st = [ping_node(d.host, d.config_port, timeout_ms) for d in alive]
+            if all(x is not None and x.get("mode") != "pipeline" for x in st):
+                break
+            if time.monotonic() > deadline:
+                raise RuntimeError(f"[ERROR] pipeline ranks did not drop their stages: {st}; restart the torchrun job")
+            time.sleep(0.2)
+        self.mode = "chain"
 
     def submit(self, text: str = "", input_ids=None, max_new_tokens: Optional[int] = None,
                reply_to: Optional[str] = None) -> None:

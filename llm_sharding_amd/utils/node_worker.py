@@ -30,6 +30,10 @@ NodeWorker - micro-batched continuous batching, hidden states over RCCL on one c
 per ring edge, hipGraph decode replays, tokens on the device. Rank 0 is the ingress: its config
 port takes the reference ``user_request`` messages (optionally with ``reply_to``) and
 ``shutdown``. No cos/sin tables travel (every stage derives positions from its own KV state).
+A pipeline that loses a rank is dropped by the survivors - on a peer's closed connection, or on
+the master's ``abort_pipeline`` (then, if still blocked inside a communicator op after
+``ABORT_GRACE_S``, by aborting its process groups) - which release their stages and groups and
+wait for the master's re-deployment as a ZMQ chain (``MasterNode.failover``).
 
 On ROCm devices the engine computes in bfloat16: ``dtype=torch.float16`` is accepted (the
 reference default) and mapped to bfloat16 with a notice.
@@ -399,6 +403,7 @@ class NodeController:
                     "uptime_s": time.monotonic() - self.t_boot}
         w = self.node_worker
         return {"listen_port": self.listen_port, "configured": w is not None,
+                "pipeline_lost": getattr(self, "pipeline_lost", None),
                 "shards": [w.start, w.end] if w is not None else None,
                 "ingress": bool(w.can_receive_user_request) if w is not None else False,
                 "forwarded": self.forwarded, "finished_requests": len(self.finished_outputs),
@@ -474,16 +479,33 @@ class NodeController:
 
     def _run_pipeline(self, max_new_tokens: int) -> None:
         """Pipeline mode: rank 0 reads requests from its config port on a thread and schedules;
-        the other ranks follow rank 0's commands until it stops (``shutdown``)."""
+        the other ranks follow rank 0's commands until it stops (``shutdown``). Returns True if
+        the pipeline was dropped because a rank was lost (a peer's error, or the master's
+        ``abort_pipeline`` from :meth:`MasterNode.failover`)."""
         import threading
         from ..parallel.ingress import Replies, run_ingress
+        lost = None
         stop = threading.Event()
+        serving = threading.Event()
+        serving.set()
+        self._aborted = False
 
         def other(msg):
             if not isinstance(msg, dict):
                 return
             if msg.get("command") == "ping":
                 self._pong(msg)
+            elif msg.get("command") == "abort_pipeline":
+                # the master lost a rank of this torchrun world (MasterNode.failover): rank 0 stops
+                # scheduling, every rank drops its pipeline and waits for a chain re-deployment
+                self._aborted = True
+                self._pong(msg)
+                # a rank still inside an RCCL op with the dead peer after the grace period cannot
+                # see a closed connection (gloo can): abort its communicators so the op fails
+                # (ncclCommAbort) instead of waiting for the watchdog
+                t = threading.Timer(self.ABORT_GRACE_S, self._abort_groups, args=(serving,))
+                t.daemon = True
+                t.start()
             elif msg.get("command") == "replan" or (msg.get("mode") == "pipeline" and "stages" in msg):
                 # live re-shard of the deployed pipeline (reference hot re-config, node_worker.py
                 # :445-474): rank 0 owns the command stream, so the new split is applied there,
@@ -504,7 +526,11 @@ class NodeController:
             th = threading.Thread(target=run_ingress, args=(self.server, self.recv_config_socket, self.tokenizer,
                                                             stop, max_new_tokens, replies, other), daemon=True)
             th.start()
-            self.server.serve(stop_when_idle=False, should_stop=stop.is_set)
+            try:
+                self.server.serve(stop_when_idle=False, should_stop=lambda: stop.is_set() or self._aborted)
+            except Exception as e:  # noqa: BLE001 - a peer rank died mid-collective
+                lost = repr(e)
+            serving.clear()
             stop.set()
             th.join(timeout=5)
             replies.close()
@@ -519,10 +545,70 @@ class NodeController:
                     other(msg)
             th = threading.Thread(target=pings, daemon=True)
             th.start()
-            self.server.serve()
+            try:
+                self.server.serve()
+            except Exception as e:  # noqa: BLE001 - a peer rank died mid-collective
+                lost = repr(e)
+            serving.clear()
             stop.set()
             th.join(timeout=5)
         self.running = False
+        if lost is None and not self._aborted:
+            return False
+        self._drop_pipeline(lost or "aborted by the master")
+        return True
+
+    ABORT_GRACE_S = 10.0  # abort_pipeline -> communicator abort if this rank is still serving
+
+    @staticmethod
+    def _abort_groups(serving) -> None:
+        if not serving.is_set():
+            return
+        import torch.distributed.distributed_c10d as c10d
+        _log("[ERROR] still blocked in the pipeline after the abort grace period: aborting its process groups")
+        try:
+            c10d._abort_process_group()
+        except Exception as e:  # noqa: BLE001
+            _log(f"[WARNING] process-group abort: {e}")
+
+    def _drop_pipeline(self, reason: str) -> None:
+        """The torchrun world lost a rank: release this rank's stage and its process groups (which
+        closes its connections, so peers still blocked on it fail too and drop theirs) and fall
+        back to the ZMQ chain transport for the master's re-deployment over the survivors."""
+        import gc
+        import torch.distributed as dist
+        _log(f"[ERROR] pipeline dropped ({reason}); waiting for the master's chain re-deployment")
+        self.server = None
+        gc.collect()
+        if dist.is_initialized():
+            try:
+                dist.destroy_process_group()
+            except Exception as e:  # noqa: BLE001
+                _log(f"[WARNING] destroy_process_group: {e}")
+        self.backend = "tcp"
+        self.pipeline_lost = reason
+
+    def _await_redeploy(self) -> bool:
+        """After :meth:`_drop_pipeline`: answer pings until a (chain) config arrives and apply it;
+        False if a ``shutdown`` came first."""
+        while True:
+            try:
+                raw = self.recv_config_socket.recv_bytes(200)
+            except Again:
+                continue
+            msg = json.loads(raw.decode())
+            cmd = msg.get("command") if isinstance(msg, dict) else None
+            if cmd == "shutdown":
+                return False
+            if cmd in ("ping", "user_request", "abort_pipeline"):
+                self._pong(msg) if cmd != "user_request" else self.pending_requests.append(msg)
+                continue
+            if msg.get("mode") == "pipeline":
+                _log("[ERROR] a pipeline config after a lost rank: restart the torchrun job to redeploy one")
+                continue
+            self.received_config = msg
+            self._apply_new_role(msg)
+            return True
 
     def _set_first_node_addr(self, cfg: dict) -> None:
         new = cfg.get("first_node_addr", "") if cfg.get("can_receive_user_request") else ""
@@ -625,8 +711,9 @@ class NodeController:
         """Serve until a ``shutdown`` command arrives (or ``max_idle_s`` without traffic)."""
         self.running = True
         if self.server is not None:
-            self._run_pipeline(max_new_tokens)
-            return
+            if not self._run_pipeline(max_new_tokens) or not self._await_redeploy():
+                return
+            self.running = True  # re-deployed as a chain stage over the survivors
         idle_since = time.monotonic()
         while self.running:
             try:
@@ -669,16 +756,17 @@ def send_user_request(node_ip: str, port: int, text: str = "", input_ids=None, m
     s.close(linger_ms=5000)
 
 
-def ping_node(node_ip: str, port: int, timeout_ms: int = 2000) -> Optional[dict]:
+def ping_node(node_ip: str, port: int, timeout_ms: int = 2000, command: str = "ping") -> Optional[dict]:
     """Liveness probe: send ``ping`` to a controller's config port and wait for its ``pong``
-    (its :meth:`NodeController.status`). Returns None if no answer within ``timeout_ms``."""
+    (its :meth:`NodeController.status`). Returns None if no answer within ``timeout_ms``.
+    ``command="abort_pipeline"``: the same exchange, asking a pipeline rank to drop its stage."""
     import secrets
     reply = PullSocket("tcp://127.0.0.1:0" if node_ip in ("127.0.0.1", "localhost") else "tcp://*:0")
     host = "127.0.0.1" if node_ip in ("127.0.0.1", "localhost") else local_ip()
     nonce = secrets.randbits(31)
     s = PushSocket(f"tcp://{node_ip}:{port}")
     try:
-        s.send_bytes(json.dumps({"command": "ping", "nonce": nonce, "reply_to": f"tcp://{host}:{reply.port}"}).encode())
+        s.send_bytes(json.dumps({"command": command, "nonce": nonce, "reply_to": f"tcp://{host}:{reply.port}"}).encode())
         deadline = time.monotonic() + timeout_ms / 1e3
         while True:
             left = int((deadline - time.monotonic()) * 1e3)

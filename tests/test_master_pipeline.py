@@ -10,12 +10,14 @@ address and receives the finished outputs, which must equal the fp32 golden mode
 generation token for token."""
 import multiprocessing as mp
 import socket
+import time
 
 import pytest
 import torch
 
 from llm_sharding_amd.models import weights as W
 from llm_sharding_amd.models.reference import ReferenceLlama
+from llm_sharding_amd.utils.node_worker import ping_node
 
 
 def _ports(n):
@@ -40,13 +42,15 @@ def _node(rank, world, port, cfg_port, shards, q):
                               verbose=False)
         assert ctrl.server is not None and ctrl.status()["mode"] == "pipeline"
         ctrl.run_worker_loop(max_new_tokens=8)
-        q.put((rank, ctrl.finished_outputs if rank == 0 else "ok"))
+        outs = [o.reshape(-1).tolist() if torch.is_tensor(o) else o for o in ctrl.finished_outputs]  # chain: tensors
+        q.put((rank, outs if rank == 0 else "ok"))
         ctrl.close()
     except Exception as e:  # noqa: BLE001
         q.put((rank, repr(e)))
         raise
     finally:
-        dist.destroy_process_group()
+        if dist.is_initialized():  # (a pipeline that lost a rank has destroyed it already)
+            dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("world", [4])
@@ -195,3 +199,73 @@ def test_master_replans_live_pipeline_token_exact(tiny8_shards):
     for prompts, outs in zip(rounds, got):
         assert outs == _golden(tiny8_shards, prompts, n_new), (prompts, outs)
     assert inflight == _golden(tiny8_shards, [[5, 6, 7, 8]], n_new)[0]
+
+
+def test_pipeline_failover_to_chain_token_exact(tiny8_shards):
+    """Failure of a DEPLOYED pipeline rank (reference failure handling is a
+    restart): 4 ranks serve, rank 2's process is killed, MasterNode.failover() notices it (no
+    pong), the survivors drop the torchrun world (abort_pipeline -> each releases its stage and
+    process groups) and are re-deployed as a 3-stage ZMQ chain over the same layers; requests
+    before and after the failure produce the fp32 golden model's greedy tokens."""
+    from llm_sharding_amd.parallel import protocol
+    from llm_sharding_amd.parallel.scheduler import DeviceSpec
+    from llm_sharding_amd.parallel.transport import PullSocket
+    from llm_sharding_amd.utils.master_node import MasterNode
+    world, n_new = 4, 6
+    port = _ports(1)[0]
+    cfg_ports, data_ports = _ports(world), _ports(world)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_node, args=(r, world, port, cfg_ports[r], tiny8_shards, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    reply = PullSocket("tcp://127.0.0.1:0")
+    before = [[1, 33, 44, 55, 66], [7, 8, 9]]
+    after = [1, 40, 41, 42]
+    res = {}
+    try:
+        devs = [DeviceSpec(host="127.0.0.1", config_port=cfg_ports[i], data_port=data_ports[i]) for i in range(world)]
+        master = MasterNode.from_shards(tiny8_shards, devs)
+        master.deploy_pipeline(batch=2, microbatches=world, max_seq=64, prefill_budget=64)
+        for pr in before:
+            master.submit(input_ids=[pr], max_new_tokens=n_new, reply_to=f"tcp://127.0.0.1:{reply.port}")
+        got = {}
+        for _ in before:
+            m = protocol.decode(reply.recv_bytes(timeout_ms=120000))
+            got[m["request_id"]] = m["output_ids"]
+        assert master.failover(1000) == []
+        ps[2].kill()
+        ps[2].join(timeout=30)
+        dropped = master.failover(1000)
+        assert [d.config_port for d in dropped] == [cfg_ports[2]]
+        assert master.mode == "chain" and len(master.plan.stages) == 3
+        assert master.plan.stages[0].start == 0 and master.plan.stages[-1].end == 8
+        t0 = time.time()
+        while True:  # every survivor re-configured with its chain range
+            st = dict((d.config_port, x) for d, x in master.health(1000))
+            if all(x and x["configured"] and x["shards"] == [sg.start, sg.end] and x["pipeline_lost"]
+                   for sg, x in ((sg, st[sg.device.config_port]) for sg in master.plan.stages)):
+                break
+            assert time.time() - t0 < 120, st
+        master.submit(input_ids=[after])
+        ing = master.plan.stages[0].device
+        t0 = time.time()
+        while (ping_node(ing.host, ing.config_port, 1000) or {}).get("finished_requests", 0) < len(before) + 1:
+            assert time.time() - t0 < 120
+            time.sleep(0.2)
+        master.shutdown()
+        for _ in range(world - 1):
+            r, v = q.get(timeout=120)
+            res[r] = v
+    finally:
+        reply.close()
+        for p in ps:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    assert sorted(res) == [0, 1, 3] and res[1] == "ok" and res[3] == "ok", res
+    assert all(ps[r].exitcode == 0 for r in (0, 1, 3)), [p.exitcode for p in ps]
+    assert [got[i] for i in range(len(before))] == _golden(tiny8_shards, before, n_new)
+    # the chain stage generates the controller's max_new_tokens (8) after the prompt
+    chain_out = res[0][-1]
+    assert chain_out == after + _golden(tiny8_shards, [after], 8)[0], chain_out
