@@ -375,8 +375,12 @@ class NodeController:
             msg = json.loads(raw.decode())
             if isinstance(msg, dict) and msg.get("command") in ("user_request", "shutdown", "ping"):
                 self._handle_command(msg)
-                if no_block:
-                    continue
+                continue
+            if isinstance(msg, dict) and "command" in msg:
+                # commands of another mode (abort_pipeline / replan outside a pipeline): acknowledged
+                # (so a master waiting on them does not stall) and otherwise ignored - never a config
+                _log(f"[WARNING] command {msg['command']!r} ignored: no pipeline deployed here")
+                self._pong(msg)
                 continue
             if self.verbose:
                 _log("[CONFIG] Received configuration file from master node:")

@@ -262,6 +262,32 @@ def test_worker_role_errors(tiny_shards):
     w.close()
 
 
+def test_foreign_command_is_not_a_config(tiny_shards):
+    """A command of another mode (the master's abort_pipeline sent during a failover, a replan)
+    reaching an unconfigured controller is acknowledged and ignored; the next real config is
+    the one applied."""
+    from llm_sharding_amd.utils.node_worker import ping_node
+    cport, dport = free_ports(2)
+    ctrl = NodeController(tiny_shards, device="cpu", dtype=torch.float32, listen_port=cport, wait_config=False,
+                          verbose=False)
+    box = {}
+    th = threading.Thread(target=lambda: box.update(cfg=ctrl._receive_config()), daemon=True)
+    th.start()
+    try:
+        assert ping_node("127.0.0.1", cport, 5000, command="abort_pipeline") is not None
+        s = PushSocket(f"tcp://127.0.0.1:{cport}")
+        s.send_bytes(json.dumps({"command": "replan", "stages": [[0, 2]]}).encode())
+        s.close(linger_ms=2000)
+        cs = ConfigSender(node_port=cport)
+        cs.build_config(0, 2, True, f"tcp://*:{dport}", f"tcp://127.0.0.1:{dport}",
+                        first_node_addr=f"tcp://127.0.0.1:{cport}")
+        assert cs.send_config("127.0.0.1", 5000)
+        th.join(timeout=30)
+        assert box["cfg"]["shards_start"] == 0 and box["cfg"]["shards_end"] == 2 and "command" not in box["cfg"]
+    finally:
+        ctrl.close()
+
+
 def _rccl_chain_worker(rank, port, ports, shards, n_new, q):
     import torch.distributed as dist
     from llm_sharding_amd.utils.node_worker import NodeWorker
