@@ -180,6 +180,10 @@ class MasterNode:
         deployed pipeline that lost a rank is dropped by its survivors first
         (:meth:`_drop_pipeline`) and they are re-deployed as a chain."""
         status = self.health(timeout_ms)
+        for _ in range(2):  # a silent controller is pinged twice more before it counts as dead
+            if all(st is not None for _, st in status):
+                break
+            status = [(d, st if st is not None else ping_node(d.host, d.config_port, timeout_ms)) for d, st in status]
         dead = [d for d, st in status if st is None]
         if not dead:
             return []
@@ -204,11 +208,12 @@ class MasterNode:
         re-deploys them as a ZMQ chain. Ranks blocked on the dead one fail on its closed
         connections and drop out the same way."""
         ing = self.plan.stages[0].device if self.plan is not None else self.devices[0]
-        for d in [d for d in alive if d is not ing] + [d for d in alive if d is ing]:
-            if ping_node(d.host, d.config_port, timeout_ms, command="abort_pipeline") is None:
-                raise RuntimeError(f"[ERROR] pipeline rank {d.host}:{d.config_port} did not acknowledge the abort; "
-                                   "restart the torchrun job and redeploy")
         deadline = time.monotonic() + drop_timeout_s
+        for d in [d for d in alive if d is not ing] + [d for d in alive if d is ing]:
+            while ping_node(d.host, d.config_port, timeout_ms, command="abort_pipeline") is None:
+                if time.monotonic() > deadline:
+                    raise RuntimeError(f"[ERROR] pipeline rank {d.host}:{d.config_port} did not acknowledge the "
+                                       "abort; restart the torchrun job and redeploy")
         while True:
             st = [ping_node(d.host, d.config_port, timeout_ms) for d in alive]
             if all(x is not None and x.get("mode") != "pipeline" for x in st):

@@ -514,8 +514,8 @@ class NodeController:
                 # live re-shard of the deployed pipeline (reference hot re-config, node_worker.py
                 # :445-474): rank 0 owns the command stream, so the new split is applied there,
                 # in order, once the requests in flight have finished
-                if not self.server.first:
-                    _log("[WARNING] replan ignored: send it to rank 0 (the ingress)")
+                if self.server is None or not self.server.first:
+                    _log("[WARNING] replan ignored: send it to rank 0 (the ingress) of a running pipeline")
                     return
                 try:
                     self.server.request_replan(msg["stages"])
@@ -535,6 +535,8 @@ class NodeController:
             except Exception as e:  # noqa: BLE001 - a peer rank died mid-collective
                 lost = repr(e)
             serving.clear()
+            if lost is not None or self._aborted:  # dropped while the listener still answers pings
+                self._drop_pipeline(lost or "aborted by the master")
             stop.set()
             th.join(timeout=5)
             replies.close()
@@ -554,13 +556,12 @@ class NodeController:
             except Exception as e:  # noqa: BLE001 - a peer rank died mid-collective
                 lost = repr(e)
             serving.clear()
+            if lost is not None or self._aborted:
+                self._drop_pipeline(lost or "aborted by the master")
             stop.set()
             th.join(timeout=5)
         self.running = False
-        if lost is None and not self._aborted:
-            return False
-        self._drop_pipeline(lost or "aborted by the master")
-        return True
+        return lost is not None or self._aborted
 
     ABORT_GRACE_S = 10.0  # abort_pipeline -> communicator abort if this rank is still serving
 
@@ -582,6 +583,7 @@ class NodeController:
         import gc
         import torch.distributed as dist
         _log(f"[ERROR] pipeline dropped ({reason}); waiting for the master's chain re-deployment")
+        self.pipeline_lost = reason
         self.server = None
         gc.collect()
         if dist.is_initialized():
@@ -590,7 +592,6 @@ class NodeController:
             except Exception as e:  # noqa: BLE001
                 _log(f"[WARNING] destroy_process_group: {e}")
         self.backend = "tcp"
-        self.pipeline_lost = reason
 
     def _await_redeploy(self) -> bool:
         """After :meth:`_drop_pipeline`: answer pings until a (chain) config arrives and apply it;
