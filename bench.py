@@ -74,6 +74,11 @@ def parse():
                          "IPC-mapped HBM rings with device flags, parallel/ipc_ring.py; prefill stays on RCCL)")
     ap.add_argument("--device", default="cuda", choices=("cuda", "cpu"),
                     help="cpu: the same schedule on gloo + the torch CPU path (multi-rank rehearsal)")
+    ap.add_argument("--no-supervise", dest="supervise", action="store_false",
+                    help="N > 1: run the rank's work in this process (default: a GPU-free per-rank supervisor "
+                         "runs it in a fresh child and can restart it once, see --no-fallback)")
+    ap.add_argument("--no-fallback", dest="fallback", action="store_false",
+                    help="N > 1: do not restart with --transport ipc when the RCCL ring preflight fails")
     return ap.parse_args()
 
 
@@ -120,6 +125,86 @@ def spawn_ranks(n: int) -> int:
     return rc
 
 
+PREFLIGHT_EXIT = 75  # = parallel.pipeline.PREFLIGHT_EXIT (not imported: the supervisor stays light)
+
+
+def _spawn_worker(argv: list, port: int, extra_env: dict):
+    import subprocess
+    env = dict(os.environ, MASTER_PORT=str(port), LSA_BENCH_ROLE="worker", PYTHONUNBUFFERED="1", **extra_env)
+    # the workers rendezvous on their own store (rank 0's worker hosts it), not torchrun's agent store
+    env.pop("TORCHELASTIC_USE_AGENT_STORE", None)
+    return subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env, start_new_session=True)
+
+
+def _watch(proc, store, rank: int, world: int, attempt: int) -> int:
+    """Wait for this rank's worker; if another rank's worker of the same attempt has already
+    failed, stop ours too (it would only wait on the dead peer until the collective timeout)."""
+    import signal
+    others = [r for r in range(world) if r != rank]
+    while True:
+        code = proc.poll()
+        if code is not None:
+            return code
+        for r in others:
+            key = f"lsa_bench/{attempt}/exit/{r}"
+            if store.check([key]) and int(store.get(key)) != 0:
+                time.sleep(2.0)  # let our worker print its own view first
+                if proc.poll() is None:
+                    try:
+                        os.killpg(proc.pid, signal.SIGTERM)
+                    except ProcessLookupError:
+                        pass
+                    try:
+                        return proc.wait(timeout=20)
+                    except Exception:  # noqa: BLE001
+                        os.killpg(proc.pid, signal.SIGKILL)
+                        return proc.wait()
+                return proc.poll()
+        time.sleep(0.2)
+
+
+def supervise(a, argv: list) -> int:
+    """Per-rank supervisor of a multi-GPU run (never touches the GPU). The rank's real work runs
+    in a FRESH child process; if any rank's child fails the ring-edge preflight
+    (parallel/pipeline.preflight_edges: a dead RCCL edge, named, within LSA_PREFLIGHT_TIMEOUT_S),
+    every supervisor starts one more fresh child with ``--transport ipc`` (IPC rings over xGMI,
+    gloo control; no RCCL communicator) and the JSON line says ``"fallback": true``. Any other
+    failure is returned as is. Coordination uses the launcher's rendezvous store (gloo group on
+    the CPU); the children rendezvous on a port rank 0 picks per attempt."""
+    import datetime
+
+    import torch.distributed as dist
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dist.init_process_group("gloo", timeout=datetime.timedelta(hours=2))
+    store = dist.distributed_c10d._get_default_store()
+    attempts = [([], {})]
+    if a.transport == "rccl" and a.fallback:
+        attempts.append((["--transport", "ipc"], {"LSA_BENCH_FALLBACK": "1"}))
+    code = 0
+    for i, (extra, env) in enumerate(attempts):
+        if rank == 0:
+            store.set(f"lsa_bench/{i}/port", str(_free_port()))
+        port = int(store.get(f"lsa_bench/{i}/port"))
+        if i and rank == 0:
+            print(f"[bench] ring preflight failed on the RCCL transport: restarting every rank once with "
+                  f"--transport ipc", file=sys.stderr, flush=True)
+        proc = _spawn_worker(argv + extra, port, env)
+        code = _watch(proc, store, rank, world, i)
+        store.set(f"lsa_bench/{i}/exit/{rank}", str(code))
+        keys = [f"lsa_bench/{i}/exit/{r}" for r in range(world)]
+        store.wait(keys, datetime.timedelta(minutes=30))
+        codes = [int(store.get(k)) for k in keys]
+        if all(c == 0 for c in codes):
+            code = 0
+            break
+        if PREFLIGHT_EXIT not in codes or i + 1 == len(attempts):
+            code = code or next(c for c in codes if c != 0)
+            break
+    dist.barrier()
+    dist.destroy_process_group()
+    return code if code >= 0 else 1
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -127,6 +212,8 @@ def main():
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         raise SystemExit(spawn_ranks(a.gpus))
+    if world > 1 and os.environ.get("LSA_BENCH_ROLE") != "worker" and a.supervise:
+        raise SystemExit(supervise(a, sys.argv[1:]))
     if a.trace:
         os.environ["LSA_TRACE"] = a.trace
     from llm_sharding_amd.parallel.pipeline import run_decode_benchmark
@@ -171,6 +258,9 @@ def main():
     }
     if res.get("transport"):
         line["config"]["transport"] = res["transport"]
+        line["transport"] = res["transport"]
+        line["fallback"] = os.environ.get("LSA_BENCH_FALLBACK") == "1"
+        line["preflight_us"] = res.get("preflight_us")
     if res.get("tokens_mb0"):  # parity digest across layouts (same prompts -> same tokens)
         import hashlib
         line["tokens_mb0_sha16"] = hashlib.sha256(json.dumps(res["tokens_mb0"]).encode()).hexdigest()[:16]

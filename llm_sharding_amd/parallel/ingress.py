@@ -41,6 +41,20 @@ class Replies:
                 "request_id": r.rid, "output_ids": list(r.output_ids), "text": text,
                 "ttft_ms": r.ttft_ms, "tpot_ms": r.tpot_ms}))
 
+    def error(self, reply_to: Optional[str], reason: str, request_id=None) -> None:
+        """Tell a client its request will not be served (``{"request_id", "error"}``)."""
+        if self.verbose:
+            print(f"[ERROR] request {request_id} not served: {reason}", flush=True)
+        if not reply_to:
+            return
+        try:
+            if reply_to not in self.socks:
+                self.socks[reply_to] = PushSocket(reply_to)
+            self.socks[reply_to].send_bytes(protocol.encode({"request_id": request_id, "error": reason,
+                                                             "output_ids": [], "text": ""}))
+        except OSError as e:
+            print(f"[WARNING] error reply to {reply_to} failed: {e}", flush=True)
+
     def close(self) -> None:
         for s in self.socks.values():
             s.close(linger_ms=2000)
@@ -69,14 +83,17 @@ def submit_message(srv, msg: dict, tokenizer, default_new: int, replies: Replies
             srv.submit(ids, n_new, on_token=replies, reply_to=msg.get("reply_to"))
             n += 1
         except ValueError as e:
-            print(f"[ERROR] request rejected: {e}", flush=True)
+            replies.error(msg.get("reply_to"), f"request rejected: {e}")
     return n
 
 
 def run_ingress(srv, sock: PullSocket, tokenizer, stop_evt: threading.Event, default_new: int,
-                replies: Replies, on_other: Optional[Callable[[dict], None]] = None) -> None:
+                replies: Replies, on_other: Optional[Callable[[dict], None]] = None,
+                accepting: Optional[Callable[[], Optional[str]]] = None) -> None:
     """Read control messages from ``sock`` until ``shutdown`` (or ``stop_evt``): queue
-    ``user_request`` prompts on the server; other commands go to ``on_other`` (e.g. ping)."""
+    ``user_request`` prompts on the server; other commands go to ``on_other`` (e.g. ping).
+    ``accepting()`` returning a reason string refuses new requests with an error reply (a
+    pipeline being dropped after a lost rank must not swallow them)."""
     while not stop_evt.is_set():
         try:
             raw = sock.recv_bytes(timeout_ms=200)
@@ -88,6 +105,10 @@ def run_ingress(srv, sock: PullSocket, tokenizer, stop_evt: threading.Event, def
             stop_evt.set()
             break
         if cmd == "user_request":
+            why = accepting() if accepting is not None else None
+            if why:
+                replies.error(msg.get("reply_to"), why)
+                continue
             submit_message(srv, msg, tokenizer, default_new, replies)
         elif on_other is not None:
             on_other(msg)

@@ -77,9 +77,76 @@ class DistP2P:
         return dist.isend(t, dst, group=self._group(dist.get_rank(), dst))
 
     def recv(self, t: torch.Tensor, src: int) -> None:
+        self.irecv(t, src).wait()
+
+    def irecv(self, t: torch.Tensor, src: int):
         import torch.distributed as dist
         src = self._global(src)
-        dist.irecv(t, src, group=self._group(src, dist.get_rank())).wait()
+        return dist.irecv(t, src, group=self._group(src, dist.get_rank()))
+
+
+PREFLIGHT_EXIT = 75  # a rank whose ring edge failed the preflight exits with this code
+
+
+def _parse_fault(spec: str):
+    """``LSA_PREFLIGHT_FAULT="a->b"``: test hook - global rank a never sends on edge a -> b."""
+    if not spec:
+        return None
+    a, b = spec.split("->")
+    return int(a), int(b)
+
+
+def preflight_edges(p2p: "DistP2P", srank: int, pp: int, dev, timeout_s: Optional[float] = None,
+                    iters: int = 5, inject: bool = True) -> dict:
+    """First-light check of this rank's two ring edges before anything heavy runs: one small
+    tensor goes ``stage -> stage+1`` on the outgoing edge's communicator while one arrives from
+    ``stage-1`` on the incoming one, ``iters`` times (the first round, which may build the
+    communicators lazily, is not timed). Returns ``{"a->b": us}`` for the INCOMING edge (global
+    ranks; median round time). A watchdog bounds the whole check: if either edge has not
+    completed within ``timeout_s`` (``LSA_PREFLIGHT_TIMEOUT_S``, default 30) the rank prints which
+    edge and exits with :data:`PREFLIGHT_EXIT` at once (``os._exit``: a communicator stuck on a
+    dead peer cannot be torn down) - the bench's per-rank supervisor then decides on a fallback."""
+    import sys
+    import threading
+    if pp < 2:
+        return {}
+    timeout_s = float(os.environ.get("LSA_PREFLIGHT_TIMEOUT_S", "30")) if timeout_s is None else timeout_s
+    me, nxt, prv = p2p._global(srank), p2p._global((srank + 1) % pp), p2p._global((srank - 1) % pp)
+    fault = _parse_fault(os.environ.get("LSA_PREFLIGHT_FAULT", "")) if inject else None
+    state = {"pending": f"{prv}->{me} (receive) and {me}->{nxt} (send)"}
+
+    def _fail():
+        print(f"[bench] PREFLIGHT FAILED on rank {me}: edge {state['pending']} did not complete within "
+              f"{timeout_s:.0f} s; exiting {PREFLIGHT_EXIT}", file=sys.stderr, flush=True)
+        os._exit(PREFLIGHT_EXIT)
+
+    wd = threading.Timer(timeout_s, _fail)
+    wd.daemon = True
+    wd.start()
+    out = torch.empty(64, dtype=torch.float32, device=dev)
+    inp = torch.empty(64, dtype=torch.float32, device=dev)
+    times = []
+    for it in range(iters + 1):
+        out.fill_(float(me * 1000 + it))
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        state["pending"] = f"{prv}->{me} (receive) and {me}->{nxt} (send)"
+        sw = None if fault == (me, nxt) else p2p.isend(out, (srank + 1) % pp)
+        rw = p2p.irecv(inp, (srank - 1) % pp)
+        rw.wait()
+        state["pending"] = f"{me}->{nxt} (send)"
+        if sw is not None:
+            sw.wait()
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        times.append(time.perf_counter() - t0)
+        if float(inp[0]) != float(prv * 1000 + it):
+            wd.cancel()
+            raise RuntimeError(f"preflight: edge {prv}->{me} delivered {float(inp[0])}, expected {prv * 1000 + it}")
+    wd.cancel()
+    t = sorted(times[1:])
+    return {f"{prv}->{me}": round(t[len(t) // 2] * 1e6, 1)}
 
 
 class LocalP2P:
@@ -679,6 +746,18 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
                          ranks=rings[replica], edges=edges)
     else:
         p2p = DistP2P(ranks=rings[replica], rings=rings)
+    preflight = {}
+    if dist is not None and not ipc_only and pp > 1:
+        # every ring edge carries a message before the weights load: a dead edge ends this rank
+        # within LSA_PREFLIGHT_TIMEOUT_S with the edge named (exit PREFLIGHT_EXIT), not after the
+        # LSA_DIST_TIMEOUT_S watchdog in the middle of the prefill
+        mine = preflight_edges(p2p, srank, pp, dev, inject=transport == "rccl")
+        got = [None] * world
+        dist.all_gather_object(got, mine)
+        for g in got:
+            preflight.update(g)
+        if verbose and rank == 0:
+            print(f"[bench] preflight (us per ring edge): {preflight}", flush=True)
     t0 = time.perf_counter()
     stage = PipelineStage(cfg, srank, pp, st.start, st.end, dev, batch, M, max_seq,
                           RandomSource(cfg, seed), use_graph=use_graph,
@@ -797,6 +876,7 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
         "plan": plan.ranges(),
         "tokens_mb0": tokens_mb0,  # rank 0 only when it holds the history (1 stage or split head)
         "transport": transport if pp > 1 else None,
+        "preflight_us": preflight or None,
         "b1_p50_tpot_ms": lat_p50 if latency_steps > 0 else None,
         "b1_tok_s": (dp * latency_steps / lat_el) if latency_steps > 0 and lat_el > 0 else None,
         "mid_batch": mid_batch or None,

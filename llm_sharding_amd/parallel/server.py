@@ -376,6 +376,13 @@ class PipelineServer:
         self.incoming.put(r)
         return rid
 
+    def unfinished(self) -> List[Request]:
+        """Rank 0, after :meth:`serve` has returned: every request that will never finish here
+        (queued, waiting or in flight) - the controller answers them with an error when the
+        pipeline is dropped (a lost rank), instead of leaving their clients waiting."""
+        self._intake()
+        return [r for r in self.requests.values() if r.state != DONE]
+
     def _intake(self) -> None:
         while True:
             try:

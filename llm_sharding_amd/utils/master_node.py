@@ -215,8 +215,11 @@ class MasterNode:
                     raise RuntimeError(f"[ERROR] pipeline rank {d.host}:{d.config_port} did not acknowledge the "
                                        "abort; restart the torchrun job and redeploy")
         while True:
+            # "awaiting_redeploy" is reported only once a rank has dropped its stage AND stopped
+            # its pipeline listener, so the chain configs sent next reach the reader that
+            # applies them (NodeController._run_pipeline)
             st = [ping_node(d.host, d.config_port, timeout_ms) for d in alive]
-            if all(x is not None and x.get("mode") != "pipeline" for x in st):
+            if all(x is not None and x.get("phase") == "awaiting_redeploy" for x in st):
                 break
             if time.monotonic() > deadline:
                 raise RuntimeError(f"[ERROR] pipeline ranks did not drop their stages: {st}; restart the torchrun job")

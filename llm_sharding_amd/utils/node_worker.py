@@ -329,6 +329,20 @@ class NodeWorker:
 CONFIG_KEYS = ("src_addr", "dst_addr", "can_receive_user_request", "first_node_addr", "shards_start", "shards_end")
 
 
+class _StageRef:
+    """What rank 0's ingress thread holds instead of the PipelineServer itself (so a dropped
+    stage can be freed while the listener still runs): ``submit`` forwards to the live stage."""
+
+    def __init__(self, ctrl):
+        self._ctrl = ctrl
+
+    def submit(self, *a, **kw):
+        srv = self._ctrl.server
+        if srv is None:
+            raise ValueError("pipeline dropped (a rank was lost)")
+        return srv.submit(*a, **kw)
+
+
 class NodeController:
     """Node-side control plane (reference C3). Config JSON arrives on ``tcp://*:listen_port``."""
 
@@ -404,14 +418,14 @@ class NodeController:
                     "shards": [self.server.start, self.server.end], "replans": self.server.replans,
                     "rank": c.get("rank"),
                     "ingress": c.get("rank") == 0, "finished_requests": len(self.finished_outputs),
-                    "uptime_s": time.monotonic() - self.t_boot}
+                    "phase": getattr(self, "phase", "serving"), "uptime_s": time.monotonic() - self.t_boot}
         w = self.node_worker
         return {"listen_port": self.listen_port, "configured": w is not None,
                 "pipeline_lost": getattr(self, "pipeline_lost", None),
                 "shards": [w.start, w.end] if w is not None else None,
                 "ingress": bool(w.can_receive_user_request) if w is not None else False,
                 "forwarded": self.forwarded, "finished_requests": len(self.finished_outputs),
-                "uptime_s": time.monotonic() - self.t_boot}
+                "phase": getattr(self, "phase", "chain"), "uptime_s": time.monotonic() - self.t_boot}
 
     def _pong(self, msg: dict) -> None:
         reply_to = msg.get("reply_to")
@@ -481,11 +495,19 @@ class NodeController:
         if self.verbose:
             _log(f"[INFO] pipeline stage {r}/{n}: layers [{cfg['shards_start']}, {cfg['shards_end']}) on {self.device}")
 
-    def _run_pipeline(self, max_new_tokens: int) -> None:
+    def _run_pipeline(self, max_new_tokens: int) -> bool:
         """Pipeline mode: rank 0 reads requests from its config port on a thread and schedules;
         the other ranks follow rank 0's commands until it stops (``shutdown``). Returns True if
         the pipeline was dropped because a rank was lost (a peer's error, or the master's
-        ``abort_pipeline`` from :meth:`MasterNode.failover`)."""
+        ``abort_pipeline`` from :meth:`MasterNode.failover`).
+
+        Failover ordering (no message may be lost between the pipeline and the chain): the
+        listener thread is the ONLY reader of the config socket until it is joined; while the
+        stage is dropped it keeps answering pings (phase ``dropping``), refuses new requests with
+        an error reply and queues any config that arrives early (``self._early_configs``).
+        Only after the join does the phase become ``awaiting_redeploy`` - the state the master
+        waits for before it sends the chain configs - and :meth:`_await_redeploy` drains the
+        early queue before it reads the socket itself."""
         import threading
         from ..parallel.ingress import Replies, run_ingress
         lost = None
@@ -493,28 +515,40 @@ class NodeController:
         serving = threading.Event()
         serving.set()
         self._aborted = False
+        self._abort_timer = None
+        self._abort_lock = threading.Lock()
+        self._early_configs = []
+        self.phase = "serving"
+        # no local (thread argument, timer argument, closure) may keep the stage alive: its
+        # process groups must be freed by _drop_pipeline so their connections close and the
+        # peers blocked on this rank fail over too
+        first = self.server.first
 
         def other(msg):
             if not isinstance(msg, dict):
                 return
-            if msg.get("command") == "ping":
+            cmd = msg.get("command")
+            if cmd == "ping":
                 self._pong(msg)
-            elif msg.get("command") == "abort_pipeline":
+            elif cmd == "abort_pipeline":
                 # the master lost a rank of this torchrun world (MasterNode.failover): rank 0 stops
                 # scheduling, every rank drops its pipeline and waits for a chain re-deployment
+                first = not self._aborted
                 self._aborted = True
                 self._pong(msg)
-                # a rank still inside an RCCL op with the dead peer after the grace period cannot
-                # see a closed connection (gloo can): abort its communicators so the op fails
-                # (ncclCommAbort) instead of waiting for the watchdog
-                t = threading.Timer(self.ABORT_GRACE_S, self._abort_groups, args=(serving,))
-                t.daemon = True
-                t.start()
-            elif msg.get("command") == "replan" or (msg.get("mode") == "pipeline" and "stages" in msg):
+                if first:
+                    # a rank still inside an RCCL op with the dead peer after the grace period
+                    # cannot see a closed connection (gloo can): abort its communicators so the
+                    # op fails instead of waiting for the watchdog
+                    t = threading.Timer(self.ABORT_GRACE_S, self._abort_groups, args=(serving,))
+                    t.daemon = True
+                    self._abort_timer = t
+                    t.start()
+            elif cmd == "replan" or (msg.get("mode") == "pipeline" and "stages" in msg):
                 # live re-shard of the deployed pipeline (reference hot re-config, node_worker.py
                 # :445-474): rank 0 owns the command stream, so the new split is applied there,
                 # in order, once the requests in flight have finished
-                if self.server is None or not self.server.first:
+                if self.server is None or not self.server.first or self._aborted:
                     _log("[WARNING] replan ignored: send it to rank 0 (the ingress) of a running pipeline")
                     return
                 try:
@@ -523,23 +557,27 @@ class NodeController:
                         _log(f"[CONFIG] re-plan requested: {msg['stages']}")
                 except ValueError as e:
                     _log(f"[ERROR] {e}")
+            elif cmd == "user_request":  # non-ingress rank (rank 0's run_ingress takes its own)
+                self._reject_request(msg, "this rank is not the pipeline's ingress")
+            elif cmd is None and msg.get("mode") != "pipeline":
+                # a chain config that arrived before this rank finished dropping its stage
+                _log("[CONFIG] chain configuration queued until the pipeline is dropped")
+                self._early_configs.append(msg)
+            else:
+                _log(f"[WARNING] message {cmd!r} ignored while a pipeline is deployed")
 
-        if self.server.first:
+        def accepting():
+            if self._aborted or self.phase != "serving":
+                return "pipeline dropped (a rank was lost); resubmit after the master's failover"
+            return None
+
+        replies = None
+        if first:
             replies = Replies(self.tokenizer, verbose=self.verbose,
                               on_done=lambda r, text: self.finished_outputs.append(list(r.output_ids)))
-            th = threading.Thread(target=run_ingress, args=(self.server, self.recv_config_socket, self.tokenizer,
-                                                            stop, max_new_tokens, replies, other), daemon=True)
-            th.start()
-            try:
-                self.server.serve(stop_when_idle=False, should_stop=lambda: stop.is_set() or self._aborted)
-            except Exception as e:  # noqa: BLE001 - a peer rank died mid-collective
-                lost = repr(e)
-            serving.clear()
-            if lost is not None or self._aborted:  # dropped while the listener still answers pings
-                self._drop_pipeline(lost or "aborted by the master")
-            stop.set()
-            th.join(timeout=5)
-            replies.close()
+            th = threading.Thread(target=run_ingress, args=(_StageRef(self), self.recv_config_socket, self.tokenizer,
+                                                            stop, max_new_tokens, replies, other, accepting),
+                                  daemon=True)
         else:
             def pings():
                 while not stop.is_set():
@@ -548,33 +586,73 @@ class NodeController:
                     except Again:
                         continue
                     msg = json.loads(raw.decode())
+                    if isinstance(msg, dict) and msg.get("command") == "shutdown":
+                        continue  # the pipeline's STOP comes from rank 0's command stream
                     other(msg)
             th = threading.Thread(target=pings, daemon=True)
-            th.start()
-            try:
+        th.start()
+        try:
+            if first:
+                self.server.serve(stop_when_idle=False, should_stop=lambda: stop.is_set() or self._aborted)
+            else:
                 self.server.serve()
-            except Exception as e:  # noqa: BLE001 - a peer rank died mid-collective
-                lost = repr(e)
+        except Exception as e:  # noqa: BLE001 - a peer rank died mid-collective
+            lost = repr(e)
+        with self._abort_lock:  # no communicator abort may start once serve() has returned
             serving.clear()
-            if lost is not None or self._aborted:
-                self._drop_pipeline(lost or "aborted by the master")
-            stop.set()
+        if self._abort_timer is not None:
+            self._abort_timer.cancel()
+        dropped = lost is not None or self._aborted
+        if dropped:
+            self.phase = "dropping"  # the listener still answers pings and queues early configs
+            if replies is not None:
+                for r in self.server.unfinished():
+                    replies.error(r.reply_to, "pipeline dropped (a rank was lost) before the request finished",
+                                  request_id=r.rid)
+            self._drop_pipeline(lost or "aborted by the master")
+        stop.set()
+        while th.is_alive():  # the listener must be gone before anyone else reads the socket
             th.join(timeout=5)
+            if th.is_alive():
+                _log("[WARNING] waiting for the config listener to stop")
+        if replies is not None:
+            replies.close()
         self.running = False
-        return lost is not None or self._aborted
+        if dropped:
+            self.phase = "awaiting_redeploy"
+        return dropped
 
     ABORT_GRACE_S = 10.0  # abort_pipeline -> communicator abort if this rank is still serving
 
-    @staticmethod
-    def _abort_groups(serving) -> None:
-        if not serving.is_set():
-            return
-        import torch.distributed.distributed_c10d as c10d
-        _log("[ERROR] still blocked in the pipeline after the abort grace period: aborting its process groups")
-        try:
-            c10d._abort_process_group()
-        except Exception as e:  # noqa: BLE001
-            _log(f"[WARNING] process-group abort: {e}")
+    def _abort_groups(self, serving) -> None:
+        """Grace period over and still inside a collective: abort every process group of the
+        stage (``ProcessGroup.abort()``, the supported form - ncclCommAbort on RCCL) so the
+        blocked op returns an error instead of waiting for the watchdog."""
+        import torch.distributed as dist
+        with self._abort_lock:
+            if not serving.is_set():
+                return
+            groups, server = [], self.server
+            if server is not None:
+                groups += list(getattr(server.p2p, "groups", {}).values())
+                if server.ctrl is not None:
+                    groups.append(server.ctrl)
+            from ..parallel import communicator
+            groups += list(getattr(communicator, "_EDGE_GROUPS", {}).values())
+            if dist.is_initialized():
+                groups.append(dist.group.WORLD)
+            _log(f"[ERROR] still blocked in the pipeline after the abort grace period: aborting "
+                 f"{len(groups)} process groups with ProcessGroup.abort()")
+            groups = [g for g in groups if isinstance(g, dist.ProcessGroup)]  # not NON_GROUP_MEMBER
+            done = 0
+            for g in groups:
+                try:
+                    g.abort()
+                    done += 1
+                except Exception as e:  # noqa: BLE001 - e.g. a backend without abort support
+                    _log(f"[WARNING] ProcessGroup.abort() on {g!r}: {e}")
+            self.abort_report = {"method": "ProcessGroup.abort", "groups": len(groups), "aborted": done}
+            _log(f"[INFO] process-group abort: {done}/{len(groups)} aborted")
 
     def _drop_pipeline(self, reason: str) -> None:
         """The torchrun world lost a rank: release this rank's stage and its process groups (which
@@ -582,37 +660,69 @@ class NodeController:
         back to the ZMQ chain transport for the master's re-deployment over the survivors."""
         import gc
         import torch.distributed as dist
+        from ..parallel import communicator
         _log(f"[ERROR] pipeline dropped ({reason}); waiting for the master's chain re-deployment")
         self.pipeline_lost = reason
+        # every reference to a process group goes (the stage's edge groups and command group,
+        # the job-wide edge groups of start_node.py); gloo closes a group's connections only
+        # when the group is freed, and a peer blocked in a receive from this rank (e.g. the
+        # command broadcast of rank 0) fails only then
         self.server = None
+        getattr(communicator, "_EDGE_GROUPS", {}).clear()
         gc.collect()
         if dist.is_initialized():
             try:
                 dist.destroy_process_group()
             except Exception as e:  # noqa: BLE001
                 _log(f"[WARNING] destroy_process_group: {e}")
+        gc.collect()
         self.backend = "tcp"
 
+    def _reject_request(self, msg: dict, reason: str) -> None:
+        reply_to = msg.get("reply_to")
+        _log(f"[ERROR] request not served: {reason}")
+        if not reply_to:
+            return
+        try:
+            s = PushSocket(reply_to)
+            s.send_bytes(protocol.encode({"request_id": None, "error": reason, "output_ids": [], "text": ""}))
+            s.close(linger_ms=2000)
+        except OSError as e:
+            _log(f"[WARNING] error reply to {reply_to} failed: {e}")
+
     def _await_redeploy(self) -> bool:
-        """After :meth:`_drop_pipeline`: answer pings until a (chain) config arrives and apply it;
-        False if a ``shutdown`` came first."""
+        """After :meth:`_drop_pipeline` (listener joined): apply a chain config that arrived while
+        the stage was being dropped, else answer pings until one arrives; False if a ``shutdown``
+        came first. Requests received meanwhile are kept for the new ingress; a survivor that
+        does not become the ingress answers them with an error (the client resubmits)."""
         while True:
-            try:
-                raw = self.recv_config_socket.recv_bytes(200)
-            except Again:
-                continue
-            msg = json.loads(raw.decode())
+            if self._early_configs:
+                msg = self._early_configs.pop(0)
+            else:
+                try:
+                    raw = self.recv_config_socket.recv_bytes(200)
+                except Again:
+                    continue
+                msg = json.loads(raw.decode())
             cmd = msg.get("command") if isinstance(msg, dict) else None
             if cmd == "shutdown":
                 return False
-            if cmd in ("ping", "user_request", "abort_pipeline"):
-                self._pong(msg) if cmd != "user_request" else self.pending_requests.append(msg)
+            if cmd == "user_request":
+                self.pending_requests.append(msg)
+                continue
+            if cmd is not None:  # ping, a repeated abort_pipeline, ...
+                self._pong(msg)
                 continue
             if msg.get("mode") == "pipeline":
                 _log("[ERROR] a pipeline config after a lost rank: restart the torchrun job to redeploy one")
                 continue
             self.received_config = msg
             self._apply_new_role(msg)
+            self.phase = "chain"
+            if not self.node_worker.can_receive_user_request:
+                for req in self.pending_requests:
+                    self._reject_request(req, "this node is not the chain's ingress after the failover")
+                self.pending_requests = []
             return True
 
     def _set_first_node_addr(self, cfg: dict) -> None:

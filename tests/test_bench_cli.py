@@ -56,3 +56,69 @@ def test_bench_cli_rank_failure_is_reported():
                        stderr=subprocess.PIPE, text=True, timeout=300)
     assert r.returncode != 0
     assert not any(l.startswith("{") for l in r.stdout.splitlines())
+
+
+def _bench_env(**extra):
+    env = dict(os.environ, OMP_NUM_THREADS="1", **extra)
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT", "LOCAL_WORLD_SIZE"):
+        env.pop(k, None)
+    return env
+
+
+def test_bench_preflight_reports_edges():
+    """The ring-edge preflight (one small message per directed edge before the weights load)
+    runs on every multi-rank run and its per-edge latencies reach the JSON line."""
+    line = _run_bench("--gpus", "3", "--model", "tiny", *COMMON)
+    assert line["transport"] == "rccl" and line["fallback"] is False
+    assert sorted(line["preflight_us"]) == ["0->1", "1->2", "2->0"], line["preflight_us"]
+    assert all(v > 0 for v in line["preflight_us"].values())
+
+
+def test_bench_dead_edge_fails_fast_and_falls_back_once():
+    """An injected dead edge (rank 1 never sends on 1 -> 2): rank 2's preflight names the edge
+    and exits 75 within LSA_PREFLIGHT_TIMEOUT_S; the per-rank supervisors (which never touched a
+    device) stop the other workers and start every rank ONCE more in a fresh process with
+    --transport ipc; that run produces the number, marked ``"fallback": true``."""
+    import time
+    env = _bench_env(LSA_PREFLIGHT_FAULT="1->2", LSA_PREFLIGHT_TIMEOUT_S="5")
+    t0 = time.time()
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--device", "cpu", "--gpus", "3",
+                        "--model", "tiny", *COMMON], cwd=ROOT, env=env, stdout=subprocess.PIPE,
+                       stderr=subprocess.PIPE, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "PREFLIGHT FAILED on rank 2: edge 1->2 (receive)" in r.stderr, r.stderr[-3000:]
+    assert "restarting every rank once with --transport ipc" in r.stderr
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["fallback"] is True and line["transport"] == "ipc" and line["value"] > 0
+    assert time.time() - t0 < 200
+
+
+def test_bench_dead_edge_without_fallback_exits_nonzero():
+    env = _bench_env(LSA_PREFLIGHT_FAULT="0->1", LSA_PREFLIGHT_TIMEOUT_S="5")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--device", "cpu", "--gpus", "2",
+                        "--model", "tiny", "--no-fallback", *COMMON], cwd=ROOT, env=env, stdout=subprocess.PIPE,
+                       stderr=subprocess.PIPE, text=True, timeout=300)
+    assert r.returncode == 75, (r.returncode, r.stderr[-3000:])
+    assert "PREFLIGHT FAILED on rank 1: edge 0->1 (receive)" in r.stderr
+    assert not any(l.startswith("{") for l in r.stdout.splitlines())
+
+
+def test_bench_under_torchrun_supervised():
+    """The driver's launch form: torch.distributed.run starts the ranks (its agent hosts the
+    rendezvous store); the supervisors' workers rendezvous on their own port."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--device", "cpu",
+                        "--gpus", "2", "--model", "tiny", *COMMON], cwd=ROOT, env=_bench_env(),
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["fallback"] is False and sorted(line["preflight_us"]) == ["0->1", "1->0"]

@@ -221,9 +221,6 @@ def test_master_replans_live_pipeline_token_exact(tiny8_shards):
     assert inflight == _golden(tiny8_shards, [[5, 6, 7, 8]], n_new)[0]
 
 
-@pytest.mark.skipif(__import__("os").environ.get("LSA_FAILOVER_TEST") != "1",
-                    reason="intermittent (about 1 run in 3 here): some survivors do not apply the chain config "
-                           "after the drop - under investigation; LSA_FAILOVER_TEST=1 runs it")
 @pytest.mark.parametrize("dead", [2, 0])
 def test_pipeline_failover_to_chain_token_exact(tiny8_shards, dead):
     """Failure of a DEPLOYED pipeline rank (reference failure handling is a
