@@ -121,13 +121,10 @@ LSA_DEVICE void glds16(const void* src, unsigned char* lds_base) {
   if constexpr (LSA_SK_ABLATE != 2 && LSA_SK_ABLATE != 11)
     __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
 }
-// weight stream; WNT: non-temporal (aux 2) - measured 1.5-4 % faster where each weight byte is
-// read by only a few row tiles (M <= ~1024: decode batches), 2.6 % slower at M = 16384 where the
-// weight panels are re-read from L2 (profiles/r3_gemm_sk_ablation.jsonl "w_nt";
-// MI355X_MICROARCH.md 'nt-weights')
-template <bool WNT>
+// weight stream: default cache policy (non-temporal weight DMA measured no better in the headline
+// step, profiles/r3_gemm_nt_retune.jsonl; ablation build 9 keeps it for probes)
 LSA_DEVICE void glds16_w(const void* src, unsigned char* lds_base) {
-  if constexpr (LSA_SK_ABLATE == 9 || WNT)
+  if constexpr (LSA_SK_ABLATE == 9)
     __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_base, 16, 0, 2 /* nt */);
   else
     glds16(src, lds_base);
@@ -144,7 +141,7 @@ LSA_DEVICE void tile_coords(const SkParams& p, int tile, int& mt, int& nt) {
   nt = r / gm;
 }
 
-template <int BM, int BN, int EPI, int NB, bool WNT>
+template <int BM, int BN, int EPI, int NB>
 struct Kern {
   using G_ = Geo<BM, BN, NB>;
   static constexpr int WM = G_::WM, WN = G_::WN, TM = G_::TM, TN = G_::TN, FM = G_::FM, FN = G_::FN;
@@ -179,7 +176,7 @@ struct Kern {
     if constexpr (LSA_SK_ABLATE == 7) return;
 #pragma unroll
     for (int s = 0; s < BGL; ++s)
-      if (s < BGL_LO || w < BHI_WAVES) glds16_w<WNT>(base + boff[nh][s], dst + (s * 8 + w) * 1024);
+      if (s < BGL_LO || w < BHI_WAVES) glds16_w(base + boff[nh][s], dst + (s * 8 + w) * 1024);
   }
   // counted wait keeping one K-tile of this wave's DMA in flight (+ EXTRA instructions)
   template <int EXTRA = 0>
@@ -577,11 +574,11 @@ struct Kern {
   }
 };
 
-template <int BM, int BN, int EPI, int NB, bool WNT>
+template <int BM, int BN, int EPI, int NB>
 __global__ __launch_bounds__(NTHR) void gemm_sk_kernel(const bf16_raw* __restrict__ A, const bf16_raw* __restrict__ W,
                                                         SkParams prm, EpiArgs ep, float* __restrict__ slab,
                                                         unsigned* __restrict__ counters) {
-  using K_ = Kern<BM, BN, EPI, NB, WNT>;
+  using K_ = Kern<BM, BN, EPI, NB>;
   __shared__ __attribute__((aligned(16))) unsigned char smem[Geo<BM, BN, NB>::SMEM];
   K_ k;
   k.smem = smem;
@@ -705,27 +702,24 @@ __global__ __launch_bounds__(NTHR) void gemm_sk_kernel(const bf16_raw* __restric
 
 template <int BM, int BN, int EPI, int NB>
 int launch(const bf16_raw* A, const bf16_raw* W, const SkParams& prm, const EpiArgs& ep, float* slab,
-           unsigned* cnt, bool wnt, hipStream_t s) {
-  if (wnt)
-    gemm_sk_kernel<BM, BN, EPI, NB, true><<<prm.G, NTHR, 0, s>>>(A, W, prm, ep, slab, cnt);
-  else
-    gemm_sk_kernel<BM, BN, EPI, NB, false><<<prm.G, NTHR, 0, s>>>(A, W, prm, ep, slab, cnt);
+           unsigned* cnt, hipStream_t s) {
+  gemm_sk_kernel<BM, BN, EPI, NB><<<prm.G, NTHR, 0, s>>>(A, W, prm, ep, slab, cnt);
   LSA_CHECK_LAUNCH();
   return LSA_OK;
 }
 
 template <int BM, int EPI>
 int dispatch(const bf16_raw* A, const bf16_raw* W, const SkParams& prm, const EpiArgs& ep, float* slab,
-             unsigned* cnt, int bn, int nb, bool wnt, hipStream_t s) {
+             unsigned* cnt, int bn, int nb, hipStream_t s) {
   if (bn == 256) {
     if constexpr (BM == 128) {
-      if (nb == 3) return launch<BM, 256, EPI, 3>(A, W, prm, ep, slab, cnt, wnt, s);
+      if (nb == 3) return launch<BM, 256, EPI, 3>(A, W, prm, ep, slab, cnt, s);
     }
-    return launch<BM, 256, EPI, 2>(A, W, prm, ep, slab, cnt, wnt, s);
+    return launch<BM, 256, EPI, 2>(A, W, prm, ep, slab, cnt, s);
   }
-  if (bn == 192) return launch<BM, 192, EPI, 2>(A, W, prm, ep, slab, cnt, wnt, s);
-  return nb == 3 ? launch<BM, 128, EPI, 3>(A, W, prm, ep, slab, cnt, wnt, s)
-                 : launch<BM, 128, EPI, 2>(A, W, prm, ep, slab, cnt, wnt, s);
+  if (bn == 192) return launch<BM, 192, EPI, 2>(A, W, prm, ep, slab, cnt, s);
+  return nb == 3 ? launch<BM, 128, EPI, 3>(A, W, prm, ep, slab, cnt, s)
+                 : launch<BM, 128, EPI, 2>(A, W, prm, ep, slab, cnt, s);
 }
 
 }  // namespace
@@ -738,12 +732,11 @@ int dispatch(const bf16_raw* A, const bf16_raw* W, const SkParams& prm, const Ep
 // partial k stored to ((float*)ep->out)[k][M][ldo], no slabs or tickets (lsa_resid_rmsnorm_partials sums them).
 // split: 0 = remainder by stream-K, S >= 1 = remainder tiles split into up to S K ranges
 // (clamped to NKT and to grid / remainder tiles; stream-K when the remainder exceeds the grid).
-// wnt: 1 = non-temporal weight DMA (decode-sized M), 0 = default cache policy.
 // slab: >= 2 * grid * bm * bn floats and counters: >= remainder tiles (zeroed) when any tile is
 // split. Returns LSA_BAD_SHAPE on any shape the kernel's indexing cannot take.
 extern "C" int lsa_gemm_sk(const void* a, int lda, const void* wp, int M, int N, int K, int epi,
                            const EpiArgs* ep, int bm, int bn, int nb, int grid, int dp, int split, int group_m, float* slab,
-                           unsigned* counters, long long slab_floats, int n_counters, int wnt, hipStream_t stream) {
+                           unsigned* counters, long long slab_floats, int n_counters, hipStream_t stream) {
   if (M < 1 || K < BK || K % BK || lda < K || lda % 8 || !ep) return LSA_BAD_SHAPE;
   if (bn != 256 && bn != 192 && bn != 128) return LSA_UNSUPPORTED;
   if (bm != 256 && bm != 128) return LSA_UNSUPPORTED;
@@ -800,8 +793,8 @@ extern "C" int lsa_gemm_sk(const void* a, int lda, const void* wp, int M, int N,
     return LSA_BAD_SHAPE;
   const bf16_raw* A = static_cast<const bf16_raw*>(a);
   const bf16_raw* W = static_cast<const bf16_raw*>(wp);
-#define LSA_G(E) (bm == 256 ? dispatch<256, E>(A, W, prm, *ep, slab, counters, bn, nb, wnt != 0, stream) \
-                    : dispatch<128, E>(A, W, prm, *ep, slab, counters, bn, nb, wnt != 0, stream))
+#define LSA_G(E) (bm == 256 ? dispatch<256, E>(A, W, prm, *ep, slab, counters, bn, nb, stream) \
+                    : dispatch<128, E>(A, W, prm, *ep, slab, counters, bn, nb, stream))
   switch (epi) {
     case EPI_STORE: return LSA_G(EPI_STORE);
     case EPI_RESID: return LSA_G(EPI_RESID);

@@ -73,13 +73,14 @@ def lib() -> ctypes.CDLL:
     L.lsa_row_ss.argtypes = [vp, i, i, i, vp, vp]
     L.lsa_argmax_finalize.argtypes = [vp, i, vp, vp, i, vp, i, i, vp, vp]
     L.lsa_pos_advance.argtypes = [vp, i, i, vp]
-    L.lsa_gemm_wr.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(EpiArgs), i, i, i, i, vp]
+    L.lsa_mall_prefetch.argtypes = [vp, ctypes.c_longlong, i, vp, vp]
+    L.lsa_gemm_wr.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(EpiArgs), i, i, vp]
     L.lsa_gemm_sk.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(EpiArgs), i, i, i, i, i, i, i, vp, vp, ctypes.c_longlong, i,
-                              i, vp]
+                              vp]
     for name in ("lsa_gemv", "lsa_gemv_coop", "lsa_gemv_fp8", "lsa_dequant_fp8_packed", "lsa_gemv_coop_fp8", "lsa_gemm",
                  "lsa_gemm_sk", "lsa_gemm_wr", "lsa_attn_decode", "lsa_attn_prefill", "lsa_embed", "lsa_rmsnorm", "lsa_layernorm",
                  "lsa_resid_rmsnorm_partials", "lsa_row_ss",
-                 "lsa_argmax_finalize", "lsa_pos_advance", "lsa_version"):
+                 "lsa_argmax_finalize", "lsa_pos_advance", "lsa_mall_prefetch", "lsa_version"):
         getattr(L, name).restype = ctypes.c_int
     _lib = L
     return L
@@ -131,6 +132,20 @@ def make_epi(out=None, resid=None, k_cache=None, v_cache=None, slot=None, pos=No
     return EpiArgs(_p(out), _p(resid), _p(k_cache), _p(v_cache), _p(slot), _p(pos), _p(cos), _p(sin),
                    _p(keys), _p(bias), ldo, ldr, n_heads, n_kv, head_dim, t_max, col_offset, int(act),
                    _p(ss_out), _p(ss_in), 0 if ssb is None else ssb.shape[1], float(ss_eps))
+
+
+def mall_prefetch(t: torch.Tensor, sink: torch.Tensor, nbytes: int = 0, offset: int = 0, grid: int = 64) -> None:
+    """Read ``nbytes`` of ``t`` (from byte ``offset``; 0 = to the end) once so the lines settle in
+    the Infinity Cache; writes nothing (``sink``: an int32 scratch word the kernel never stores
+    to in practice)."""
+    _req(t.is_cuda and t.is_contiguous(), "mall_prefetch: contiguous device tensor")
+    total = t.numel() * t.element_size()
+    nbytes = (total - offset) if nbytes <= 0 else nbytes
+    _req(0 <= offset and offset + nbytes <= total and offset % 16 == 0 and nbytes % 16 == 0 and nbytes >= 16,
+         "mall_prefetch: range")
+    _req(sink.is_cuda and sink.dtype == torch.int32, "mall_prefetch: sink")
+    _check(lib().lsa_mall_prefetch(ctypes.c_void_p(t.data_ptr() + offset), nbytes, grid, _p(sink), _stream()),
+           "lsa_mall_prefetch")
 
 
 # ------------------------------------------------------------------------------ projections
@@ -311,7 +326,7 @@ def gemm(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep
             and a.data_ptr() % 16 == 0:
         wr = gemm_wr_plan(M, N, K, epi, ep)
         if wr:
-            gemm_wr(a, wp, M, N, K, epi, ep, bn=wr[0], ng=wr[1])
+            gemm_wr(a, wp, M, N, K, epi, ep, bn=wr)
         else:
             gemm_sk(a, wp, M, N, K, epi, ep, ws=sk_ws)
         return
@@ -345,62 +360,44 @@ def gemm(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep
 SK_BM = 256  # gemm_sk.hip row tile (default; 128-row tiles for small / odd M: plan field bm)
 
 # gemm_wr.hip (weights streamed into MFMA registers, 128 x bn tiles, one round of whole-K tiles)
-# where it measured faster than gemm_sk's best plan (profiles/r3_gemm_wr.md):
-# * one round of 224-256 whole 128 x 192 tiles with a store / QKV epilogue, i.e. the 7B qkv
-#   projection at 448-512 rows (54-55 us vs 59-81 us);
-# * opt-in (LSA_GEMM_WR_RESID=1): the residual projection with 4 row tiles x 28-32 128-column
-#   tiles (the 7B o projection at 448-512 rows) on two wave groups per tile (ng = 2), fused-RMSNorm
-#   sums of squares included - faster than gemm_sk in isolation with cold weights (39.4 vs 45.8
-#   us) but 1.5 % slower per headline step in the engine (13.59-13.63 vs 13.38-13.40 ms), so off.
-# LSA_GEMM_WR=0 turns both off (A/B runs).
+# where it measured faster than gemm_sk's best plan in the engine (profiles/r3_gemm_wr.md): one
+# round of 224-256 whole 128 x 192 tiles with a store / QKV epilogue. Measured only for the 7B qkv
+# projection (N 12288, K 4096) at 448-512 rows (54-55 us vs 59-81 us), so the route is limited to
+# the measured (N, K) pairs. LSA_GEMM_WR=0 turns it off (A/B runs).
 WR_TILES = (224, 256)
-WR_RESID_TILES = (112, 128)
+WR_MEASURED_NK = {(12288, 4096)}
 
 
-def gemm_wr_plan(M: int, N: int, K: int, epi: int, ep: "EpiArgs") -> Optional[Tuple[int, int]]:
-    """(bn, ng) for :func:`gemm_wr`, or None when gemm_sk takes the shape."""
-    if os.environ.get("LSA_GEMM_WR", "1") == "0" or ep.act or ep.bias:
+def gemm_wr_plan(M: int, N: int, K: int, epi: int, ep: "EpiArgs") -> Optional[int]:
+    """bn for :func:`gemm_wr`, or None when gemm_sk takes the shape."""
+    if os.environ.get("LSA_GEMM_WR", "1") == "0" or ep.act or ep.bias or ep.ss_out:
+        return None
+    if (N, K) not in WR_MEASURED_NK or epi not in (EPI_STORE, EPI_QKV):
         return None
     mt = -(-M // 128)
     # the last row tile at least half full: the kernel computes whole 128-row tiles, gemm_sk's
     # 128-row plans do not (measured at 448 and 512 rows)
     if M - (mt - 1) * 128 < 64:
         return None
-    if epi in (EPI_STORE, EPI_QKV) and not ep.ss_out and K % 256 == 0 and N % 192 == 0 \
-            and WR_TILES[0] <= mt * (N // 192) <= WR_TILES[1]:
-        return 192, 1
-    if epi == EPI_RESID and os.environ.get("LSA_GEMM_WR_RESID", "0") == "1" and K % 512 == 0 and N % 128 == 0 \
-            and mt == 4 and WR_RESID_TILES[0] <= mt * (N // 128) <= WR_RESID_TILES[1]:
-        return 128, 2
+    if K % 256 == 0 and N % 192 == 0 and WR_TILES[0] <= mt * (N // 192) <= WR_TILES[1]:
+        return 192
     return None
 
 
 def gemm_wr(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep: EpiArgs, bn: int = 192,
-            grid: int = 0, split: int = 1, out_numel: int = 0, ng: int = 1) -> None:
+            grid: int = 0) -> None:
     """Projection GEMM with the weights fetched straight into MFMA B registers (gemm_wr.hip):
-    128 x ``bn`` tiles, one per workgroup per round, A staged by LDS-DMA, EPI_STORE / EPI_RESID
-    (with the fused-RMSNorm sums of squares, ``ep.ss_out``) / EPI_QKV (with the fused RMSNorm row
-    scale, ``ep.ss_in``) / EPI_PARTIAL (every tile split into ``split`` K ranges of multiples of
-    256; fp32 partial k to ``ep.out`` [k][M][ldo], summed by :func:`resid_rmsnorm_partials`;
-    ``out_numel`` = the buffer's capacity in floats, checked). K % 256 == 0, N % bn == 0.
-    ``ng`` = 2: two wave groups per tile, each over half the K range (bn 128, EPI_STORE /
-    EPI_RESID, K % 512 == 0)."""
+    128 x ``bn`` tiles, one per workgroup per round, A staged by LDS-DMA, EPI_STORE / EPI_QKV
+    (with the fused RMSNorm row scale, ``ep.ss_in``). K % 256 == 0, N % bn == 0."""
     _req(_is_bf16_cuda(a, wp), "gemm_wr: bf16 cuda tensors required")
     _req(wp.numel() == N * K and K % 256 == 0, "gemm_wr: packed weight shape (K % 256 == 0)")
     _req(a.dim() == 2 and a.shape[0] >= M >= 1 and a.shape[1] >= K and a.stride(1) == 1 and a.stride(0) % 8 == 0
          and a.data_ptr() % 16 == 0, "gemm_wr: A must be [>=M, >=K] row-major with 16-B aligned rows")
     _req(bn in (128, 192, 256) and N % bn == 0, f"gemm_wr: N={N} does not tile by bn={bn}")
-    _req(epi in (EPI_STORE, EPI_QKV, EPI_PARTIAL, EPI_RESID), "gemm_wr: EPI_STORE / EPI_RESID / EPI_QKV / EPI_PARTIAL")
-    _req(not ep.ss_out or (epi == EPI_RESID and N % 64 == 0 and ep.ss_n == N // 64), "gemm_wr: ss_out shape")
-    _req(split == 1 or (epi == EPI_PARTIAL and 1 <= split <= K // 256), f"gemm_wr: split {split}")
-    _req(ng == 1 or (ng == 2 and bn == 128 and epi in (EPI_STORE, EPI_RESID) and split == 1 and K % 512 == 0),
-         f"gemm_wr: ng {ng} (2: bn 128, store / resid, K % 512 == 0)")
-    if epi == EPI_PARTIAL:
-        _req(out_numel >= split * M * ep.ldo, f"gemm_wr partial: output holds {out_numel} floats, "
-             f"split {split} x {M} rows x ldo {ep.ldo} needed")
+    _req(epi in (EPI_STORE, EPI_QKV), "gemm_wr: EPI_STORE / EPI_QKV")
+    _req(not ep.ss_out, "gemm_wr: no ss_out epilogue")
     _check_epi(epi, ep, N)
-    rc = lib().lsa_gemm_wr(_p(a), a.stride(0), _p(wp), M, N, K, epi, ctypes.byref(ep), bn, grid or N_CU, split, ng,
-                           _stream())
+    rc = lib().lsa_gemm_wr(_p(a), a.stride(0), _p(wp), M, N, K, epi, ctypes.byref(ep), bn, grid or N_CU, _stream())
     _check(rc, "lsa_gemm_wr")
 
 
@@ -427,10 +424,6 @@ def default_sk_workspace(device=None) -> SkWorkspace:
 
 
 N_CU = 256
-# gemm_sk: non-temporal weight DMA up to this many rows. Off by default: the ablation builds measured
-# 1.5-4 % at M = 512 (profiles/r3_gemm_sk_ablation.jsonl "w_nt"), but the re-tuned decode shapes and
-# the headline bench did not move beyond noise (36.33k vs 36.56k tok/s; profiles/r3_gemm_nt_retune.jsonl)
-SK_NT_MAX_ROWS = int(os.environ.get("LSA_SK_NT_MAX_ROWS", "0"))
 
 
 SK_TUNING_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_sk_tuning.json")
@@ -511,14 +504,12 @@ def gemm_sk_plan(M: int, N: int, K: int, tuned: bool = True) -> tuple:
 
 def gemm_sk(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep: EpiArgs,
             bn: int = 0, grid: int = 0, dp: int = 1, group_m: int = 8, nb: int = 0, split: int = -1,
-            ws: Optional[SkWorkspace] = None, bm: int = 0, out_numel: int = 0, wnt: Optional[bool] = None) -> None:
+            ws: Optional[SkWorkspace] = None, bm: int = 0, out_numel: int = 0) -> None:
     """Projection GEMM for any M (gemm_sk.hip): ``bm`` x ``bn`` tiles (bm 256 / 128), LDS-DMA
     staged, data-parallel rounds + stream-K, fused epilogue. ``wp`` = pack_b(W[N, K]); K % 64
     == 0; N % bn == 0 for bn = 128 / 256, N % 16 == 0 for bn = 192 (partial last column tile).
     bn = bm = 0: the plan's (gemm_sk_plan). EPI_PARTIAL writes ``split`` x M x ldo fp32 values
-    to ``ep.out``: ``out_numel`` (its capacity in floats) is required and checked first.
-    ``wnt``: non-temporal weight DMA (default: M <= SK_NT_MAX_ROWS, the decode-sized GEMMs whose
-    weights are streamed once)."""
+    to ``ep.out``: ``out_numel`` (its capacity in floats) is required and checked first."""
     _req(_is_bf16_cuda(a, wp), "gemm_sk: bf16 cuda tensors required")
     _req(wp.numel() == N * K and K % 64 == 0 and K >= 64, "gemm_sk: packed weight shape")
     _req(a.dim() == 2 and a.shape[0] >= M >= 1 and a.shape[1] >= K and a.stride(1) == 1 and a.stride(0) % 8 == 0,
@@ -554,10 +545,8 @@ def gemm_sk(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int,
     _req(bm in (128, 256), "gemm_sk: bm")
     _req(ws.slab.numel() >= 2 * grid * bm * bn and ws.counters.numel() >= 2 * grid,
          f"gemm_sk: workspace too small for grid={grid} bn={bn}")
-    if wnt is None:
-        wnt = M <= SK_NT_MAX_ROWS
     rc = lib().lsa_gemm_sk(_p(a), a.stride(0), _p(wp), M, N, K, epi, ctypes.byref(ep), bm, bn, nb, grid, dp, split, group_m,
-                           _p(ws.slab), _p(ws.counters), ws.slab.numel(), ws.counters.numel(), int(bool(wnt)), _stream())
+                           _p(ws.slab), _p(ws.counters), ws.slab.numel(), ws.counters.numel(), _stream())
     _check(rc, "lsa_gemm_sk")
 
 

@@ -40,7 +40,7 @@ def main():
                 def run(j, L=L):
                     rc = L.lsa_gemm_sk(x.data_ptr(), K, wps[j % nbuf].data_ptr(), M, N, K, e, ctypes.byref(ep), bm, bn,
                                        0, hip.N_CU, 1, split, 8, ws.slab.data_ptr(), ws.counters.data_ptr(),
-                                       ws.slab.numel(), ws.counters.numel(), 0, torch.cuda.current_stream().cuda_stream)
+                                       ws.slab.numel(), ws.counters.numel(), torch.cuda.current_stream().cuda_stream)
                     assert rc == 0, rc
                 res[name].append(timeit(run))
                 if rnd == 0:

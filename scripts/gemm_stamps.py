@@ -49,7 +49,7 @@ def main():
         rc = L.lsa_gemm_sk(ctypes.c_void_p(x.data_ptr()), x.stride(0), ctypes.c_void_p(wps[r % nbuf].data_ptr()), M, N, K,
                            hip.EPI_STORE, ctypes.byref(ep), bm, bn, 0, grid, dp, split, 8,
                            ctypes.c_void_p(ws.slab.data_ptr()), ctypes.c_void_p(ws.counters.data_ptr()),
-                           ws.slab.numel(), ws.counters.numel(), 0, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+                           ws.slab.numel(), ws.counters.numel(), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
         assert rc == 0, rc
         torch.cuda.synchronize()
     s = st.view(-1, 32).cpu().double()

@@ -2,7 +2,6 @@
 """Experimental W-in-registers GEMM (csrc/kernels/gemm_wr.hip) vs gemm_sk: correctness against
 fp32 torch and timing (cold weights: a ring of weight copies larger than the Infinity Cache).
 usage: gemm_wr_probe.py [M,N,K ...]"""
-import ctypes
 import json
 import os
 import sys
@@ -30,11 +29,6 @@ def timeit(fn, reps=20):
 
 
 def main():
-    L = hip.lib()
-    if os.environ.get("WR_LIB"):  # an ablation build of gemm_wr.hip (-DLSA_WR_ABLATE=n)
-        L = ctypes.CDLL(os.environ["WR_LIB"])
-    vp, i = ctypes.c_void_p, ctypes.c_int
-    L.lsa_gemm_wr.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(hip.EpiArgs), i, i, i, i, vp]
     shapes = [tuple(int(v) for v in a.split(",")) for a in sys.argv[1:]] or [
         (512, 12288, 4096), (512, 22016, 4096), (512, 4096, 11008), (512, 4096, 4096), (16384, 4096, 4096)]
     for M, N, K in shapes:
@@ -43,46 +37,25 @@ def main():
         wps = [packing.pack_b(w) for w in ws]
         x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
         ref = (x.float() @ ws[0].float().T)
-        stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
         res = {"M": M, "N": N, "K": K}
-        only = os.environ.get("WR_ONLY")  # "bn,ng,grid": one configuration (profiling)
-        cfgs = [tuple(int(v) for v in only.split(","))] if only else [
-            (bn, ng, g) for bn in (128, 192, 256) for ng in ((1, 2) if bn == 128 else (1,)) for g in (256, 512)]
-        for bn, ng, grid in cfgs:
-            if ng == 2 and K % 512:
-                continue
+        only = os.environ.get("WR_ONLY")  # "bn,grid": one configuration (profiling)
+        cfgs = [tuple(int(v) for v in only.split(","))] if only else [(bn, g) for bn in (128, 192, 256) for g in (256, 512)]
+        for bn, grid in cfgs:
             if N % bn:
                 continue
-            if True:
-                if True:
-                    out = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+            out = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+            epw = hip.make_epi(out=out, ldo=N)
 
-                    epw = hip.make_epi(out=out, ldo=N)
-
-                    def run(r=0, bn=bn, grid=grid, epw=epw, ng=ng):
-                        rc = L.lsa_gemm_wr(vp(x.data_ptr()), K, vp(wps[r % nbuf].data_ptr()), M, N, K, hip.EPI_STORE,
-                                           ctypes.byref(epw), bn, grid, 1, ng, stream)
-                        assert rc == 0, rc
-                    run(0)
-                    torch.cuda.synchronize()
-                    err = ((out.float() - ref).norm() / ref.norm()).item()
-                    us = timeit(run)
-                    res[f"bn{bn}_ng{ng}_g{grid}"] = [round(us, 2), round(2 * M * N * K / us / 1e6, 1), f"{err:.1e}"]
-        if os.environ.get("WR_ONLY"):
-            print(json.dumps(res), flush=True)
-            continue
-        # gemm_sk at its tuned plan, same cold-weight ring
-        out = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
-        ep = hip.make_epi(out=out, ldo=N)
-
-        def run_sk(r=0):
-            hip.gemm_sk(x, wps[r % nbuf], M, N, K, hip.EPI_STORE, ep)
-        run_sk()
-        torch.cuda.synchronize()
-        err = ((out.float() - ref).norm() / ref.norm()).item()
-        us = timeit(run_sk)
-        res["gemm_sk"] = [round(us, 2), round(2 * M * N * K / us / 1e6, 1), f"{err:.1e}"]
+            def run(r=0, bn=bn, grid=grid, epw=epw):
+                hip.gemm_wr(x, wps[r % nbuf], M, N, K, hip.EPI_STORE, epw, bn=bn, grid=grid)
+            run(0)
+            torch.cuda.synchronize()
+            err = ((out.float() - ref).norm() / ref.norm()).item()
+            us = timeit(run)
+            res[f"bn{bn}_g{grid}"] = [round(us, 2), round(2 * M * N * K / us / 1e6, 1), f"{err:.1e}"]
         print(json.dumps(res), flush=True)
+        del ws, wps
+        torch.cuda.empty_cache()
 
 
 if __name__ == "__main__":

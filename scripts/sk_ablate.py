@@ -62,7 +62,7 @@ def main():
             def run(it, L=L):
                 rc = L.lsa_gemm_sk(x.data_ptr(), x.stride(0), wps[it % nbuf].data_ptr(), M, N, K, hip.EPI_STORE,
                                    ctypes.byref(ep), 256, bn, 0, hip.N_CU, 1, split, 8, ws.slab.data_ptr(),
-                                   ws.counters.data_ptr(), ws.slab.numel(), ws.counters.numel(), 0,
+                                   ws.counters.data_ptr(), ws.slab.numel(), ws.counters.numel(),
                                    torch.cuda.current_stream().cuda_stream)
                 assert rc == 0, rc
             res[v] = round(timeit(run), 2)

@@ -30,32 +30,23 @@ def test_cost_model_for_untuned_shapes():
 
 
 def test_gemm_wr_route(monkeypatch):
-    """hip.gemm sends a projection to gemm_wr.hip only where it measured faster than gemm_sk: one
-    round of 224-256 whole 128 x 192 tiles with a store / QKV epilogue (the 7B qkv projection at
-    448-512 rows), and, opted in with LSA_GEMM_WR_RESID=1, the residual projection with 4 x 28-32
-    128-column tiles on two wave groups (the 7B o projection at 448-512 rows); everything else, and
-    LSA_GEMM_WR=0, stays on gemm_sk."""
+    """hip.gemm sends a projection to gemm_wr.hip only where it measured faster than gemm_sk in the
+    engine: one round of 224-256 whole 128 x 192 tiles with a store / QKV epilogue, for the measured
+    (N, K) pairs only (the 7B qkv projection at 448-512 rows); everything else, and LSA_GEMM_WR=0,
+    stays on gemm_sk."""
     monkeypatch.delenv("LSA_GEMM_WR", raising=False)
-    monkeypatch.delenv("LSA_GEMM_WR_RESID", raising=False)
     ep = hip.EpiArgs()
-    assert hip.gemm_wr_plan(512, 4096, 4096, hip.EPI_RESID, ep) is None  # off by default (slower in the engine)
-    monkeypatch.setenv("LSA_GEMM_WR_RESID", "1")
-    assert hip.gemm_wr_plan(512, 12288, 4096, hip.EPI_QKV, ep) == (192, 1)
-    assert hip.gemm_wr_plan(448, 12288, 4096, hip.EPI_STORE, ep) == (192, 1)
+    assert hip.gemm_wr_plan(512, 12288, 4096, hip.EPI_QKV, ep) == 192
+    assert hip.gemm_wr_plan(448, 12288, 4096, hip.EPI_STORE, ep) == 192
     assert hip.gemm_wr_plan(447, 12288, 4096, hip.EPI_STORE, ep) is None  # last row tile < half full
-    assert hip.gemm_wr_plan(512, 4096, 4096, hip.EPI_RESID, ep) == (128, 2)
-    assert hip.gemm_wr_plan(450, 4096, 4096, hip.EPI_RESID, ep) == (128, 2)
     for M, N, K, epi in [(384, 12288, 4096, hip.EPI_QKV),   # 3 row tiles: 192 tiles
                          (513, 12288, 4096, hip.EPI_QKV),   # 5 row tiles: 320 tiles
                          (512, 12288, 4096, hip.EPI_SWIGLU),
-                         (512, 4096, 11008, hip.EPI_RESID),  # down: K % 512 != 0
-                         (384, 4096, 4096, hip.EPI_RESID),   # 3 row tiles
-                         (512, 8192, 4096, hip.EPI_RESID),   # 256 tiles: unmeasured
+                         (512, 4096, 4096, hip.EPI_RESID),
+                         (384, 15360, 5120, hip.EPI_QKV),   # 13B qkv: tiles by 192, never measured
+                         (1024, 6144, 4096, hip.EPI_QKV),   # 224 tiles, never measured
                          (512, 22016, 4096, hip.EPI_SWIGLU),
                          (512, 12288, 4160, hip.EPI_QKV)]:  # K % 256 != 0
         assert hip.gemm_wr_plan(M, N, K, epi, ep) is None, (M, N, K, epi)
-    monkeypatch.setenv("LSA_GEMM_WR_RESID", "0")
-    assert hip.gemm_wr_plan(512, 4096, 4096, hip.EPI_RESID, ep) is None
-    assert hip.gemm_wr_plan(512, 12288, 4096, hip.EPI_QKV, ep) == (192, 1)
     monkeypatch.setenv("LSA_GEMM_WR", "0")
     assert hip.gemm_wr_plan(512, 12288, 4096, hip.EPI_QKV, ep) is None
