@@ -361,31 +361,4 @@ extern "C" int lsa_pos_advance(int* pos, int rows, int inc, hipStream_t stream) 
   return LSA_OK;
 }
 
-// Infinity-Cache warm-up: every byte of [p, p + bytes) is read once (16 B per lane, default
-// cache policy, so the lines allocate in the die-level cache on their way from HBM) and nothing is
-// written. Runs on a side stream of the batch-1 decode graph, one projection ahead of the chain,
-// so the next projection's weights stream from the Infinity Cache (MI355X_MICROARCH.md
-// "Infinity Cache"). The folded value goes to `sink` only if it equals an impossible pattern,
-// which keeps the loads live without a store.
-__global__ __launch_bounds__(256) void mall_prefetch_kernel(const u32x4_t* __restrict__ p, long long n16,
-                                                            unsigned* __restrict__ sink) {
-  const long long stride = (long long)gridDim.x * 256;
-  u32x4_t acc = {0u, 0u, 0u, 0u};
-  long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  for (; i + 3 * stride < n16; i += 4 * stride) {
-    const u32x4_t a = p[i], b = p[i + stride], c = p[i + 2 * stride], d = p[i + 3 * stride];
-    acc ^= a ^ b ^ c ^ d;
-  }
-  for (; i < n16; i += stride) acc ^= p[i];
-  const unsigned v = acc[0] ^ acc[1] ^ acc[2] ^ acc[3];
-  if (v == 0x9e3779b9u && acc[0] == 0x7f4a7c15u) sink[0] = v;
-}
-
-extern "C" int lsa_mall_prefetch(const void* p, long long bytes, int grid, unsigned* sink, hipStream_t stream) {
-  if (!p || bytes < 16 || bytes % 16 || grid < 1 || !sink) return LSA_BAD_SHAPE;
-  mall_prefetch_kernel<<<grid, 256, 0, stream>>>(static_cast<const u32x4_t*>(p), bytes / 16, sink);
-  LSA_CHECK_LAUNCH();
-  return LSA_OK;
-}
-
 extern "C" int lsa_version() { return 1; }

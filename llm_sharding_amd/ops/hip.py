@@ -73,14 +73,13 @@ def lib() -> ctypes.CDLL:
     L.lsa_row_ss.argtypes = [vp, i, i, i, vp, vp]
     L.lsa_argmax_finalize.argtypes = [vp, i, vp, vp, i, vp, i, i, vp, vp]
     L.lsa_pos_advance.argtypes = [vp, i, i, vp]
-    L.lsa_mall_prefetch.argtypes = [vp, ctypes.c_longlong, i, vp, vp]
     L.lsa_gemm_wr.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(EpiArgs), i, i, vp]
     L.lsa_gemm_sk.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(EpiArgs), i, i, i, i, i, i, i, vp, vp, ctypes.c_longlong, i,
                               vp]
     for name in ("lsa_gemv", "lsa_gemv_coop", "lsa_gemv_fp8", "lsa_dequant_fp8_packed", "lsa_gemv_coop_fp8", "lsa_gemm",
                  "lsa_gemm_sk", "lsa_gemm_wr", "lsa_attn_decode", "lsa_attn_prefill", "lsa_embed", "lsa_rmsnorm", "lsa_layernorm",
                  "lsa_resid_rmsnorm_partials", "lsa_row_ss",
-                 "lsa_argmax_finalize", "lsa_pos_advance", "lsa_mall_prefetch", "lsa_version"):
+                 "lsa_argmax_finalize", "lsa_pos_advance", "lsa_version"):
         getattr(L, name).restype = ctypes.c_int
     _lib = L
     return L
@@ -132,20 +131,6 @@ def make_epi(out=None, resid=None, k_cache=None, v_cache=None, slot=None, pos=No
     return EpiArgs(_p(out), _p(resid), _p(k_cache), _p(v_cache), _p(slot), _p(pos), _p(cos), _p(sin),
                    _p(keys), _p(bias), ldo, ldr, n_heads, n_kv, head_dim, t_max, col_offset, int(act),
                    _p(ss_out), _p(ss_in), 0 if ssb is None else ssb.shape[1], float(ss_eps))
-
-
-def mall_prefetch(t: torch.Tensor, sink: torch.Tensor, nbytes: int = 0, offset: int = 0, grid: int = 64) -> None:
-    """Read ``nbytes`` of ``t`` (from byte ``offset``; 0 = to the end) once so the lines settle in
-    the Infinity Cache; writes nothing (``sink``: an int32 scratch word the kernel never stores
-    to in practice)."""
-    _req(t.is_cuda and t.is_contiguous(), "mall_prefetch: contiguous device tensor")
-    total = t.numel() * t.element_size()
-    nbytes = (total - offset) if nbytes <= 0 else nbytes
-    _req(0 <= offset and offset + nbytes <= total and offset % 16 == 0 and nbytes % 16 == 0 and nbytes >= 16,
-         "mall_prefetch: range")
-    _req(sink.is_cuda and sink.dtype == torch.int32, "mall_prefetch: sink")
-    _check(lib().lsa_mall_prefetch(ctypes.c_void_p(t.data_ptr() + offset), nbytes, grid, _p(sink), _stream()),
-           "lsa_mall_prefetch")
 
 
 # ------------------------------------------------------------------------------ projections

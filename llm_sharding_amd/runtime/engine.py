@@ -692,12 +692,6 @@ class StageEngine:
         # row by its rstd in the epilogue - no standalone norm kernel between projections
         fuse = not decode and self.ss_buf is not None and rows <= self.ss_buf.shape[0]
         ss = self.ss_buf[:rows] if fuse else None
-        # small decode batches: a side stream warms the Infinity Cache with the weights of the
-        # projections that follow the attention (o, then the head of gate_up) while the chain
-        # runs qkv's tail, the attention and the launch boundaries (the weight stream of a
-        # batch-1 step is otherwise idle there); joined at the end of the forward
-        pf = self._pf_plan(rows)
-        cur = torch.cuda.current_stream(self.device) if pf else None
         ss_valid = False  # ss holds the partials of hbuf's current values
         pending = 0  # down-projection partials not yet added to hbuf
         for li, lw in enumerate(self.layers):
@@ -727,12 +721,6 @@ class StageEngine:
                 else:
                     hip.rmsnorm(hbuf, None, xn, rows, eps, H)
                     pre(xn, lw.qkv, lw.qkv_s, cfg.qkv_size, H, hip.EPI_QKV, ep_qkv)
-            if pf:
-                self._pf_stream.wait_stream(cur)  # after qkv(l): overlaps the attention
-                with torch.cuda.stream(self._pf_stream):
-                    for t, nbytes in ((lw.o, pf[0]), (lw.gate_up, pf[1])):
-                        if nbytes:
-                            hip.mall_prefetch(t, self._pf_sink, nbytes=min(nbytes, t.numel() * 2), grid=pf[2])
             if tiles is not None:
                 hip.attn_prefill(q, kc, vc, tiles[1], nh, nkv, hd, attn_o, causal=kv_len is None, tiles_host=tiles[0])
             else:
@@ -761,24 +749,7 @@ class StageEngine:
                 ss_valid = fuse and not pending
         if pending:  # the stage's output residual stream
             hip.resid_rmsnorm_partials(hbuf, self.part_k, pending, rows, eps)
-        if pf:
-            cur.wait_stream(self._pf_stream)
         return hbuf
-
-    # LSA_MALL_PF="<o MB>,<gate_up MB>,<grid>,<max rows>" (A/B switch; "" = off)
-    MALL_PF = os.environ.get("LSA_MALL_PF", "")
-
-    def _pf_plan(self, rows: int):
-        if not self.MALL_PF or not self.gpu or self.fp8 or self.cfg.is_gpt2:
-            return None
-        o_mb, gu_mb, grid, max_rows = (self.MALL_PF.split(",") + ["34", "64", "32", "16"][len(self.MALL_PF.split(",")):])[:4]
-        if rows > int(max_rows):
-            return None
-        if getattr(self, "_pf_stream", None) is None:
-            self._pf_stream = torch.cuda.Stream(self.device)
-            self._pf_sink = torch.zeros(4, dtype=torch.int32, device=self.device)
-        mb = 1 << 20
-        return (int(float(o_mb) * mb) // 16 * 16, int(float(gu_mb) * mb) // 16 * 16, int(grid))
 
     def _forward_hip_gpt2(self, hbuf, slot, pos, kv_len, rows, nsplit, tiles, decode, native_fp8) -> torch.Tensor:
         """GPT-2 layer on the HIP path: LayerNorm kernel (ln_1, with the wpe add fused in front
@@ -809,12 +780,6 @@ class StageEngine:
             ep_qkv = hip.make_epi(out=q, k_cache=kc, v_cache=vc, slot=slot, pos=pos, ldo=q.stride(0), n_heads=nh,
                                   n_kv=nkv, head_dim=hd, t_max=self.max_seq, bias=lw.qkv_b)
             proj(xn, lw.qkv, lw.qkv_s, cfg.qkv_size, H, hip.EPI_QKV, ep_qkv)
-            if pf:
-                self._pf_stream.wait_stream(cur)  # after qkv(l): overlaps the attention
-                with torch.cuda.stream(self._pf_stream):
-                    for t, nbytes in ((lw.o, pf[0]), (lw.gate_up, pf[1])):
-                        if nbytes:
-                            hip.mall_prefetch(t, self._pf_sink, nbytes=min(nbytes, t.numel() * 2), grid=pf[2])
             if tiles is not None:
                 hip.attn_prefill(q, kc, vc, tiles[1], nh, nkv, hd, attn_o, causal=kv_len is None, tiles_host=tiles[0])
             else:
