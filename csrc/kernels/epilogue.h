@@ -111,6 +111,23 @@ LSA_DEVICE void epi_qkv_store(const EpiArgs& ep, int m, int n, float v, float vp
 // (packed column order). One thread per (tile, row) instead of one per element: 16-B stores,
 // 16-B residual / bias / cos / sin loads, the index math (shifts: head_dim is a power of two)
 // done once per 16 outputs. EPI_SWIGLU and EPI_ARGMAX are handled by the callers.
+// 16-B store; WT: write-through to memory (two 8-B agent-scope relaxed atomic stores = sc1), so a
+// consumer on another CU / XCD may read the bytes after an arrival counter with no release
+// fence on this side (MI355X_MICROARCH.md 'Valid forms'; qkv_attn.hip)
+template <bool WT>
+LSA_DEVICE void st16x(void* p, u32x4_t v) {
+  if constexpr (WT) {
+    unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
+    __hip_atomic_store(q, (unsigned long long)v[0] | ((unsigned long long)v[1] << 32), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(q + 1, (unsigned long long)v[2] | ((unsigned long long)v[3] << 32), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    st16(p, v);
+  }
+}
+
+template <bool WT = false>
 LSA_DEVICE void epi_qkv_row16(const EpiArgs& ep, int m, int c0, const float* v) {
   const int hd = ep.head_dim, sh = __builtin_ctz((unsigned)hd);
   const int qs = ep.n_heads << sh, ks = ep.n_kv << sh;
@@ -123,8 +140,8 @@ LSA_DEVICE void epi_qkv_row16(const EpiArgs& ep, int m, int c0, const float* v) 
                            : (sec == 1 ? ep.k_cache : ep.v_cache) +
                                  ((((size_t)ep.slot[m] * ep.n_kv + head) * ep.t_max + p) << sh);
   if (ep.cos_t == nullptr || sec == 2) {  // v (or no RoPE): natural order, 16 contiguous dims
-    st16(dst + c, pack8(v));
-    st16(dst + c + 8, pack8(v + 8));
+    st16x<WT>(dst + c, pack8(v));
+    st16x<WT>(dst + c + 8, pack8(v + 8));
     return;
   }
   // rotate_half pairs live in this tile: columns 0..7 -> dims 8tt+j, 8..15 -> hd/2 + 8tt + j
@@ -141,8 +158,8 @@ LSA_DEVICE void epi_qkv_row16(const EpiArgs& ep, int m, int c0, const float* v) 
     lo[j] = v[j] * cs[j] - v[j + 8] * sn[j];
     hi[j] = v[j + 8] * cs[j] + v[j] * sn[j];
   }
-  st16(dst + fi0, pack8(lo));
-  st16(dst + half + fi0, pack8(hi));
+  st16x<WT>(dst + fi0, pack8(lo));
+  st16x<WT>(dst + half + fi0, pack8(hi));
 }
 
 // Adds the bias (if any) to v in place.

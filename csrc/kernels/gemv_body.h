@@ -22,7 +22,9 @@
 #pragma once
 #include "epilogue.h"
 
-template <int TN, int MB, int NW, int U, int EPI, bool NORM>
+// WT (EPI_QKV only): the q / k / v outputs leave through 16-B write-through stores (one thread
+// per 16-column tile row, epi_qkv_row16<true>) for an in-launch consumer (qkv_attn.hip)
+template <int TN, int MB, int NW, int U, int EPI, bool NORM, bool WT = false>
 LSA_DEVICE void gemv_packed_body(const bf16_raw* __restrict__ x, int ldx, const int* __restrict__ a_rows,
                                  const bf16_raw* __restrict__ wp, int M, int N, int K, float eps, const EpiArgs& ep,
                                  int block) {
@@ -164,6 +166,16 @@ LSA_DEVICE void gemv_packed_body(const bf16_raw* __restrict__ x, int ldx, const 
       const float g = rsum(2 * tp, mm, n) * r, u = rsum(2 * tp + 1, mm, n) * r;
       const int col = (nt0 / 2 + tp) * 16 + n;
       ep.out[(size_t)mm * ep.ldo + col] = f2bf(silu(g) * u);
+    }
+  } else if (EPI == EPI_QKV && WT) {
+    for (int e = tid; e < TN * MR; e += NTHR) {
+      const int t = e / MR, mm = e % MR;
+      if (mm >= M) continue;
+      const float r = rstd(mm);
+      float v[16];
+#pragma unroll
+      for (int n = 0; n < 16; ++n) v[n] = rsum(t, mm, n) * r;
+      epi_qkv_row16<true>(ep, mm, (nt0 + t) * 16, v);
     }
   } else {
     for (int e = tid; e < TN * MR * 16; e += NTHR) {

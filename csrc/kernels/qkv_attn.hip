@@ -6,8 +6,9 @@
 // while the qkv GEMV in front of it streams 100 MB. Here the attention of kv group g starts as
 // soon as the q / k / v tiles of group g have been stored, inside the same grid:
 //  * blocks [0, n_prod): the GEMV of gemv_body.h (one workgroup per TN 16-column tiles). A
-//    workgroup's tiles belong to exactly one kv group g ((head_dim / 16) % TN == 0); once its
-//    stores are drained it publishes them (agent release) and adds 1 to sync[g].
+//    workgroup's tiles belong to exactly one kv group g ((head_dim / 16) % TN == 0); its q / k /
+//    v stores are write-through (sc1, 16 B), so once they are drained it adds 1 to sync[g] (no
+//    release fence: MI355X_MICROARCH.md 'Valid forms', sc1 stores + consumer acquire).
 //  * blocks [n_prod, n_prod + rows * n_kv): one attention workgroup per (row, kv group). It
 //    polls sync[g] (one lane, relaxed agent loads, s_sleep) until all (G + 2) * head_dim / 16 /
 //    TN producers of group g arrived, acquires (agent) and runs the split-KV attention body of
@@ -42,12 +43,12 @@ __global__ __launch_bounds__(ATT_THR) void qkv_attn_kernel(const bf16_raw* __res
   constexpr int TPH = HD / 16;  // 16-column tiles per head
   const int b = blockIdx.x;
   if (b < n_prod) {
-    gemv_packed_body<TN, 1, ATT_WAVES, U, EPI_QKV, true>(x, ldx, nullptr, wp, M, N, K, eps, ep, b);
+    // q / k / v leave by write-through (sc1) 16-B stores: no L2 write-back (release fence) per
+    // workgroup - 768 of them at batch 1 made the launch 2x slower than the two it replaces
+    gemv_packed_body<TN, 1, ATT_WAVES, U, EPI_QKV, true, true>(x, ldx, nullptr, wp, M, N, K, eps, ep, b);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drained
     __syncthreads();
     if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the release completes before the arrival
       const int g = qa_group_of_tile(b * TN, ep.n_heads, ep.n_kv, G, TPH);
       __hip_atomic_fetch_add(sync + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }

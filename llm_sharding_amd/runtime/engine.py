@@ -174,7 +174,9 @@ def keys_max_torch(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
 
 
 class StageEngine:
-    DECODE_MAX_ROWS = packing.GEMV_MAX_ROWS  # rows handled by the weight-streaming GEMV paths (128)
+    DECODE_MAX_ROWS = packing.GEMV_MAX_ROWS  # rows handled by the decode attention / graph paths (128)
+    # rows above which the projections run on the MFMA GEMMs instead of the weight-streaming GEMVs
+    GEMV_MAX_ROWS = int(os.environ.get("LSA_GEMV_MAX_ROWS", str(packing.GEMV_MAX_ROWS)))
     # split-KV chunks never shorter than this many keys: below ~256 keys per split the merge
     # costs more than the extra parallelism buys (profiles/r1_bench_kernels_sweep.jsonl, attn)
     ATTN_MIN_CHUNK = int(os.environ.get("LSA_ATTN_MIN_CHUNK", "256"))  # keys per decode split, at least
@@ -676,7 +678,10 @@ class StageEngine:
 
         # residual projections as split-K partials summed by the next norm kernel, where measured
         # faster than the fused residual epilogue (ops/gemm_sk_tuning.json "partial" entries)
-        part_ok = not decode and self.part_k is not None and rows <= self.part_k.shape[1]
+        # the projection kernel family: the weight-streaming GEMVs up to GEMV_MAX_ROWS rows, the
+        # LDS-DMA MFMA GEMMs (gemm_sk / gemm_wr) above - independent of the attention's decode mode
+        proj_gemm = (not decode) or (rows > self.GEMV_MAX_ROWS and not native_fp8 and self.sk_ws is not None)
+        part_ok = proj_gemm and self.part_k is not None and rows <= self.part_k.shape[1]
 
         def resid_proj(x, w, s, N, K, ep):
             # returns the split count of partials left in part_k (0: residual applied in-GEMM)
@@ -692,7 +697,7 @@ class StageEngine:
         # RMSNorm fused across the GEMMs: residual GEMMs write per-64-column sums of squares of
         # their outputs (ss), the qkv / gate_up GEMMs read the raw residual stream and scale each
         # row by its rstd in the epilogue - no standalone norm kernel between projections
-        fuse = not decode and self.ss_buf is not None and rows <= self.ss_buf.shape[0]
+        fuse = proj_gemm and self.ss_buf is not None and rows <= self.ss_buf.shape[0]
         ss = self.ss_buf[:rows] if fuse else None
         ss_valid = False  # ss holds the partials of hbuf's current values
         pending = 0  # down-projection partials not yet added to hbuf
@@ -705,7 +710,7 @@ class StageEngine:
             if qa is not None and lw.qkv_s is None:
                 hip.qkv_attn(hbuf, lw.qkv, rows, cfg.qkv_size, H, eps, ep_qkv, attn_o,
                              self.attn_cnt[-2 * nkv:], self.qa_err, qa)
-            elif decode:
+            elif not proj_gemm:
                 dec(hbuf, lw.qkv, lw.qkv_s, cfg.qkv_size, H, hip.EPI_QKV, ep_qkv, norm=True)
             else:
                 if pending and not fuse:
@@ -735,7 +740,7 @@ class StageEngine:
                          kv_len=kv_len, counters=self.attn_cnt, min_chunk=self.ATTN_MIN_CHUNK)
             ep_o = hip.make_epi(out=hbuf, resid=hbuf, ldo=hbuf.stride(0), ldr=hbuf.stride(0))
             ep_gu = hip.make_epi(out=act, ldo=act.stride(0))
-            if decode:
+            if not proj_gemm:
                 dec_resid(attn_o, lw.o, lw.o_s, H, cfg.q_size, ep_o)
                 dec(hbuf, lw.gate_up, lw.gate_up_s, 2 * I, H, hip.EPI_SWIGLU, ep_gu, norm=True)
                 dec_resid(act, lw.down, lw.down_s, H, I, ep_o)
@@ -769,7 +774,7 @@ class StageEngine:
         from ..ops import hip
         cfg = self.cfg
         if (not self.QKV_ATTN or not self.gpu or native_fp8 or cfg.is_gpt2 or kv_len is not None or tiles is not None
-                or self.max_seq > self.QKV_ATTN_MAX_SEQ or rows > 16):
+                or self.max_seq > self.QKV_ATTN_MAX_SEQ or rows > min(16, self.GEMV_MAX_ROWS)):
             return None
         return hip.qkv_attn_config(rows, cfg.qkv_size, cfg.hidden_size, cfg.num_attention_heads,
                                    cfg.num_key_value_heads, cfg.head_dim)

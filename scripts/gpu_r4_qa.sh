@@ -17,3 +17,6 @@ f=$(find gpurun_out/r4_qa/p1 -name '*kernel_trace.csv' | head -1)
 python3 scripts/kstats.py $f flash_prefill 12 > gpurun_out/r4_qa/b1_kstats.txt
 rm -rf gpurun_out/r4_qa/p1
 head -16 gpurun_out/r4_qa/b1_kstats.txt
+timeout -k 10 300 python -u -m pytest tests/test_gemm_sk_gpu.py -x -q --timeout 120 --timeout-method thread \
+    > gpurun_out/r4_qa/pytest_sk.log 2>&1 || { tail -30 gpurun_out/r4_qa/pytest_sk.log; exit 4; }
+tail -2 gpurun_out/r4_qa/pytest_sk.log

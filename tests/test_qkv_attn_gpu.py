@@ -150,5 +150,5 @@ def test_decode_graph_fused_matches_unfused(monkeypatch, rows, shape):
         torch.cuda.synchronize()
         e.check_errors()
         hist.append(dg.history.cpu().tolist())
-    assert calls and all(r == rows for r in calls)
+    assert rows in calls  # (the 5-token prompts also take it: short prefills run the decode path)
     assert hist[0] == hist[1]
