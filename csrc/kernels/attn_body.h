@@ -1,7 +1,7 @@
 // Body of the split-KV decode attention (attention.hip, design notes there): one workgroup of
 // ATT_THR threads streams one contiguous chunk of a (row, kv-head)'s keys for the whole GQA
-// group. Shared by attn_split_kernel (attention.hip) and the fused QKV + attention kernel
-// (qkv_attn.hip).
+// group. Shared by attn_split_kernel (attention.hip) and the fused QKV + attention probe
+// (scripts/probes/qkv_attn.hip).
 #pragma once
 #include "common.h"
 
@@ -12,7 +12,9 @@ constexpr int ATT_MAX_SPLIT = 16;  // split-KV factor limit (the merge keeps one
 
 // U: key groups in flight per wave per iteration; PF: software-pipelined (the next iteration's
 // K/V loads issued before this one's math); NT: non-temporal K/V loads
-template <int HD, int G, int U = 4, int PF = 0, int NT = 0>
+// SPLIT = false: the caller guarantees nsplit == 1 (one workgroup per (row, kv head), output
+// written directly); the partial / merge code is then not compiled in at all.
+template <int HD, int G, int U = 4, int PF = 0, int NT = 0, bool SPLIT = true>
 LSA_DEVICE void attn_split_body(
     const bf16_raw* __restrict__ q, int ldq, const bf16_raw* __restrict__ kc,
     const bf16_raw* __restrict__ vc, const int* __restrict__ slot, const int* __restrict__ pos,
@@ -218,7 +220,7 @@ LSA_DEVICE void attn_split_body(
       ls += s_l[i][r] * a;
       os += s_o[i][r][d] * a;
     }
-    if (nact == 1) {  // lone active split: final output directly, no merge
+    if (!SPLIT || nact == 1) {  // lone active split: final output directly, no merge
       out[(size_t)row * ldo + (size_t)(kvh * G + r) * HD + d] = f2bf(os / ls);
     } else {
       const int pi = (int)(pbase + (size_t)r * nsplit);
@@ -226,6 +228,8 @@ LSA_DEVICE void attn_split_body(
       if (d == 0) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(mm + log2f(ls)), plr, pi * 4, 0, 16);
     }
   }
-  if (nact > 1) arrive();
+  if constexpr (SPLIT) {
+    if (nact > 1) arrive();
+  }
 }
 

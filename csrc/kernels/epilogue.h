@@ -113,7 +113,7 @@ LSA_DEVICE void epi_qkv_store(const EpiArgs& ep, int m, int n, float v, float vp
 // done once per 16 outputs. EPI_SWIGLU and EPI_ARGMAX are handled by the callers.
 // 16-B store; WT: write-through to memory (two 8-B agent-scope relaxed atomic stores = sc1), so a
 // consumer on another CU / XCD may read the bytes after an arrival counter with no release
-// fence on this side (MI355X_MICROARCH.md 'Valid forms'; qkv_attn.hip)
+// fence on this side (MI355X_MICROARCH.md 'Valid forms'; scripts/probes/qkv_attn.hip)
 template <bool WT>
 LSA_DEVICE void st16x(void* p, u32x4_t v) {
   if constexpr (WT) {

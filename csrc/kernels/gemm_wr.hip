@@ -33,24 +33,32 @@ LSA_DEVICE void wr_vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
 }
 
+template <int... S, typename F>
+LSA_DEVICE void wr_static_for(std::integer_sequence<int, S...>, F&& f) {
+  (f(std::integral_constant<int, S>{}), ...);
+}
+
 LSA_DEVICE void wr_barrier() {
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <int FN>
+template <int FN, int NS_>
 struct WrGeo {
   static constexpr int TN = FN * 16, BN = 4 * TN;
-  static constexpr int NS = 4;                        // W register slots = A ring slots (distance 3)
+  static constexpr int NS = NS_;                      // W register slots = A ring slots (distance NS-1)
   static constexpr int ADMA = WR_ABUF / 1024 / 4;     // A DMA instructions per wave per step (4)
   static constexpr int PER = 2 * FN + ADMA;           // VMEM instructions per wave per step
   static constexpr int ELD = TN + 4;                  // fp32 row stride of the epilogue image
   static constexpr int EPI_BYTES = 4 * WR_BM * ELD * 4;
   static constexpr int RS_OFF = (NS * WR_ABUF > EPI_BYTES ? NS * WR_ABUF : EPI_BYTES);  // row rstd [128]
   static constexpr int SMEM = RS_OFF + WR_BM * 4;
+  // counted waits: the prologue leaves NS-2 steps in flight, the mid-step wait NS-3 steps + one
+  // step's weights; vmcnt holds 6 bits
+  static constexpr int WAIT_PRO = (NS - 2) * PER, WAIT_MID = (NS - 3) * PER + 2 * FN;
   static_assert(SMEM <= 160 * 1024, "LDS budget");
-  static_assert(2 * PER <= 63, "vmcnt range");
+  static_assert(NS >= 4 && WAIT_PRO <= 63 && WAIT_MID <= 63, "vmcnt range");
   static_assert(ADMA == 4, "one A DMA block per two rows of phase B");
 };
 
@@ -67,12 +75,12 @@ struct WrGeo {
 //            step t+3 into ring slot (t+3)%4 = (t-1)%4.
 // (the body is a __device__ function: lambdas directly inside a __global__ template kept the
 // host pass from emitting the kernel's launch stub)
-template <int FN, int EPI>
+template <int FN, int NS_, int EPI>
 LSA_DEVICE void gemm_wr_body(unsigned char* smem, const bf16_raw* __restrict__ A, int lda,
                              const bf16_raw* __restrict__ Wp, int M, int N, int K, const EpiArgs& ep, int MT,
                              int NT) {
-  using G_ = WrGeo<FN>;
-  constexpr int TN = G_::TN, BN = G_::BN, NS = G_::NS, ADMA = G_::ADMA, PER = G_::PER;
+  using G_ = WrGeo<FN, NS_>;
+  constexpr int TN = G_::TN, BN = G_::BN, NS = G_::NS, ADMA = G_::ADMA;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // column owner
   const int G = gridDim.x;
@@ -88,7 +96,7 @@ LSA_DEVICE void gemm_wr_body(unsigned char* smem, const bf16_raw* __restrict__ A
   const unsigned roff1 = (lane & 15) * 128 + (((4 + (lane >> 4)) ^ (lane & 7)) * 16);
 
   // work item = tile: row tiles fastest, then column tiles (the items running together share
-  // weight panels); every tile covers the whole K range (64-deep steps [0, nsteps), K % 256 == 0)
+  // weight panels); every tile covers the whole K range (64-deep steps [0, nsteps), K % 64 == 0)
   for (int tile = g; tile < MT * NT; tile += G) {
     const int mt = tile % MT, nt = tile / MT;
     const int k0 = 0, nsteps = K / WR_BK;
@@ -140,27 +148,21 @@ LSA_DEVICE void gemm_wr_body(unsigned char* smem, const bf16_raw* __restrict__ A
       dst = ld16(smem + slot * WR_ABUF + i * 2048 + (kf1 ? roff1 : roff0));
     };
     // prologue: steps 0 .. NS-2 in flight (per step: W then A), A(0) kf0 frags read
-    static_assert(NS == 4, "prologue issues steps 0, 1, 2");
+    wr_static_for(std::make_integer_sequence<int, NS - 1>{}, [&](auto sc) {
+      constexpr int S = decltype(sc)::value;
 #pragma unroll
-    for (int v = 0; v < 2 * FN; ++v) wload(wr[0], v, k0);
+      for (int v = 0; v < 2 * FN; ++v) wload(wr[S], v, min(k0 + S, nsteps - 1));
 #pragma unroll
-    for (int s = 0; s < ADMA; ++s) aload(0, s, k0);
-#pragma unroll
-    for (int v = 0; v < 2 * FN; ++v) wload(wr[1], v, min(k0 + 1, nsteps - 1));
-#pragma unroll
-    for (int s = 0; s < ADMA; ++s) aload(1, s, min(k0 + 1, nsteps - 1));
-#pragma unroll
-    for (int v = 0; v < 2 * FN; ++v) wload(wr[2], v, min(k0 + 2, nsteps - 1));
-#pragma unroll
-    for (int s = 0; s < ADMA; ++s) aload(2, s, min(k0 + 2, nsteps - 1));
-    wr_vm_wait<(NS - 2) * PER>();
+      for (int s = 0; s < ADMA; ++s) aload(S, s, min(k0 + S, nsteps - 1));
+    });
+    wr_vm_wait<G_::WAIT_PRO>();
     wr_barrier();
 #pragma unroll
     for (int i = 0; i < 8; ++i) rd(0, false, a0[i], i);
 
-    // VMEM order per step: W(t+3) in phase A, A(t+3) in phase B; at barrier(t) A(t+1) and
-    // W(t+1) must have landed: issued after them are W(t+2), A(t+2), W(t+3)
-    constexpr int WAIT_MID = 2 * (2 * FN) + ADMA;
+    // VMEM order per step: W(t+NS-1) in phase A, A(t+NS-1) in phase B; at barrier(t) A(t+1)
+    // and W(t+1) must have landed: issued after them are W/A(t+2 .. t+NS-2) and W(t+NS-1)
+    constexpr int WAIT_MID = G_::WAIT_MID;
     auto step = [&](int t, auto slot_c) {
       constexpr int slot = decltype(slot_c)::value, nslot = (slot + NS - 1) % NS;
       const int tp = min(t + NS - 1, nsteps - 1);  // past the end: re-fetch the last step (dead)
@@ -191,11 +193,10 @@ LSA_DEVICE void gemm_wr_body(unsigned char* smem, const bf16_raw* __restrict__ A
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       }
     };
-    for (int t = k0; t < nsteps; t += NS) {  // k0, nsteps multiples of NS
-      step(t, std::integral_constant<int, 0>{});
-      step(t + 1, std::integral_constant<int, 1>{});
-      step(t + 2, std::integral_constant<int, 2>{});
-      step(t + 3, std::integral_constant<int, 3>{});
+    for (int t = k0; t < nsteps; t += NS) {  // k0 a multiple of NS; a partial last group is cut short
+      wr_static_for(std::make_integer_sequence<int, NS>{}, [&](auto sc) {
+        if (t + decltype(sc)::value < nsteps) step(t + decltype(sc)::value, sc);
+      });
     }
     wr_vm_wait<0>();  // the dead prefetches land before the LDS is reused
     // ... and before their destination registers are: the compiler sees the last group's weight
@@ -262,21 +263,21 @@ LSA_DEVICE void gemm_wr_body(unsigned char* smem, const bf16_raw* __restrict__ A
   }
 }
 
-template <int FN, int EPI>
+template <int FN, int NS, int EPI>
 __global__ __launch_bounds__(WR_NTHR) void gemm_wr_kernel(const bf16_raw* __restrict__ A, int lda,
                                                           const bf16_raw* __restrict__ Wp, int M, int N, int K,
                                                           EpiArgs ep, int MT, int NT) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[WrGeo<FN>::SMEM];
-  gemm_wr_body<FN, EPI>(smem, A, lda, Wp, M, N, K, ep, MT, NT);
+  __shared__ __attribute__((aligned(16))) unsigned char smem[WrGeo<FN, NS>::SMEM];
+  gemm_wr_body<FN, NS, EPI>(smem, A, lda, Wp, M, N, K, ep, MT, NT);
 }
 
-template <int FN, int EPI>
+template <int FN, int NS, int EPI>
 int wr_launch(const bf16_raw* A, int lda, const bf16_raw* W, int M, int N, int K, const EpiArgs& ep, int grid,
               hipStream_t s) {
-  constexpr int BN = WrGeo<FN>::BN;
+  constexpr int BN = WrGeo<FN, NS>::BN;
   const int MT = (M + WR_BM - 1) / WR_BM, NT = N / BN;
   const int items = MT * NT;
-  gemm_wr_kernel<FN, EPI><<<grid < items ? grid : items, WR_NTHR, 0, s>>>(A, lda, W, M, N, K, ep, MT, NT);
+  gemm_wr_kernel<FN, NS, EPI><<<grid < items ? grid : items, WR_NTHR, 0, s>>>(A, lda, W, M, N, K, ep, MT, NT);
   LSA_CHECK_LAUNCH();
   return LSA_OK;
 }
@@ -285,11 +286,14 @@ int wr_launch(const bf16_raw* A, int lda, const bf16_raw* W, int M, int N, int K
 
 // 128-row x bn tiles, weights straight into MFMA registers (see the header comment). epi:
 // EPI_STORE or EPI_QKV (with the fused-RMSNorm row scale when ep->ss_in is set: K == 64 ss_n).
-// bn: 128 / 192 / 256 with N % bn == 0; K % 256 == 0; grid: workgroups (tiles beyond it loop).
+// bn: 128 / 192 / 256 with N % bn == 0; K % 64 == 0; grid: workgroups (tiles beyond it loop).
 // Returns LSA_BAD_SHAPE on any shape the kernel's indexing cannot take.
+// (Ring depth: 4 slots. 6 and 8 slots - weights prefetched 5 / 7 K-steps ahead - measured no
+// faster on any 7B projection shape, profiles/r4_gemm_wr_depth.jsonl: the weight stream is not
+// latency-bound.)
 extern "C" int lsa_gemm_wr(const void* a, int lda, const void* wp, int M, int N, int K, int epi, const EpiArgs* ep,
                            int bn, int grid, hipStream_t stream) {
-  if (M < 1 || K < 4 * WR_BK || K % (4 * WR_BK) || lda < K || lda % 8 || grid < 1 || !ep) return LSA_BAD_SHAPE;
+  if (M < 1 || K < WR_BK || K % WR_BK || lda < K || lda % 8 || grid < 1 || !ep) return LSA_BAD_SHAPE;
   if (bn != 128 && bn != 192 && bn != 256) return LSA_UNSUPPORTED;
   if (N % bn) return LSA_BAD_SHAPE;
   if (epi != EPI_STORE && epi != EPI_QKV) return LSA_UNSUPPORTED;
@@ -300,8 +304,8 @@ extern "C" int lsa_gemm_wr(const void* a, int lda, const void* wp, int M, int N,
   const bf16_raw* A = static_cast<const bf16_raw*>(a);
   const bf16_raw* W = static_cast<const bf16_raw*>(wp);
 #define LSA_WR(FN)                                                                                    \
-  return epi == EPI_QKV ? wr_launch<FN, EPI_QKV>(A, lda, W, M, N, K, *ep, grid, stream)            \
-                        : wr_launch<FN, EPI_STORE>(A, lda, W, M, N, K, *ep, grid, stream);
+  return epi == EPI_QKV ? wr_launch<FN, 4, EPI_QKV>(A, lda, W, M, N, K, *ep, grid, stream)         \
+                        : wr_launch<FN, 4, EPI_STORE>(A, lda, W, M, N, K, *ep, grid, stream);
   if (bn == 128) { LSA_WR(2) }
   if (bn == 192) { LSA_WR(3) }
   LSA_WR(4)

@@ -1,6 +1,6 @@
 // Decode projection kernel: y[M, N] = A[M, K] @ W^T with M <= 64 (decode batch), bf16 in,
 // fp32 accumulate, fused RMSNorm and fused epilogues (epilogue.h). The body (design notes
-// there) lives in gemv_body.h, shared with the fused QKV + attention kernel (qkv_attn.hip).
+// there) lives in gemv_body.h, shared with the fused QKV + attention probe (scripts/probes/qkv_attn.hip).
 #include "gemv_body.h"
 
 namespace {

@@ -1,6 +1,6 @@
 // Body of the decode projection kernel (gemv.hip): y[M, N] = A[M, K] @ W^T, M <= 64, one
 // workgroup per TN 16-column tiles (``block``), fused RMSNorm + epilogues. Shared by
-// gemv_packed_kernel (gemv.hip) and the fused QKV + attention kernel (qkv_attn.hip).
+// gemv_packed_kernel (gemv.hip) and the fused QKV + attention probe (scripts/probes/qkv_attn.hip).
 //
 // Design (MI355X-first, not a translation of the reference's per-op nn.Linear calls in
 // /root/reference/utils/shard_loader.py:67-73 / node_worker.py:262):
@@ -23,7 +23,7 @@
 #include "epilogue.h"
 
 // WT (EPI_QKV only): the q / k / v outputs leave through 16-B write-through stores (one thread
-// per 16-column tile row, epi_qkv_row16<true>) for an in-launch consumer (qkv_attn.hip)
+// per 16-column tile row, epi_qkv_row16<true>) for an in-launch consumer (scripts/probes/qkv_attn.hip)
 template <int TN, int MB, int NW, int U, int EPI, bool NORM, bool WT = false>
 LSA_DEVICE void gemv_packed_body(const bf16_raw* __restrict__ x, int ldx, const int* __restrict__ a_rows,
                                  const bf16_raw* __restrict__ wp, int M, int N, int K, float eps, const EpiArgs& ep,

@@ -105,17 +105,21 @@ __global__ __launch_bounds__(NW * KW * 64) void gemv_coop_kernel(
 
   // ---- A staging: thread -> (row + i*RSTEP, 16-B chunk) fixed for all chunks, one load per
   // k-group per i
-  constexpr int LPT = MR * C16 / NTHR;         // A loads per thread per chunk and k-group (exact:
-  static_assert(LPT >= 1 && LPT * NTHR == MR * C16, "A tile must split evenly");  // no guards)
+  // A loads per thread per chunk and k-group; with 3- or 6-wave workgroups the tile does not
+  // split evenly and the last load's row can fall past the tile (in_tile: not stored, not summed)
+  constexpr int LPT = (MR * C16 + NTHR - 1) / NTHR;
+  constexpr bool A_EXACT = LPT * NTHR == MR * C16;
+  static_assert(NTHR % C16 == 0, "a thread keeps its 16-B column for every load");
   constexpr int RSTEP = NTHR / C16;
   const int arow = tid / C16, ac16 = tid % C16;
+  auto in_tile = [&](int i) { return A_EXACT || arow + i * RSTEP < MR; };
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, 0x7fffffff, 0x00020000);
   int a_voff[LPT];
   bool a_valid[LPT];
 #pragma unroll
   for (int i = 0; i < LPT; ++i) {
     const int r = arow + i * RSTEP;
-    a_valid[i] = r < M;
+    a_valid[i] = r < M && in_tile(i);
     a_voff[i] = ((a_valid[i] ? (a_rows ? a_rows[r] : r) : 0) * ldx + ac16 * 8) * 2;
   }
   const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)wp, (short)0, 0x7fffffff, 0x00020000);
@@ -150,7 +154,7 @@ __global__ __launch_bounds__(NW * KW * 64) void gemv_coop_kernel(
           for (int j = 0; j < 8; ++j) t += f[j] * f[j];
           ss[i] += count * t;
         }
-        *reinterpret_cast<u32x4_t*>(smem + buf * ABUFT + q * ABUF + a_off<KC>(arow + i * RSTEP, ac16)) = av;
+        if (in_tile(i)) *reinterpret_cast<u32x4_t*>(smem + buf * ABUFT + q * ABUF + a_off<KC>(arow + i * RSTEP, ac16)) = av;
       }
   };
   // B fragments: bf16 -> one 16-B load per k-fragment; FP8 (W8A16, packed as in gemv_fp8.hip)
@@ -305,7 +309,8 @@ __global__ __launch_bounds__(NW * KW * 64) void gemv_coop_kernel(
           red[((w * TNW + t) * MR + rb * 16 + (lane >> 4) * 4 + r) * RS + (lane & 15)] = acc[rb][t][r];
     if (NORM && ac16 == 0) {
 #pragma unroll
-      for (int i = 0; i < LPT; ++i) s_ss[arow + i * RSTEP] = ss[i];
+      for (int i = 0; i < LPT; ++i)
+        if (in_tile(i)) s_ss[arow + i * RSTEP] = ss[i];
     }
   } else {
     // Split-K hand-off (cdna_hip_programming.md §5 'In-launch split-K reduction', sc1 form):
@@ -329,8 +334,9 @@ __global__ __launch_bounds__(NW * KW * 64) void gemv_coop_kernel(
     if (NORM && ac16 == 0) {
 #pragma unroll
       for (int i = 0; i < LPT; ++i)
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ss[i]), sr, ((s * G + g) * MR + arow + i * RSTEP) * 4,
-                                              ss_base * 4, 16);
+        if (in_tile(i))
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ss[i]), sr, ((s * G + g) * MR + arow + i * RSTEP) * 4,
+                                                ss_base * 4, 16);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -487,13 +493,16 @@ int launch(bool norm, const bf16_raw* x, int ldx, const int* a_rows, const bf16_
   return LSA_OK;
 }
 
-// (mb, tnw, nw, kf, kw); kw > 1 needs mb*16*kf/8 a multiple of nw*kw*64 (exact A staging)
+// (mb, tnw, nw, kf, kw). nw = 3 / 6: one workgroup per CU for 768-tile projections (Llama-2-7B
+// qkv) with no split at all; nw = 1: one tile per workgroup (4096-column projections).
 #define LSA_COOP_CONFIGS(X) \
   X(2, 1, 8, 8, 1) X(4, 1, 8, 8, 1) X(2, 1, 8, 4, 1) X(4, 1, 8, 4, 1) X(2, 2, 8, 4, 1) X(4, 2, 8, 4, 1) X(2, 2, 4, 4, 1) \
   X(4, 2, 4, 4, 1) X(8, 1, 8, 4, 1) X(8, 1, 8, 2, 1) X(8, 2, 4, 2, 1) X(2, 1, 4, 4, 1) X(4, 1, 4, 4, 1) X(2, 1, 4, 8, 1) \
   X(8, 1, 4, 2, 1) \
   X(2, 1, 4, 8, 2) X(4, 1, 4, 4, 2) X(4, 1, 4, 8, 2) X(4, 1, 8, 4, 2) X(4, 2, 4, 4, 2) X(8, 1, 4, 2, 2) X(8, 1, 4, 4, 2) \
-  X(4, 1, 4, 4, 4) X(4, 1, 2, 4, 2) X(4, 1, 2, 4, 1) X(2, 1, 2, 4, 2) X(8, 1, 2, 2, 2)
+  X(4, 1, 4, 4, 4) X(4, 1, 2, 4, 2) X(4, 1, 2, 4, 1) X(2, 1, 2, 4, 2) X(8, 1, 2, 2, 2) \
+  X(8, 1, 3, 2, 1) X(8, 1, 3, 2, 2) X(8, 1, 6, 2, 1) X(8, 1, 1, 2, 2) X(8, 1, 1, 2, 4) X(8, 1, 2, 2, 1) \
+  X(4, 1, 3, 4, 1) X(4, 1, 3, 4, 2)
 
 // fp8-weight instantiations (subset; KF even so one 16-B load carries two k-fragments)
 #define LSA_COOP_FP8_CONFIGS(X) \
@@ -529,6 +538,7 @@ int coop_entry(const void* x, int ldx, const int* a_rows, const void* wp, int M,
   const int mb = M <= 32 ? 2 : (M <= 64 ? 4 : 8);
   const int tg = nw * tnw;
   if (N % (16 * tg) || sk > K / (32 * kf)) return LSA_BAD_SHAPE;
+  if (epi == EPI_SWIGLU && tg % 2) return LSA_BAD_SHAPE;  // gate / up tile pairs stay in one workgroup
   if (sk > 1 && (!slab || !counters)) return LSA_BAD_SHAPE;
   const bf16_raw* xx = static_cast<const bf16_raw*>(x);
   const bf16_raw* w = static_cast<const bf16_raw*>(wp);

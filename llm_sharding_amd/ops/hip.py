@@ -73,14 +73,13 @@ def lib() -> ctypes.CDLL:
     L.lsa_row_ss.argtypes = [vp, i, i, i, vp, vp]
     L.lsa_argmax_finalize.argtypes = [vp, i, vp, vp, i, vp, i, i, vp, vp]
     L.lsa_pos_advance.argtypes = [vp, i, i, vp]
-    L.lsa_qkv_attn.argtypes = [vp, i, vp, i, i, i, f, ctypes.POINTER(EpiArgs), i, i, i, f, vp, i, vp, vp, vp]
     L.lsa_gemm_wr.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(EpiArgs), i, i, vp]
     L.lsa_gemm_sk.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(EpiArgs), i, i, i, i, i, i, i, vp, vp, ctypes.c_longlong, i,
                               vp]
     for name in ("lsa_gemv", "lsa_gemv_coop", "lsa_gemv_fp8", "lsa_dequant_fp8_packed", "lsa_gemv_coop_fp8", "lsa_gemm",
                  "lsa_gemm_sk", "lsa_gemm_wr", "lsa_attn_decode", "lsa_attn_prefill", "lsa_embed", "lsa_rmsnorm", "lsa_layernorm",
                  "lsa_resid_rmsnorm_partials", "lsa_row_ss",
-                 "lsa_argmax_finalize", "lsa_pos_advance", "lsa_qkv_attn", "lsa_version"):
+                 "lsa_argmax_finalize", "lsa_pos_advance", "lsa_version"):
         getattr(L, name).restype = ctypes.c_int
     _lib = L
     return L
@@ -204,7 +203,8 @@ def gemv(x: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep
         if epi == EPI_PARTIAL:
             _req(out_numel >= sk * M * ep.ldo, f"gemv partial: output holds {out_numel} floats, "
                  f"{sk} splits x {M} rows x ldo {ep.ldo} needed")
-        _req(coop in coop_candidates(N // 16, K, M), f"gemv: coop config {coop} invalid for N={N} K={K} M={M}")
+        _req(coop in coop_candidates(N // 16, K, M, epi == EPI_SWIGLU),
+             f"gemv: coop config {coop} invalid for N={N} K={K} M={M}")
         if ws is None:
             ws = default_workspace(x.device)
         need = coop_slab_floats(N, M, tnw, cnw, kf, sk)
@@ -220,47 +220,6 @@ def gemv(x: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep
     rc = lib().lsa_gemv(_p(x), x.stride(0), _p(a_rows), _p(wp), M, N, K, int(norm), float(eps), epi,
                         ctypes.byref(ep), tn, nw, u, _stream())
     _check(rc, "lsa_gemv")
-
-
-QKV_ATTN_CONFIGS = {(1, 4, 4), (1, 4, 8), (2, 4, 4)}  # (tn, nw, u) built in qkv_attn.hip (streaming-GEMV configs, nw 4)
-
-
-def qkv_attn_config(M: int, N: int, K: int, n_heads: int, n_kv: int, head_dim: int) -> Optional[tuple]:
-    """The tuned streaming-GEMV config of the qkv projection when the fused QKV + attention
-    kernel can run it (rows <= 16, head_dim 128, G in 1/2/3/4/8), else None."""
-    from .packing import proj_config
-    if not (1 <= M <= 16) or head_dim != 128 or n_heads % n_kv or n_heads // n_kv not in (1, 2, 3, 4, 8):
-        return None
-    if N != (n_heads + 2 * n_kv) * head_dim:
-        return None
-    algo, cfg = proj_config(N // 16, M, need_even=False, k=K)
-    if algo != "gemv" or tuple(cfg) not in QKV_ATTN_CONFIGS or (K // 32) % cfg[2]:
-        return None
-    return tuple(cfg)
-
-
-def qkv_attn(x: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, eps: float, ep: EpiArgs,
-             attn_out: torch.Tensor, sync: torch.Tensor, err: torch.Tensor, cfg: tuple,
-             scale: Optional[float] = None) -> None:
-    """Fused decode head of a layer (qkv_attn.hip): the qkv GEMV (``wp`` = pack_b(fold_norm(W_qkv,
-    g)), RMSNorm in-kernel) with the RoPE + KV-append epilogue ``ep`` (EPI_QKV), then, in the same
-    launch, the attention of every row over its keys [0, pos] into ``attn_out``. ``cfg`` = (tn,
-    nw, u) from :func:`qkv_attn_config`. ``sync``: >= 2 * n_kv zeroed int32 (left zeroed);
-    ``err``: int32 word set to 1 if a wait timed out (check it: ``StageEngine.check_errors``)."""
-    _check_epi(EPI_QKV, ep, N)
-    _req(_is_bf16_cuda(x, wp, attn_out), "qkv_attn: bf16 cuda tensors required")
-    _req(wp.numel() == N * K and K % 32 == 0, "qkv_attn: packed weight shape")
-    _req(x.dim() == 2 and x.shape[0] >= M and x.shape[1] >= K and x.stride(1) == 1, "qkv_attn: x [rows, >=K]")
-    _req(attn_out.dim() == 2 and attn_out.shape[0] >= M and attn_out.stride(1) == 1, "qkv_attn: attn_out")
-    _req(sync.dtype == torch.int32 and sync.is_cuda and sync.numel() >= 2 * ep.n_kv, "qkv_attn: sync")
-    _req(err.dtype == torch.int32 and err.is_cuda and err.numel() >= 1, "qkv_attn: err")
-    _req(ep.head_dim == 128 and attn_out.shape[1] >= ep.n_heads * 128, "qkv_attn: head_dim 128")
-    _req(tuple(cfg) in QKV_ATTN_CONFIGS, f"qkv_attn: config {cfg} not built")
-    tn, nw, u = cfg
-    sc = ep.head_dim ** -0.5 if scale is None else scale
-    rc = lib().lsa_qkv_attn(_p(x), x.stride(0), _p(wp), M, N, K, float(eps), ctypes.byref(ep), tn, nw, u, float(sc),
-                            _p(attn_out), attn_out.stride(0), _p(sync), _p(err), _stream())
-    _check(rc, "lsa_qkv_attn")
 
 
 def gemv_fp8(x: torch.Tensor, wq: torch.Tensor, wscale: torch.Tensor, M: int, N: int, K: int, epi: int,
@@ -415,9 +374,9 @@ def gemm_wr(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int,
             grid: int = 0) -> None:
     """Projection GEMM with the weights fetched straight into MFMA B registers (gemm_wr.hip):
     128 x ``bn`` tiles, one per workgroup per round, A staged by LDS-DMA, EPI_STORE / EPI_QKV
-    (with the fused RMSNorm row scale, ``ep.ss_in``). K % 256 == 0, N % bn == 0."""
+    (with the fused RMSNorm row scale, ``ep.ss_in``). K % 64 == 0, N % bn == 0."""
     _req(_is_bf16_cuda(a, wp), "gemm_wr: bf16 cuda tensors required")
-    _req(wp.numel() == N * K and K % 256 == 0, "gemm_wr: packed weight shape (K % 256 == 0)")
+    _req(wp.numel() == N * K and K % 64 == 0, "gemm_wr: packed weight shape (K % 64 == 0)")
     _req(a.dim() == 2 and a.shape[0] >= M >= 1 and a.shape[1] >= K and a.stride(1) == 1 and a.stride(0) % 8 == 0
          and a.data_ptr() % 16 == 0, "gemm_wr: A must be [>=M, >=K] row-major with 16-B aligned rows")
     _req(bn in (128, 192, 256) and N % bn == 0, f"gemm_wr: N={N} does not tile by bn={bn}")

@@ -176,21 +176,23 @@ COOP_CONFIGS = [(2, 1, 8, 8, 1), (4, 1, 8, 8, 1), (2, 1, 8, 4, 1), (4, 1, 8, 4, 
                 (2, 1, 4, 4, 1), (4, 1, 4, 4, 1), (2, 1, 4, 8, 1), (8, 1, 4, 2, 1),
                 (2, 1, 4, 8, 2), (4, 1, 4, 4, 2), (4, 1, 4, 8, 2), (4, 1, 8, 4, 2), (4, 2, 4, 4, 2), (8, 1, 4, 2, 2),
                 (8, 1, 4, 4, 2), (4, 1, 4, 4, 4), (4, 1, 2, 4, 2), (4, 1, 2, 4, 1), (2, 1, 2, 4, 2),
-                (8, 1, 2, 2, 2)]
+                (8, 1, 2, 2, 2),
+                (8, 1, 3, 2, 1), (8, 1, 3, 2, 2), (8, 1, 6, 2, 1), (8, 1, 1, 2, 2), (8, 1, 1, 2, 4), (8, 1, 2, 2, 1),
+                (4, 1, 3, 4, 1), (4, 1, 3, 4, 2)]
 GEMV_MAX_ROWS = 128  # rows 65..128 are served by the coop kernel only
 COOP_SPLITS = (1, 2, 4, 8, 16)
 
 
-def coop_candidates(n_tiles: int, k: int, rows: int) -> list:
+def coop_candidates(n_tiles: int, k: int, rows: int, need_even: bool = False) -> list:
     """(tnw, nw, kf, sk, kw) for the cooperative split-K GEMV (rows 17..128): every split
     (and every k-group of a split) keeps at least one K chunk of 32*kf, and kw > 1 needs the
-    chunks to divide evenly over sk*kw."""
+    chunks to divide evenly over sk*kw. need_even (SwiGLU): an even tile count per workgroup."""
     if rows <= 16:
         return []
     mb = row_blocks(rows)
     out = []
     for (b, tnw, nw, kf, kw) in COOP_CONFIGS:
-        if b != mb or n_tiles % (tnw * nw) or k % (32 * kf):
+        if b != mb or n_tiles % (tnw * nw) or k % (32 * kf) or (need_even and (tnw * nw) % 2):
             continue
         nch = k // (32 * kf)
         for sk in COOP_SPLITS:
@@ -282,11 +284,11 @@ def proj_config(n_tiles: int, rows: int, need_even: bool = False, k: int = 4096)
     t = _tuned().get((n_tiles * 16, k, row_blocks(rows), bool(need_even)))
     if t is not None:
         algo, cfg = t
-        if (algo == "coop" and cfg in coop_candidates(n_tiles, k, rows)) or \
+        if (algo == "coop" and cfg in coop_candidates(n_tiles, k, rows, need_even)) or \
            (algo == "gemv" and cfg in gemv_candidates(n_tiles, k, rows, need_even)):
             return t
     if rows > 16:
-        allc = coop_candidates(n_tiles, k, rows)
+        allc = coop_candidates(n_tiles, k, rows, need_even)
         cands = []
         for pref in ((1, 8, 8), (1, 8, 4), (1, 8, 2)):
             cands = [c for c in allc if c[:3] == pref and c[4] == 1]

@@ -349,8 +349,6 @@ class StageEngine:
             self.part_lse = torch.zeros(ws_rows * cfg.num_attention_heads, dtype=torch.float32, device=dev)
             # per-(row, kv-head) arrival tickets of the in-kernel split-KV merge (self-resetting)
             self.attn_cnt = torch.zeros(ws_rows * cfg.num_key_value_heads, dtype=torch.int32, device=dev)
-            # sticky error word of the fused QKV + attention kernel (a timed-out wait)
-            self.qa_err = torch.zeros(1, dtype=torch.int32, device=dev)
             self.ws_rows = ws_rows
             self.keys = torch.zeros(R, dtype=torch.int64, device=dev)
             self.tokens = torch.zeros(R, dtype=torch.int32, device=dev)
@@ -701,16 +699,11 @@ class StageEngine:
         ss = self.ss_buf[:rows] if fuse else None
         ss_valid = False  # ss holds the partials of hbuf's current values
         pending = 0  # down-projection partials not yet added to hbuf
-        # small decode batches: qkv GEMV + attention in one launch (qkv_attn.hip)
-        qa = self._qkv_attn_plan(rows, kv_len, tiles, native_fp8)
         for li, lw in enumerate(self.layers):
             kc, vc = self.k_cache[li], self.v_cache[li]
             ep_qkv = hip.make_epi(out=q, k_cache=kc, v_cache=vc, slot=slot, pos=pos, cos=self.cos, sin=self.sin,
                                   ldo=q.stride(0), n_heads=nh, n_kv=nkv, head_dim=hd, t_max=self.max_seq)
-            if qa is not None and lw.qkv_s is None:
-                hip.qkv_attn(hbuf, lw.qkv, rows, cfg.qkv_size, H, eps, ep_qkv, attn_o,
-                             self.attn_cnt[-2 * nkv:], self.qa_err, qa)
-            elif not proj_gemm:
+            if not proj_gemm:
                 dec(hbuf, lw.qkv, lw.qkv_s, cfg.qkv_size, H, hip.EPI_QKV, ep_qkv, norm=True)
             else:
                 if pending and not fuse:
@@ -735,7 +728,7 @@ class StageEngine:
                     pre(xn, lw.qkv, lw.qkv_s, cfg.qkv_size, H, hip.EPI_QKV, ep_qkv)
             if tiles is not None:
                 hip.attn_prefill(q, kc, vc, tiles[1], nh, nkv, hd, attn_o, causal=kv_len is None, tiles_host=tiles[0])
-            elif qa is None or lw.qkv_s is not None:
+            else:
                 hip.attn(q, kc, vc, slot, pos, rows, nh, nkv, hd, nsplit, self.part_o, self.part_lse, attn_o,
                          kv_len=kv_len, counters=self.attn_cnt, min_chunk=self.ATTN_MIN_CHUNK)
             ep_o = hip.make_epi(out=hbuf, resid=hbuf, ldo=hbuf.stride(0), ldr=hbuf.stride(0))
@@ -762,30 +755,6 @@ class StageEngine:
         if pending:  # the stage's output residual stream
             hip.resid_rmsnorm_partials(hbuf, self.part_k, pending, rows, eps)
         return hbuf
-
-    # fused QKV + attention (qkv_attn.hip) for decode batches of <= 16 rows while the whole key
-    # range is short enough for one workgroup per (row, kv head): longer caches keep the
-    # split-KV attention launch (profiles/r3_attn_small_batch_nsplit.jsonl: at 2,048 keys one
-    # workgroup is 3x slower than 8 splits). LSA_QKV_ATTN=0 turns it off (A/B runs).
-    QKV_ATTN_MAX_SEQ = 1024
-    QKV_ATTN = os.environ.get("LSA_QKV_ATTN", "1") != "0"
-
-    def _qkv_attn_plan(self, rows: int, kv_len, tiles, native_fp8: bool):
-        from ..ops import hip
-        cfg = self.cfg
-        if (not self.QKV_ATTN or not self.gpu or native_fp8 or cfg.is_gpt2 or kv_len is not None or tiles is not None
-                or self.max_seq > self.QKV_ATTN_MAX_SEQ or rows > min(16, self.GEMV_MAX_ROWS)):
-            return None
-        return hip.qkv_attn_config(rows, cfg.qkv_size, cfg.hidden_size, cfg.num_attention_heads,
-                                   cfg.num_key_value_heads, cfg.head_dim)
-
-    def check_errors(self) -> None:
-        """Raise if a fused QKV + attention launch timed out waiting for its producers (its
-        outputs were then invalid); clears the word."""
-        err = getattr(self, "qa_err", None)
-        if err is not None and int(err.item()) != 0:
-            err.zero_()
-            raise RuntimeError("qkv_attn: a consumer workgroup timed out waiting for its q/k/v producers")
 
     def _forward_hip_gpt2(self, hbuf, slot, pos, kv_len, rows, nsplit, tiles, decode, native_fp8) -> torch.Tensor:
         """GPT-2 layer on the HIP path: LayerNorm kernel (ln_1, with the wpe add fused in front

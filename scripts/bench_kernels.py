@@ -93,7 +93,7 @@ def gemv_sweep(out_rows, models, rows_list, tune_entries, fp8=False):
                 for tn, nw, u in packing.gemv_candidates(N // 16, K, M, even):
                     us = timeit(lambda i: hip.gemv(x, ws[i % nbuf], M, N, K, epi, ep, norm=norm, tn=tn, nw=nw, u=u))
                     res.append((us, "gemv", (tn, nw, u), N * K * 2 / us / 1e6))
-                for cfg in packing.coop_candidates(N // 16, K, M):
+                for cfg in packing.coop_candidates(N // 16, K, M, even):
                     us = timeit(lambda i: hip.gemv(x, ws[i % nbuf], M, N, K, epi, ep, norm=norm, coop=cfg, ws=cws))
                     res.append((us, "coop", cfg, N * K * 2 / us / 1e6))
                 if fp8:

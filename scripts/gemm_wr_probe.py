@@ -39,7 +39,7 @@ def main():
         ref = (x.float() @ ws[0].float().T)
         res = {"M": M, "N": N, "K": K}
         only = os.environ.get("WR_ONLY")  # "bn,grid": one configuration (profiling)
-        cfgs = [tuple(int(v) for v in only.split(","))] if only else [(bn, g) for bn in (128, 192, 256) for g in (256, 512)]
+        cfgs = [tuple(int(v) for v in only.split(","))] if only else [(bn, 256) for bn in (128, 192, 256)]
         for bn, grid in cfgs:
             if N % bn:
                 continue
@@ -52,7 +52,12 @@ def main():
             torch.cuda.synchronize()
             err = ((out.float() - ref).norm() / ref.norm()).item()
             us = timeit(run)
-            res[f"bn{bn}_g{grid}"] = [round(us, 2), round(2 * M * N * K / us / 1e6, 1), f"{err:.1e}"]
+            res[f"bn{bn}"] = [round(us, 2), round(2 * M * N * K / us / 1e6, 1), f"{err:.1e}"]
+        if not only:  # gemm_sk's plan for the shape, same cold-weight ring
+            out = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+            eps_ = hip.make_epi(out=out, ldo=N)
+            ws_sk = hip.SkWorkspace("cuda")
+            res["gemm_sk"] = round(timeit(lambda r=0: hip.gemm_sk(x, wps[r % nbuf], M, N, K, hip.EPI_STORE, eps_, ws=ws_sk)), 2)
         print(json.dumps(res), flush=True)
         del ws, wps
         torch.cuda.empty_cache()

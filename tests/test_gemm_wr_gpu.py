@@ -27,10 +27,11 @@ def _rnd(*shape, scale=1.0):
 
 
 @pytest.mark.parametrize("M,N,K", [(512, 12288, 4096), (300, 1536, 512), (1, 768, 256), (777, 1024, 1024),
-                                   (129, 3072, 2816)])
+                                   (129, 3072, 2816), (200, 768, 320), (64, 384, 64)])
 @pytest.mark.parametrize("bn", [128, 192, 256])
 @pytest.mark.parametrize("grid", [256, 37])
 def test_gemm_wr_store(M, N, K, bn, grid):
+    """K = 320 / 64 / 2816 leave a partial last group of K-steps (the ring holds 4)."""
     h = hip()
     if N % bn:
         pytest.skip("N not a multiple of bn")
