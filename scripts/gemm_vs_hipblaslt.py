@@ -6,7 +6,7 @@ plain-store epilogue) against torch.matmul
 stream from HBM (beyond the 256 MB Infinity Cache) as in a decode step; both timed as
 20 launches captured in one hipGraph (no host overhead).
 
-usage: gemm_vs_hipblaslt.py [M,M,...]   (default 384,512,768,2048,16384)
+usage: gemm_vs_hipblaslt.py [M,M,...] [model]   (default 384,512,768,2048,16384 llama2-7b)
 One JSON line per (shape, M)."""
 import json
 import os
@@ -22,7 +22,8 @@ from scripts.bench_kernels import MODEL_SHAPES, timeit  # noqa: E402
 def main():
     rows = [int(r) for r in sys.argv[1].split(",")] if len(sys.argv) > 1 else [384, 512, 768, 2048, 16384]
     sk_ws = hip.SkWorkspace("cuda")
-    for name, (N, K) in MODEL_SHAPES["llama2-7b"].items():
+    model = sys.argv[2] if len(sys.argv) > 2 else "llama2-7b"
+    for name, (N, K) in MODEL_SHAPES[model].items():
         if name == "lm_head":
             continue
         nbuf = max(2, (600 << 20) // (N * K * 2) + 1)

@@ -7,9 +7,12 @@ export TMPDIR=/tmp
 out=gpurun_out/r4_coop
 mkdir -p $out
 rm -f $out/*
-timeout -k 10 600 python -u -m pytest tests/test_kernels_gpu.py tests/test_gemm_wr_gpu.py -x -q --timeout 120 --timeout-method thread \
-    > $out/pytest.log 2>&1 || { tail -30 $out/pytest.log; exit 2; }
-tail -1 $out/pytest.log
+timeout -k 10 120 python3 scripts/probes/gemv_rows_diag.py > $out/diag.jsonl 2> $out/diag.err || { tail -20 $out/diag.err; exit 1; }
+cat $out/diag.jsonl
+timeout -k 10 600 python -u -m pytest tests/test_kernels_gpu.py tests/test_gemm_wr_gpu.py -q --timeout 120 --timeout-method thread \
+    > $out/pytest.log 2>&1; rc=$?
+tail -8 $out/pytest.log
+grep -q "Timeout\|Fatal\|core dumped" $out/pytest.log && exit 2
 timeout -k 10 200 python3 bench.py --batch 128 --steps 32 --warmup 8 --latency-steps 0 --mid-batch 0 > $out/mid_old.log 2>&1 || { tail -20 $out/mid_old.log; exit 3; }
 echo "old $(grep '^\[bench\] load' $out/mid_old.log)"
 timeout -k 10 600 python3 scripts/bench_kernels.py --only gemv --models llama2-7b --rows 128,64,32 --tune \

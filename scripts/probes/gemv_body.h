@@ -1,6 +1,9 @@
 // Body of the decode projection kernel (gemv.hip): y[M, N] = A[M, K] @ W^T, M <= 64, one
-// workgroup per TN 16-column tiles (``block``), fused RMSNorm + epilogues. Shared by
-// gemv_packed_kernel (gemv.hip) and the fused QKV + attention probe (scripts/probes/qkv_attn.hip).
+// workgroup per TN 16-column tiles (``block``), fused RMSNorm + epilogues. Used by
+// the fused QKV + attention probe (scripts/probes/qkv_attn.hip): a copy of gemv_packed_kernel's body
+// (csrc/kernels/gemv.hip) as a device function. The library keeps its own kernel: built through
+// this shared body, the (tn 2, 64 rows, 8 waves) configuration computed wrong rows
+// nondeterministically (profiles/r4_gemv_body_regression.md).
 //
 // Design (MI355X-first, not a translation of the reference's per-op nn.Linear calls in
 // /root/reference/utils/shard_loader.py:67-73 / node_worker.py:262):
