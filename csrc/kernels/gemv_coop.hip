@@ -16,6 +16,13 @@
 //    is reset by the last arriver, so the kernel is replay-safe inside hipGraphs.
 #include "epilogue.h"
 
+#include <utility>
+
+// Register ring depth of the main loop (chunks in flight + 1); a diagnostic build may override it.
+#ifndef COOP_DEPTH
+#define COOP_DEPTH 3
+#endif
+
 // Timing-only builds (scripts/coop_phases.py; outputs garbage): 1 = exit after the main loop,
 // 2 = exit after the k-group / split reduction (no epilogue), 3 = epilogue without its global
 // stores, 4 = epilogue stores of constants (no LDS reads, no math).
@@ -40,6 +47,12 @@ __device__ unsigned long long* g_coop_stamps;
 #endif
 
 namespace {
+
+// f(integral_constant<S>) for S = 0, 1, ... while f returns true
+template <int... S, typename F>
+LSA_DEVICE bool coop_static_all(std::integer_sequence<int, S...>, F&& f) {
+  return (f(std::integral_constant<int, S>{}) && ...);
+}
 
 // A tile [MR][KC] bf16 in LDS, 16-B chunks XOR-swizzled so that the 16 lanes of one
 // ds_read_b128 pass (16 consecutive rows, same logical chunk) hit all 64 banks: rows of >= 16
@@ -219,40 +232,41 @@ __global__ __launch_bounds__(NW * KW * 64) void gemv_coop_kernel(
   };
 
   {
-    // Prefetch distance 2 chunks for both operands through 3-deep register rings: B (HBM
-    // weights) is consumed straight from registers, A (L2-resident activations) is written
-    // to one of 2 LDS buffers one chunk before use. vmcnt is in-order, so A(c+1) must be
-    // issued before B(c+1) - otherwise waiting for A would drain the B prefetch too. Loads
-    // are unconditional (tail chunk indices clamped, duplicates hit L2) so every s_waitcnt
-    // is a static count, never vmcnt(0).
-    u32x4_t bX[BL][TNW], bY[BL][TNW], bZ[BL][TNW];
-    AV aX, aY, aZ;
+    // B (HBM weights) is consumed straight from registers, A (L2-resident activations) is
+    // written to one of 2 LDS buffers one chunk before use. Loads are unconditional (tail
+    // chunk indices clamped, duplicates hit L2) so every s_waitcnt is a static count, never
+    // vmcnt(0).
+    // D-deep register rings for both operands (prefetch distance D-1 chunks): A and W of one
+    // chunk are issued together, so the counted wait for A(c+1) never drains a W prefetch
+    // issued after it.
+    constexpr int D = COOP_DEPTH;
+    u32x4_t bw[D][BL][TNW];
+    AV aw[D];
     const int last = nchunk - 1;
     auto clampc = [&](int c) { return c < last ? c : last; };
-    aX = load_a(0);
-    load_b(0, bX);
-    aY = load_a(clampc(1));
-    load_b(clampc(1), bY);
-    store_a(0, aX, 1.f);
+    coop_static_all(std::make_integer_sequence<int, D - 1>{}, [&](auto sc) {
+      constexpr int S = decltype(sc)::value;
+      aw[S] = load_a(clampc(S));
+      load_b(clampc(S), bw[S]);
+      return true;
+    });
+    store_a(0, aw[0], 1.f);
     __syncthreads();
-    // step c: prefetch chunk c+2 into (a2, b2), compute chunk c from (LDS c&1, bc), then
-    // publish A(c+1) from a1 into LDS.
-    auto step = [&](int c, u32x4_t (&bc)[BL][TNW], u32x4_t (&b2)[BL][TNW], AV& a1, AV& a2) {
-      a2 = load_a(clampc(c + 2));
-      load_b(clampc(c + 2), b2);
-      __builtin_amdgcn_sched_barrier(0);  // keep the prefetches ahead of this chunk's MFMAs
-      compute(c & 1, bc);
-      __builtin_amdgcn_sched_barrier(0);
-      store_a((c + 1) & 1, a1, c < last ? 1.f : 0.f);
-      __syncthreads();
-    };
+    // step c (ring slot S = c % D): prefetch chunk c+D-1 into slot (c-1) % D, compute chunk c
+    // from (LDS c&1, W slot S), then publish A(c+1) into LDS.
     for (int c = 0;;) {
-      step(c, bX, bZ, aY, aZ);
-      if (++c > last) break;
-      step(c, bY, bX, aZ, aX);
-      if (++c > last) break;
-      step(c, bZ, bY, aX, aY);
-      if (++c > last) break;
+      const bool more = coop_static_all(std::make_integer_sequence<int, D>{}, [&](auto sc) {
+        constexpr int S = decltype(sc)::value, SN = (S + D - 1) % D, S1 = (S + 1) % D;
+        aw[SN] = load_a(clampc(c + D - 1));
+        load_b(clampc(c + D - 1), bw[SN]);
+        __builtin_amdgcn_sched_barrier(0);  // keep the prefetches ahead of this chunk's MFMAs
+        compute(c & 1, bw[S]);
+        __builtin_amdgcn_sched_barrier(0);
+        store_a((c + 1) & 1, aw[S1], c < last ? 1.f : 0.f);
+        __syncthreads();
+        return ++c <= last;
+      });
+      if (!more) break;
     }
   }
 
