@@ -18,11 +18,6 @@
 
 #include <utility>
 
-// Register ring depth of the main loop (chunks in flight + 1); a diagnostic build may override it.
-#ifndef COOP_DEPTH
-#define COOP_DEPTH 3
-#endif
-
 // Timing-only builds (scripts/coop_phases.py; outputs garbage): 1 = exit after the main loop,
 // 2 = exit after the k-group / split reduction (no epilogue), 3 = epilogue without its global
 // stores, 4 = epilogue stores of constants (no LDS reads, no math).
@@ -81,7 +76,8 @@ LSA_DEVICE u32x4_t fp8x8_to_bf16(unsigned lo, unsigned hi) {
 // side by side in LDS), and the groups' fp32 partials are summed through LDS before the
 // epilogue. More waves (bytes in flight) per workgroup at the same column grouping: the
 // decode projections have too few 16-column tiles to give every CU a workgroup of 8+ waves.
-template <int MB, int TNW, int NW, int KF, int KW, int EPI, bool NORM, bool FP8>
+// D: register-ring depth of the main loop (prefetch distance D-1 chunks for both operands).
+template <int MB, int TNW, int NW, int KF, int KW, int D, int EPI, bool NORM, bool FP8>
 __global__ __launch_bounds__(NW * KW * 64) void gemv_coop_kernel(
     const bf16_raw* __restrict__ x, int ldx, const int* __restrict__ a_rows, const bf16_raw* __restrict__ wp,
     int M, int N, int K, int SK, float eps, EpiArgs ep, float* __restrict__ slab, unsigned* __restrict__ counters,
@@ -239,7 +235,6 @@ __global__ __launch_bounds__(NW * KW * 64) void gemv_coop_kernel(
     // D-deep register rings for both operands (prefetch distance D-1 chunks): A and W of one
     // chunk are issued together, so the counted wait for A(c+1) never drains a W prefetch
     // issued after it.
-    constexpr int D = COOP_DEPTH;
     u32x4_t bw[D][BL][TNW];
     AV aw[D];
     const int last = nchunk - 1;
@@ -494,40 +489,46 @@ __global__ __launch_bounds__(NW * KW * 64) void gemv_coop_kernel(
   LSA_CSTAMP(8);
 }
 
-template <int MB, int TNW, int NW, int KF, int KW, int EPI, bool FP8>
+template <int MB, int TNW, int NW, int KF, int KW, int D, int EPI, bool FP8>
 int launch(bool norm, const bf16_raw* x, int ldx, const int* a_rows, const bf16_raw* wp, int M, int N, int K, int SK, float eps,
            const EpiArgs& ep, float* slab, unsigned* cnt, const float* wscale, hipStream_t s) {
   const int G = N / 16 / (NW * TNW);
   dim3 grid(G * SK), block(NW * KW * 64);
   if (norm)
-    gemv_coop_kernel<MB, TNW, NW, KF, KW, EPI, true, FP8><<<grid, block, 0, s>>>(x, ldx, a_rows, wp, M, N, K, SK, eps, ep, slab, cnt, wscale);
+    gemv_coop_kernel<MB, TNW, NW, KF, KW, D, EPI, true, FP8><<<grid, block, 0, s>>>(x, ldx, a_rows, wp, M, N, K, SK, eps, ep, slab, cnt, wscale);
   else
-    gemv_coop_kernel<MB, TNW, NW, KF, KW, EPI, false, FP8><<<grid, block, 0, s>>>(x, ldx, a_rows, wp, M, N, K, SK, eps, ep, slab, cnt, wscale);
+    gemv_coop_kernel<MB, TNW, NW, KF, KW, D, EPI, false, FP8><<<grid, block, 0, s>>>(x, ldx, a_rows, wp, M, N, K, SK, eps, ep, slab, cnt, wscale);
   LSA_CHECK_LAUNCH();
   return LSA_OK;
 }
 
-// (mb, tnw, nw, kf, kw). nw = 3 / 6: one workgroup per CU for 768-tile projections (Llama-2-7B
-// qkv) with no split at all; nw = 1: one tile per workgroup (4096-column projections).
+// (mb, tnw, nw, kf, kw, d). nw = 3 / 6: one workgroup per CU for 768-tile projections (Llama-2-7B
+// qkv) with no split at all; nw = 1: one tile per workgroup (4096-column projections). d = 4
+// (a deeper ring) where it measured faster: the long unsplit K ranges of gate_up / lm_head and
+// 32-row qkv / down (profiles/r4_coop_depth_probe.jsonl); d = 3 everywhere else (deeper rings
+// slowed the split configs).
 #define LSA_COOP_CONFIGS(X) \
-  X(2, 1, 8, 8, 1) X(4, 1, 8, 8, 1) X(2, 1, 8, 4, 1) X(4, 1, 8, 4, 1) X(2, 2, 8, 4, 1) X(4, 2, 8, 4, 1) X(2, 2, 4, 4, 1) \
-  X(4, 2, 4, 4, 1) X(8, 1, 8, 4, 1) X(8, 1, 8, 2, 1) X(8, 2, 4, 2, 1) X(2, 1, 4, 4, 1) X(4, 1, 4, 4, 1) X(2, 1, 4, 8, 1) \
-  X(8, 1, 4, 2, 1) \
-  X(2, 1, 4, 8, 2) X(4, 1, 4, 4, 2) X(4, 1, 4, 8, 2) X(4, 1, 8, 4, 2) X(4, 2, 4, 4, 2) X(8, 1, 4, 2, 2) X(8, 1, 4, 4, 2) \
-  X(4, 1, 4, 4, 4) X(4, 1, 2, 4, 2) X(4, 1, 2, 4, 1) X(2, 1, 2, 4, 2) X(8, 1, 2, 2, 2) \
-  X(8, 1, 3, 2, 1) X(8, 1, 3, 2, 2) X(8, 1, 6, 2, 1) X(8, 1, 1, 2, 2) X(8, 1, 1, 2, 4) X(8, 1, 2, 2, 1) \
-  X(4, 1, 3, 4, 1) X(4, 1, 3, 4, 2)
+  X(2, 1, 8, 8, 1, 3) X(4, 1, 8, 8, 1, 3) X(2, 1, 8, 4, 1, 3) X(4, 1, 8, 4, 1, 3) X(2, 2, 8, 4, 1, 3) X(4, 2, 8, 4, 1, 3) \
+  X(2, 2, 4, 4, 1, 3) X(4, 2, 4, 4, 1, 3) X(8, 1, 8, 4, 1, 3) X(8, 1, 8, 2, 1, 3) X(8, 2, 4, 2, 1, 3) X(2, 1, 4, 4, 1, 3) \
+  X(4, 1, 4, 4, 1, 3) X(2, 1, 4, 8, 1, 3) X(8, 1, 4, 2, 1, 3) \
+  X(2, 1, 4, 8, 2, 3) X(4, 1, 4, 4, 2, 3) X(4, 1, 4, 8, 2, 3) X(4, 1, 8, 4, 2, 3) X(4, 2, 4, 4, 2, 3) X(8, 1, 4, 2, 2, 3) \
+  X(8, 1, 4, 4, 2, 3) X(4, 1, 4, 4, 4, 3) X(4, 1, 2, 4, 2, 3) X(4, 1, 2, 4, 1, 3) X(2, 1, 2, 4, 2, 3) X(8, 1, 2, 2, 2, 3) \
+  X(8, 1, 3, 2, 1, 3) X(8, 1, 3, 2, 2, 3) X(8, 1, 6, 2, 1, 3) X(8, 1, 1, 2, 2, 3) X(8, 1, 1, 2, 4, 3) X(8, 1, 2, 2, 1, 3) \
+  X(4, 1, 3, 4, 1, 3) X(4, 1, 3, 4, 2, 3) \
+  X(8, 1, 8, 2, 1, 4) X(8, 1, 8, 4, 1, 4) X(4, 1, 8, 4, 1, 4) X(2, 1, 8, 4, 1, 4) X(2, 1, 4, 4, 1, 4)
 
-// fp8-weight instantiations (subset; KF even so one 16-B load carries two k-fragments)
+// fp8-weight instantiations (subset; KF even so one 16-B load carries two k-fragments; d = 3)
 #define LSA_COOP_FP8_CONFIGS(X) \
-  X(2, 1, 8, 4, 1) X(4, 1, 8, 4, 1) X(2, 1, 4, 4, 1) X(4, 1, 4, 4, 1) X(8, 1, 8, 4, 1) X(8, 1, 4, 2, 1) X(2, 1, 8, 8, 1) \
-  X(4, 1, 8, 8, 1)
+  X(2, 1, 8, 4, 1, 3) X(4, 1, 8, 4, 1, 3) X(2, 1, 4, 4, 1, 3) X(4, 1, 4, 4, 1, 3) X(8, 1, 8, 4, 1, 3) X(8, 1, 4, 2, 1, 3) \
+  X(2, 1, 8, 8, 1, 3) X(4, 1, 8, 8, 1, 3)
 
 template <int EPI, bool FP8>
-int dispatch(int mb, int tnw, int nw, int kf, int kw, bool norm, const bf16_raw* x, int ldx, const int* a_rows, const bf16_raw* wp, int M, int N,
-             int K, int SK, float eps, const EpiArgs& ep, float* slab, unsigned* cnt, const float* wscale, hipStream_t s) {
-#define LSA_C(B, T, W, F, Q) \
-  if (mb == B && tnw == T && nw == W && kf == F && kw == Q) return launch<B, T, W, F, Q, EPI, FP8>(norm, x, ldx, a_rows, wp, M, N, K, SK, eps, ep, slab, cnt, wscale, s);
+int dispatch(int mb, int tnw, int nw, int kf, int kw, int d, bool norm, const bf16_raw* x, int ldx, const int* a_rows,
+             const bf16_raw* wp, int M, int N, int K, int SK, float eps, const EpiArgs& ep, float* slab, unsigned* cnt,
+             const float* wscale, hipStream_t s) {
+#define LSA_C(B, T, W, F, Q, DD)                                                                              \
+  if (mb == B && tnw == T && nw == W && kf == F && kw == Q && d == DD)                                          \
+    return launch<B, T, W, F, Q, DD, EPI, FP8>(norm, x, ldx, a_rows, wp, M, N, K, SK, eps, ep, slab, cnt, wscale, s);
   if constexpr (FP8) {
     LSA_COOP_FP8_CONFIGS(LSA_C)
   } else {
@@ -537,15 +538,13 @@ int dispatch(int mb, int tnw, int nw, int kf, int kw, bool norm, const bf16_raw*
   return LSA_UNSUPPORTED;
 }
 
-
-
 // K is split into 32*kf-k chunks, spread over the SK splits as evenly as possible.
 // Workspace: slab >= SK*N*16*MB*4 + SK*(N/16/(nw*tnw))*16*MB*4 bytes (only when SK > 1);
 // counters: N/16/(nw*tnw) zero-initialised uint32 (reset by the kernel itself).
 template <bool FP8>
 int coop_entry(const void* x, int ldx, const int* a_rows, const void* wp, int M, int N, int K, int norm, float eps,
-               int epi, const EpiArgs* ep, int tnw, int nw, int kf, int sk, int kw, float* slab, unsigned* counters,
-               const float* wscale, hipStream_t stream) {
+               int epi, const EpiArgs* ep, int tnw, int nw, int kf, int sk, int kw, int d, float* slab,
+               unsigned* counters, const float* wscale, hipStream_t stream) {
   if (M < 1 || M > 128 || kf < 1 || K % (32 * kf) || ldx < K || sk < 1 || kw < 1) return LSA_BAD_SHAPE;
   if (kw > 1 && (K / (32 * kf)) % (sk * kw)) return LSA_BAD_SHAPE;  // every k-group: same chunk count
   if (FP8 && (kf % 2 || !wscale)) return LSA_BAD_SHAPE;
@@ -557,7 +556,7 @@ int coop_entry(const void* x, int ldx, const int* a_rows, const void* wp, int M,
   const bf16_raw* xx = static_cast<const bf16_raw*>(x);
   const bf16_raw* w = static_cast<const bf16_raw*>(wp);
   const bool n = norm != 0;
-#define LSA_D(E) dispatch<E, FP8>(mb, tnw, nw, kf, kw, n, xx, ldx, a_rows, w, M, N, K, sk, eps, *ep, slab, counters, wscale, stream)
+#define LSA_D(E) dispatch<E, FP8>(mb, tnw, nw, kf, kw, d, n, xx, ldx, a_rows, w, M, N, K, sk, eps, *ep, slab, counters, wscale, stream)
   switch (epi) {
     case EPI_STORE: return LSA_D(EPI_STORE);
     case EPI_RESID: return LSA_D(EPI_RESID);
@@ -575,14 +574,14 @@ int coop_entry(const void* x, int ldx, const int* a_rows, const void* wp, int M,
 // K is split into 32*kf-k chunks, spread over the SK splits as evenly as possible; each split
 // over kw k-groups of nw waves (kw > 1: (K/(32*kf)) % (sk*kw) == 0). EPI_PARTIAL: no in-kernel
 // split reduction - split s stores its fp32 tile to ((float*)ep->out)[s][M][ldo] for
-// lsa_resid_rmsnorm_partials.
+// lsa_resid_rmsnorm_partials. depth: register-ring depth of an instantiated config (3 or 4).
 // Workspace: slab >= SK*N*16*MB*4 + SK*(N/16/(nw*tnw))*16*MB*4 bytes (only when SK > 1);
 // counters: N/16/(nw*tnw) zero-initialised uint32 (reset by the kernel itself).
 extern "C" int lsa_gemv_coop(const void* x, int ldx, const int* a_rows, const void* wp, int M, int N, int K, int norm, float eps,
-                             int epi, const EpiArgs* ep, int tnw, int nw, int kf, int sk, int kw, float* slab,
+                             int epi, const EpiArgs* ep, int tnw, int nw, int kf, int sk, int kw, int depth, float* slab,
                              unsigned* counters, hipStream_t stream) {
-  return coop_entry<false>(x, ldx, a_rows, wp, M, N, K, norm, eps, epi, ep, tnw, nw, kf, sk, kw, slab, counters, nullptr,
-                           stream);
+  return coop_entry<false>(x, ldx, a_rows, wp, M, N, K, norm, eps, epi, ep, tnw, nw, kf, sk, kw, depth, slab, counters,
+                           nullptr, stream);
 }
 
 #ifdef LSA_COOP_STAMPS
@@ -595,6 +594,6 @@ extern "C" int lsa_coop_set_stamps(unsigned long long* buf) {
 extern "C" int lsa_gemv_coop_fp8(const void* x, int ldx, const int* a_rows, const void* wq, const float* wscale, int M,
                                  int N, int K, int norm, float eps, int epi, const EpiArgs* ep, int tnw, int nw, int kf,
                                  int sk, float* slab, unsigned* counters, hipStream_t stream) {
-  return coop_entry<true>(x, ldx, a_rows, wq, M, N, K, norm, eps, epi, ep, tnw, nw, kf, sk, 1, slab, counters, wscale,
-                          stream);
+  return coop_entry<true>(x, ldx, a_rows, wq, M, N, K, norm, eps, epi, ep, tnw, nw, kf, sk, 1, 3, slab, counters,
+                          wscale, stream);
 }

@@ -58,7 +58,7 @@ def lib() -> ctypes.CDLL:
     L = ctypes.CDLL(KERNELS_SO, mode=ctypes.RTLD_GLOBAL)
     vp, i, f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
     L.lsa_gemv.argtypes = [vp, i, vp, vp, i, i, i, i, f, i, ctypes.POINTER(EpiArgs), i, i, i, vp]
-    L.lsa_gemv_coop.argtypes = [vp, i, vp, vp, i, i, i, i, f, i, ctypes.POINTER(EpiArgs), i, i, i, i, i, vp, vp, vp]
+    L.lsa_gemv_coop.argtypes = [vp, i, vp, vp, i, i, i, i, f, i, ctypes.POINTER(EpiArgs), i, i, i, i, i, i, vp, vp, vp]
     L.lsa_gemv_fp8.argtypes = [vp, i, vp, vp, vp, i, i, i, i, f, i, ctypes.POINTER(EpiArgs), i, i, i, vp]
     L.lsa_dequant_fp8_packed.argtypes = [vp, vp, vp, i, i, vp]
     L.lsa_gemv_coop_fp8.argtypes = [vp, i, vp, vp, vp, i, i, i, i, f, i, ctypes.POINTER(EpiArgs), i, i, i, i, vp, vp, vp]
@@ -176,11 +176,11 @@ def gemv(x: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep
     when ``norm``: RMSNorm of the A rows is then applied in-kernel), W: [N, K].
 
     Kernel choice: explicit ``tn/nw/u`` -> streaming GEMV (gemv.hip); explicit
-    ``coop=(tnw, nw, kf, sk[, kw])`` -> cooperative split-K (gemv_coop.hip); neither -> the tuned
+    ``coop=(tnw, nw, kf, sk[, kw[, d]])`` -> cooperative split-K (gemv_coop.hip); neither -> the tuned
     choice of :func:`packing.proj_config`. EPI_PARTIAL (coop only): split s writes its fp32 tile
     to ``ep.out`` viewed as [sk][M][ldo] (``out_numel`` = its capacity in floats, checked) for
     :func:`resid_rmsnorm_partials`."""
-    from .packing import GEMV_CONFIGS, coop_candidates, coop_slab_floats, proj_config, row_blocks
+    from .packing import GEMV_CONFIGS, coop_candidates, coop_norm, coop_slab_floats, proj_config, row_blocks
     _req(1 <= M <= 128, f"gemv supports 1..128 rows, got {M}")
     _check_epi(epi, ep, N)
     _req(_is_bf16_cuda(x, wp), "gemv: bf16 cuda tensors required")
@@ -198,8 +198,8 @@ def gemv(x: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep
             tn, nw, u = cfg
     _req(epi != EPI_PARTIAL or coop is not None, "gemv: EPI_PARTIAL needs an explicit coop config")
     if coop is not None:
-        coop = tuple(coop) if len(coop) == 5 else tuple(coop) + (1,)
-        tnw, cnw, kf, sk, kw = coop
+        coop = coop_norm(coop)
+        tnw, cnw, kf, sk, kw, depth = coop
         if epi == EPI_PARTIAL:
             _req(out_numel >= sk * M * ep.ldo, f"gemv partial: output holds {out_numel} floats, "
                  f"{sk} splits x {M} rows x ldo {ep.ldo} needed")
@@ -211,7 +211,7 @@ def gemv(x: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep
         _req(ws.slab.numel() >= need, f"gemv: coop workspace too small ({ws.slab.numel()} < {need} floats)")
         _req(ws.counters.numel() >= N // 16 // (tnw * cnw), "gemv: coop workspace counters too small")
         rc = lib().lsa_gemv_coop(_p(x), x.stride(0), _p(a_rows), _p(wp), M, N, K, int(norm), float(eps), epi,
-                                 ctypes.byref(ep), tnw, cnw, kf, sk, kw, _p(ws.slab), _p(ws.counters), _stream())
+                                 ctypes.byref(ep), tnw, cnw, kf, sk, kw, depth, _p(ws.slab), _p(ws.counters), _stream())
         _check(rc, "lsa_gemv_coop")
         return
     mb = row_blocks(M)

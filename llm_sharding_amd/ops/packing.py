@@ -169,29 +169,31 @@ def gemv_candidates(n_tiles: int, k: int, rows: int, need_even: bool = False) ->
             if b == mb and n_tiles % tn == 0 and (not need_even or tn % 2 == 0) and (k // 32) % u == 0]
 
 
-# (mb, tnw, nw, kf, kw) instantiated in csrc/kernels/gemv_coop.hip (LSA_COOP_CONFIGS) - keep in sync.
-# kw = k-groups of nw waves per workgroup (kw * nw waves stream the same nw * tnw tiles).
-COOP_CONFIGS = [(2, 1, 8, 8, 1), (4, 1, 8, 8, 1), (2, 1, 8, 4, 1), (4, 1, 8, 4, 1), (2, 2, 8, 4, 1),
-                (4, 2, 8, 4, 1), (2, 2, 4, 4, 1), (4, 2, 4, 4, 1), (8, 1, 8, 4, 1), (8, 1, 8, 2, 1), (8, 2, 4, 2, 1),
-                (2, 1, 4, 4, 1), (4, 1, 4, 4, 1), (2, 1, 4, 8, 1), (8, 1, 4, 2, 1),
-                (2, 1, 4, 8, 2), (4, 1, 4, 4, 2), (4, 1, 4, 8, 2), (4, 1, 8, 4, 2), (4, 2, 4, 4, 2), (8, 1, 4, 2, 2),
-                (8, 1, 4, 4, 2), (4, 1, 4, 4, 4), (4, 1, 2, 4, 2), (4, 1, 2, 4, 1), (2, 1, 2, 4, 2),
-                (8, 1, 2, 2, 2),
-                (8, 1, 3, 2, 1), (8, 1, 3, 2, 2), (8, 1, 6, 2, 1), (8, 1, 1, 2, 2), (8, 1, 1, 2, 4), (8, 1, 2, 2, 1),
-                (4, 1, 3, 4, 1), (4, 1, 3, 4, 2)]
+# (mb, tnw, nw, kf, kw, d) instantiated in csrc/kernels/gemv_coop.hip (LSA_COOP_CONFIGS) - keep in sync.
+# kw = k-groups of nw waves per workgroup (kw * nw waves stream the same nw * tnw tiles);
+# d = register-ring depth (prefetch distance d - 1 chunks).
+COOP_CONFIGS = [(2, 1, 8, 8, 1, 3), (4, 1, 8, 8, 1, 3), (2, 1, 8, 4, 1, 3), (4, 1, 8, 4, 1, 3), (2, 2, 8, 4, 1, 3),
+                (4, 2, 8, 4, 1, 3), (2, 2, 4, 4, 1, 3), (4, 2, 4, 4, 1, 3), (8, 1, 8, 4, 1, 3), (8, 1, 8, 2, 1, 3),
+                (8, 2, 4, 2, 1, 3), (2, 1, 4, 4, 1, 3), (4, 1, 4, 4, 1, 3), (2, 1, 4, 8, 1, 3), (8, 1, 4, 2, 1, 3),
+                (2, 1, 4, 8, 2, 3), (4, 1, 4, 4, 2, 3), (4, 1, 4, 8, 2, 3), (4, 1, 8, 4, 2, 3), (4, 2, 4, 4, 2, 3),
+                (8, 1, 4, 2, 2, 3), (8, 1, 4, 4, 2, 3), (4, 1, 4, 4, 4, 3), (4, 1, 2, 4, 2, 3), (4, 1, 2, 4, 1, 3),
+                (2, 1, 2, 4, 2, 3), (8, 1, 2, 2, 2, 3),
+                (8, 1, 3, 2, 1, 3), (8, 1, 3, 2, 2, 3), (8, 1, 6, 2, 1, 3), (8, 1, 1, 2, 2, 3), (8, 1, 1, 2, 4, 3),
+                (8, 1, 2, 2, 1, 3), (4, 1, 3, 4, 1, 3), (4, 1, 3, 4, 2, 3),
+                (8, 1, 8, 2, 1, 4), (8, 1, 8, 4, 1, 4), (4, 1, 8, 4, 1, 4), (2, 1, 8, 4, 1, 4), (2, 1, 4, 4, 1, 4)]
 GEMV_MAX_ROWS = 128  # rows 65..128 are served by the coop kernel only
 COOP_SPLITS = (1, 2, 4, 8, 16)
 
 
 def coop_candidates(n_tiles: int, k: int, rows: int, need_even: bool = False) -> list:
-    """(tnw, nw, kf, sk, kw) for the cooperative split-K GEMV (rows 17..128): every split
+    """(tnw, nw, kf, sk, kw, d) for the cooperative split-K GEMV (rows 17..128): every split
     (and every k-group of a split) keeps at least one K chunk of 32*kf, and kw > 1 needs the
     chunks to divide evenly over sk*kw. need_even (SwiGLU): an even tile count per workgroup."""
     if rows <= 16:
         return []
     mb = row_blocks(rows)
     out = []
-    for (b, tnw, nw, kf, kw) in COOP_CONFIGS:
+    for (b, tnw, nw, kf, kw, d) in COOP_CONFIGS:
         if b != mb or n_tiles % (tnw * nw) or k % (32 * kf) or (need_even and (tnw * nw) % 2):
             continue
         nch = k // (32 * kf)
@@ -199,7 +201,7 @@ def coop_candidates(n_tiles: int, k: int, rows: int, need_even: bool = False) ->
             if nch < sk * kw or (kw > 1 and nch % (sk * kw)):
                 continue
             if (n_tiles // (tnw * nw)) * sk <= 4 * N_CU:
-                out.append((tnw, nw, kf, sk, kw))
+                out.append((tnw, nw, kf, sk, kw, d))
     return out
 
 
@@ -220,6 +222,17 @@ def coop_fp8_candidates(n_tiles: int, k: int, rows: int) -> list:
             if k // (32 * kf) >= sk and (n_tiles // (tnw * nw)) * sk <= 4 * N_CU:
                 out.append((tnw, nw, kf, sk))
     return out
+
+
+def coop_norm(cfg) -> tuple:
+    """A coop config as the full (tnw, nw, kf, sk, kw, d) tuple: tables and callers written
+    before k-groups / ring depths existed give 4 or 5 entries (kw = 1, d = 3)."""
+    c = tuple(cfg)
+    if len(c) == 4:
+        c = c + (1,)
+    if len(c) == 5:
+        c = c + (3,)
+    return c
 
 
 def coop_slab_floats(n: int, rows: int, tnw: int, nw: int, kf: int, sk: int, kw: int = 1) -> int:
@@ -256,17 +269,17 @@ def _tuned() -> dict:
                     if e.get("algo") in ("fp8", "coop_fp8"):
                         _TUNED[(e["N"], e["K"], e["mb"], bool(e["even"]), "fp8")] = (e["algo"], tuple(e["cfg"]))
                     elif e.get("algo") == "coop_partial":
-                        _TUNED[(e["N"], e["K"], e["mb"], False, "partial")] = (e["algo"], tuple(e["cfg"]))
+                        _TUNED[(e["N"], e["K"], e["mb"], False, "partial")] = (e["algo"], coop_norm(e["cfg"]))
                     else:
                         cfg = tuple(e["cfg"])
-                        if e.get("algo") == "coop" and len(cfg) == 4:
-                            cfg = cfg + (1,)  # tables written before k-groups existed
+                        if e.get("algo") == "coop":
+                            cfg = coop_norm(cfg)
                         _TUNED[(e["N"], e["K"], e["mb"], bool(e["even"]))] = (e.get("algo", "gemv"), cfg)
     return _TUNED
 
 
 def partial_config(n_tiles: int, rows: int, k: int = 4096) -> Optional[tuple]:
-    """(tnw, nw, kf, sk, kw) when a residual decode projection of ``rows`` rows is measured
+    """(tnw, nw, kf, sk, kw, d) when a residual decode projection of ``rows`` rows is measured
     faster as coop EPI_PARTIAL (splits store fp32 tiles) + lsa_resid_rmsnorm_partials than with
     the in-kernel split reduction + residual epilogue (scripts/tune_coop_partial.py), else None."""
     t = _tuned().get((n_tiles * 16, k, row_blocks(rows), False, "partial"))
@@ -277,7 +290,7 @@ def partial_config(n_tiles: int, rows: int, k: int = 4096) -> Optional[tuple]:
 
 
 def proj_config(n_tiles: int, rows: int, need_even: bool = False, k: int = 4096) -> tuple:
-    """("gemv", (tn, nw, u)) or ("coop", (tnw, nw, kf, sk, kw)) for a decode projection of ``rows``
+    """("gemv", (tn, nw, u)) or ("coop", (tnw, nw, kf, sk, kw, d)) for a decode projection of ``rows``
     rows. The tuning table (measured on MI355X) wins; otherwise rows <= 16 use the
     weight-streaming GEMV and larger row counts the cooperative split-K kernel with the
     smallest split that fills the 256 CUs."""
@@ -291,7 +304,7 @@ def proj_config(n_tiles: int, rows: int, need_even: bool = False, k: int = 4096)
         allc = coop_candidates(n_tiles, k, rows, need_even)
         cands = []
         for pref in ((1, 8, 8), (1, 8, 4), (1, 8, 2)):
-            cands = [c for c in allc if c[:3] == pref and c[4] == 1]
+            cands = [c for c in allc if c[:3] == pref and c[4] == 1 and c[5] == 3]
             if cands:
                 break
         cands = cands or allc

@@ -1,56 +1,26 @@
 #!/usr/bin/env python3
-"""Register-ring depth of the cooperative decode GEMV (csrc/kernels/gemv_coop.hip, COOP_DEPTH):
-the library's depth against diagnostic builds with deeper rings (--build: _native/liblsa_coop_d{D}.so),
-timed on the 7B decode projections at 32 / 64 / 128 rows over the 8 best configs of the last
-re-tune (profiles/r4_decode_proj_sweep.jsonl, copied to coop_depth_cfgs.json). Weights rotate over > 600 MB (HBM-cold), as in a
-decode step. One JSON line per (shape, rows)."""
-import ctypes
+"""Register-ring depth of the cooperative decode GEMV (csrc/kernels/gemv_coop.hip, template D):
+configs instantiated at both d = 3 and d = 4 timed against each other on the 7B decode
+projections at 32 / 64 / 128 rows, over the 8 best configs of the round-4 re-tune
+(profiles/r4_decode_proj_sweep.jsonl, copied to coop_depth_cfgs.json). Weights rotate over
+> 600 MB (HBM-cold), as in a decode step. One JSON line per (shape, rows).
+
+(The d = 4 / 5 / 6 numbers in profiles/r4_coop_depth_probe.jsonl came from an earlier form of this
+probe that rebuilt the whole kernel file at a fixed depth; they picked the d = 4 instantiations.)"""
 import json
 import os
-import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
-DEPTHS = (4, 5, 6)
-
-
-def so(d):
-    return os.path.join(ROOT, "llm_sharding_amd", "_native", f"liblsa_coop_d{d}.so")
-
-
-def build():
-    for d in DEPTHS:
-        subprocess.check_call(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "-shared", "--offload-arch=gfx950",
-                               "-munsafe-fp-atomics", f"-DCOOP_DEPTH={d}", "-I", os.path.join(ROOT, "csrc", "kernels"),
-                               "-o", so(d), os.path.join(ROOT, "csrc", "kernels", "gemv_coop.hip")])
-        print("built", so(d), flush=True)
-
-
-class _Proxy:
-    def __init__(self, real, coop):
-        self._real, self.lsa_gemv_coop = real, coop
-
-    def __getattr__(self, name):
-        return getattr(self._real, name)
 
 
 def main():
-    if sys.argv[1:2] == ["--build"]:
-        build()
-        return
     import torch
     from llm_sharding_amd.ops import hip, packing
     from llm_sharding_amd.models.rope import rope_table
     from llm_sharding_amd.config import llama2_7b
     from scripts.bench_kernels import EPIS, MODEL_SHAPES, timeit
-    real = hip.lib()
-    libs = {3: real}
-    for d in DEPTHS:
-        L = ctypes.CDLL(so(d))
-        L.lsa_gemv_coop.argtypes = real.lsa_gemv_coop.argtypes
-        L.lsa_gemv_coop.restype = ctypes.c_int
-        libs[d] = _Proxy(real, L.lsa_gemv_coop)
     # the 8 best coop configs per (shape, rows) of profiles/r4_decode_proj_sweep.jsonl
     with open(os.path.join(ROOT, "scripts", "probes", "coop_depth_cfgs.json")) as f:
         sweep = {(k.split(",")[0], int(k.split(",")[1])): [tuple(c) for c in v] for k, v in json.load(f).items()}
@@ -76,17 +46,17 @@ def main():
                 ep = hip.make_epi(out=out, resid=out, ldo=N, ldr=N)
             norm = epi in (hip.EPI_QKV, hip.EPI_SWIGLU)
             res = {"shape": name, "M": M}
-            for d, L in libs.items():
-                hip._lib = L
+            cands = packing.coop_candidates(N // 16, K, M, epi == hip.EPI_SWIGLU)
+            for d in (3, 4):
                 best = None
                 for cfg in sweep.get((name, M), []):
-                    us = timeit(lambda i: hip.gemv(x, ws[i % nbuf], M, N, K, epi, ep, norm=norm, coop=cfg, ws=cws))
+                    c = packing.coop_norm(cfg)[:5] + (d,)
+                    if c not in cands:
+                        continue
+                    us = timeit(lambda i: hip.gemv(x, ws[i % nbuf], M, N, K, epi, ep, norm=norm, coop=c, ws=cws))
                     if best is None or us < best[0]:
-                        best = (round(us, 2), list(cfg))
+                        best = (round(us, 2), list(c))
                 res[f"d{d}"] = best
-                if best:
-                    res[f"d{d}_TBps"] = round(N * K * 2 / best[0] / 1e6, 2)
-            hip._lib = real
             print(json.dumps(res), flush=True)
         del ws
         torch.cuda.empty_cache()

@@ -97,7 +97,7 @@ def test_gemv_coop_every_config(cfg):
     with the fused RMSNorm + residual epilogue (partial sum(x^2) combined across splits and
     k-groups) and uneven chunk splits (K = 11008 -> 43 or 86 chunks)."""
     h = hip()
-    mb, tnw, nw, kf, kw = cfg
+    mb, tnw, nw, kf, kw, d = cfg
     M = {2: 29, 4: 50, 8: 100}[mb]
     N = 16 * tnw * nw * 3
     tested = 0
@@ -109,7 +109,7 @@ def test_gemv_coop_every_config(cfg):
         resid = _rnd(M, N)
         ref = resid.float() + _rmsnorm(x, g, 1e-5) @ w.float().T
         for c in packing.coop_candidates(N // 16, K, M):
-            if c[:3] != (tnw, nw, kf) or c[4] != kw:
+            if c[:3] != (tnw, nw, kf) or c[4] != kw or c[5] != d:
                 continue
             tested += 1
             out = resid.clone()
