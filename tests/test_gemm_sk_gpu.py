@@ -266,3 +266,34 @@ def test_gemm_sk_fused_rmsnorm_across_gemms(M, bn, bm, ws):
     pl = pos.long()
     assert rel_err(q, _rope_ref((xn @ wq.float().T).view(M, nh, hd), pl, cos, sin).reshape(M, -1)) < 1e-2
     assert rel_err(vc[0, :, pl].transpose(0, 1), (xn @ wv.float().T).view(M, nkv, hd)) < 1e-2
+
+
+@pytest.mark.parametrize("name,N,K,epi", [("qkv", 10240, 8192, "store"), ("o", 8192, 8192, "resid"),
+                                          ("gate_up", 57344, 8192, "swiglu"), ("down", 8192, 28672, "resid")])
+def test_gemm_llama70b_projections_at_512_rows(name, N, K, epi):
+    """The four Llama-2-70B projections at the 512-row micro-batch of the 70B stage bench, through
+    hip.gemm's tuned plan (profiles/r4_gemm_vs_hipblaslt_70b.jsonl), against fp32 PyTorch."""
+    h = hip()
+    M = 512
+    a = _rnd(M, K)
+    w = _rnd(N, K, scale=0.02)
+    ref = a.float() @ w.float().T
+    wp = packing.pack_b(w)
+    del w
+    sk_ws = h.SkWorkspace(DEV)
+    if epi == "store":
+        out = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=DEV)
+        h.gemm(a, wp, M, N, K, h.EPI_STORE, h.make_epi(out=out, ldo=N), sk_ws=sk_ws)
+        want = ref
+    elif epi == "resid":
+        resid = _rnd(M, N)
+        out = resid.clone()
+        h.gemm(a, wp, M, N, K, h.EPI_RESID, h.make_epi(out=out, resid=out, ldo=N, ldr=N), sk_ws=sk_ws)
+        want = resid.float() + ref
+    else:
+        out = torch.full((M, N // 2), float("nan"), dtype=torch.bfloat16, device=DEV)
+        h.gemm(a, wp, M, N, K, h.EPI_SWIGLU, h.make_epi(out=out, ldo=N // 2), sk_ws=sk_ws)
+        g, u = ref.view(M, N // 32, 2, 16)[:, :, 0].reshape(M, -1), ref.view(M, N // 32, 2, 16)[:, :, 1].reshape(M, -1)
+        want = F.silu(g) * u
+    torch.cuda.synchronize()
+    assert rel_err(out, want) < 1e-2, name
