@@ -347,10 +347,12 @@ SK_BM = 256  # gemm_sk.hip row tile (default; 128-row tiles for small / odd M: p
 
 # gemm_wr.hip (weights streamed into MFMA registers, 128 x bn tiles, one round of whole-K tiles)
 # where it measured faster than gemm_sk's best plan in the engine (profiles/r3_gemm_wr.md): one
-# round of 224-256 whole 128 x 192 tiles with a store / QKV epilogue. Measured only for the 7B qkv
-# projection (N 12288, K 4096) at 448-512 rows (54-55 us vs 59-81 us), so the route is limited to
-# the measured (N, K) pairs. LSA_GEMM_WR=0 turns it off (A/B runs).
-WR_TILES = (224, 256)
+# round of 192-256 whole 128 x 192 tiles with a store / QKV epilogue. Measured only for the 7B qkv
+# projection (N 12288, K 4096): at 448-512 rows 54-55 us vs 59-81 us (engine and cold-weight
+# probes), at 384 rows (192 tiles) 55.4 vs 64.1-72.5 us and hipBLASLt 59.0 (cold weights,
+# profiles/r4_gemm_wr_depth.jsonl, r4_gemm_vs_hipblaslt.jsonl), so the route is limited to the
+# measured (N, K) pairs. LSA_GEMM_WR=0 turns it off (A/B runs).
+WR_TILES = (192, 256)
 WR_MEASURED_NK = {(12288, 4096)}
 
 

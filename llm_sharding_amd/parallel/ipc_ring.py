@@ -17,7 +17,9 @@ A message must be a multiple of 4 bytes; one larger than ``slot_bytes`` (a promp
 hidden states) is carried as consecutive slot-sized chunks, so every message of a run - decode
 and prefill - can go through the rings with no communicator at all. Up to R messages per edge
 are in flight; a sender that runs R ahead waits in-kernel for the receiver's ack. Every spin is
-bounded (``timeout_s``, env ``LSA_IPC_TIMEOUT_S``): a launch that gives up sets a sticky error
+bounded (``timeout_s``, env ``LSA_IPC_TIMEOUT_S``, per R slots of a message: a chunked prefill
+message of C chunks allows ceil(C / R) x timeout_s, since its sender waits for the receiver to drain
+the ring, and the receiver may start only after its own stage's compute): a launch that gives up sets a sticky error
 word, poisons its receive buffer (0xFF bytes) instead of returning stale data, and every later
 launch of the endpoint is poisoned too; :meth:`check` raises once that happened.
 An edge whose two ends are the same rank (loopback) works without IPC mapping.
@@ -167,6 +169,11 @@ class IpcRingP2P:
         hip._req(n > 0 and n % 4 == 0, "ipc ring: message bytes must be a positive multiple of 4")
         return [(o, min(self.slot_bytes, n - o)) for o in range(0, n, self.slot_bytes)]
 
+    def _timeout_for(self, n_chunks: int) -> int:
+        """Spin bound (us) of each launch of a message of ``n_chunks`` slot-sized chunks: one
+        timeout per R chunks (a message longer than the ring waits for its receiver to drain it)."""
+        return int(self.timeout_us * max(1, -(-n_chunks // self.R)))
+
     def isend(self, t: torch.Tensor, dst: int):
         e = (self.rank, self._global(dst))
         hip._req(t.is_cuda, "ipc ring: cuda tensor")
@@ -182,9 +189,10 @@ class IpcRingP2P:
         # receive could sit behind a send that waits for it
         hip._req(e[0] != e[1] or len(chunks) <= self.R,
                  f"ipc ring: a loopback message may span at most {self.R} slots ({len(chunks)} needed)")
+        tmo = self._timeout_for(len(chunks))
         for off, nb in chunks:
             _ok(L.lsa_ipc_send(src.data_ptr() + off, nb, base + _FLAG_BYTES, self.slot_bytes, base, self.ackbox[e],
-                               self.R, self._state(e, True), self.err.data_ptr(), self.timeout_us, self.grid,
+                               self.R, self._state(e, True), self.err.data_ptr(), tmo, self.grid,
                                cs.cuda_stream), "lsa_ipc_send")
         src.record_stream(cs)
         if torch.cuda.is_current_stream_capturing():
@@ -204,9 +212,11 @@ class IpcRingP2P:
         cur, cs = torch.cuda.current_stream(self.dev), self.streams.get((e, "recv"), self.streams[e])
         cs.wait_stream(cur)
         L = _lib()
-        for off, nb in self._chunks(n):
+        chunks = self._chunks(n)
+        tmo = self._timeout_for(len(chunks))
+        for off, nb in chunks:
             _ok(L.lsa_ipc_recv(dst.data_ptr() + off, nb, base + _FLAG_BYTES, self.slot_bytes, base, self.peer_acks[e],
-                               self.R, self._state(e, False), self.err.data_ptr(), self.timeout_us, self.grid,
+                               self.R, self._state(e, False), self.err.data_ptr(), tmo, self.grid,
                                cs.cuda_stream), "lsa_ipc_recv")
         dst.record_stream(cs)
         self.captured_ops += int(torch.cuda.is_current_stream_capturing())

@@ -31,15 +31,17 @@ def test_cost_model_for_untuned_shapes():
 
 def test_gemm_wr_route(monkeypatch):
     """hip.gemm sends a projection to gemm_wr.hip only where it measured faster than gemm_sk in the
-    engine: one round of 224-256 whole 128 x 192 tiles with a store / QKV epilogue, for the measured
-    (N, K) pairs only (the 7B qkv projection at 448-512 rows); everything else, and LSA_GEMM_WR=0,
+    engine: one round of 192-256 whole 128 x 192 tiles with a store / QKV epilogue, for the measured
+    (N, K) pairs only (the 7B qkv projection at 320-512 rows); everything else, and LSA_GEMM_WR=0,
     stays on gemm_sk."""
     monkeypatch.delenv("LSA_GEMM_WR", raising=False)
     ep = hip.EpiArgs()
     assert hip.gemm_wr_plan(512, 12288, 4096, hip.EPI_QKV, ep) == 192
     assert hip.gemm_wr_plan(448, 12288, 4096, hip.EPI_STORE, ep) == 192
+    assert hip.gemm_wr_plan(384, 12288, 4096, hip.EPI_QKV, ep) == 192  # 3 row tiles: 192 tiles
     assert hip.gemm_wr_plan(447, 12288, 4096, hip.EPI_STORE, ep) is None  # last row tile < half full
-    for M, N, K, epi in [(384, 12288, 4096, hip.EPI_QKV),   # 3 row tiles: 192 tiles
+    assert hip.gemm_wr_plan(319, 12288, 4096, hip.EPI_STORE, ep) is None  # last row tile < half full
+    for M, N, K, epi in [(256, 12288, 4096, hip.EPI_QKV),   # 2 row tiles: 128 tiles
                          (513, 12288, 4096, hip.EPI_QKV),   # 5 row tiles: 320 tiles
                          (512, 12288, 4096, hip.EPI_SWIGLU),
                          (512, 4096, 4096, hip.EPI_RESID),

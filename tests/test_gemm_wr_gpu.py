@@ -98,7 +98,7 @@ def test_gemm_wr_qkv_rope_kv_append(nh, nkv, hd, norm, M):
 
 
 def test_gemm_dispatches_wr_for_one_round_of_192_tiles(monkeypatch):
-    """hip.gemm sends the 7B qkv shape at 512 rows to gemm_wr (one round of 256 whole tiles) and
+    """hip.gemm sends the 7B qkv shape at 384-512 rows to gemm_wr (one round of 192-256 whole tiles) and
     everything else to gemm_sk; LSA_GEMM_WR=0 turns it off."""
     h = hip()
     ep = h.make_epi(out=torch.empty(1, 1, device=DEV))
