@@ -96,6 +96,26 @@ def _parse_fault(spec: str):
     return int(a), int(b)
 
 
+def _startup_watchdog(rank: int, timeout_s: Optional[float] = None):
+    """Started before the RCCL process group is created, cancelled after the ring preflight's
+    results are gathered: if RCCL's own setup (eager communicator init, the world all-gather)
+    has not finished within ``timeout_s`` (``LSA_STARTUP_TIMEOUT_S``, default 180) the rank says
+    so and exits with :data:`PREFLIGHT_EXIT`."""
+    import sys
+    import threading
+    timeout_s = float(os.environ.get("LSA_STARTUP_TIMEOUT_S", "180")) if timeout_s is None else timeout_s
+
+    def _fail():
+        print(f"[bench] PREFLIGHT FAILED on rank {rank}: RCCL process-group setup did not complete within "
+              f"{timeout_s:.0f} s; exiting {PREFLIGHT_EXIT}", file=sys.stderr, flush=True)
+        os._exit(PREFLIGHT_EXIT)
+
+    wd = threading.Timer(timeout_s, _fail)
+    wd.daemon = True
+    wd.start()
+    return wd
+
+
 def preflight_edges(p2p: "DistP2P", srank: int, pp: int, dev, timeout_s: Optional[float] = None,
                     iters: int = 5, inject: bool = True) -> dict:
     """First-light check of this rank's two ring edges before anything heavy runs: one small
@@ -707,6 +727,7 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
     ipc_only = transport == "ipc" and gpu and pp > 1
     if transport not in ("rccl", "ipc"):
         raise ValueError(f"transport {transport!r}: rccl or ipc")
+    startup_wd = None
     if world > 1:
         import datetime
 
@@ -714,6 +735,11 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
         # a stuck peer surfaces as an error after 5 minutes instead of the 10-minute default
         tmo = datetime.timedelta(seconds=int(os.environ.get("LSA_DIST_TIMEOUT_S", "300")))
         if gpu and not ipc_only:
+            # the eager RCCL init (device_id) and the preflight's result gather run on the world
+            # communicator: bound them too, so a rank that never gets through RCCL's own setup
+            # exits legibly with PREFLIGHT_EXIT (the bench supervisor's fallback signal) instead of
+            # hanging until the launcher's timeout
+            startup_wd = _startup_watchdog(rank)
             dist.init_process_group("nccl", device_id=dev, timeout=tmo)
         else:
             dist.init_process_group("gloo", timeout=tmo)
@@ -758,6 +784,8 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
             preflight.update(g)
         if verbose and rank == 0:
             print(f"[bench] preflight (us per ring edge): {preflight}", flush=True)
+    if startup_wd is not None:
+        startup_wd.cancel()
     t0 = time.perf_counter()
     stage = PipelineStage(cfg, srank, pp, st.start, st.end, dev, batch, M, max_seq,
                           RandomSource(cfg, seed), use_graph=use_graph,
