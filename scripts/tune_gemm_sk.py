@@ -84,14 +84,16 @@ def main():
                     for bn in (256, 192, 128):
                         if N % (16 if bn == 192 else bn):
                             continue
-                        for sp in SPLITS:
+                        # dp 1: whole-tile rounds first, the remainder by split / stream-K; dp 0 (split 0):
+                        # pure stream-K over the whole grid (every CU busy when the tiles do not fill a round)
+                        for dp, sp in [(1, s_) for s_ in SPLITS] + [(0, 0)]:
                             try:
                                 us = timeit(lambda i: hip.gemm_sk(x, ws[i % nbuf], M, N, K, epi, ep, bn=bn, grid=hip.N_CU,
-                                                                  dp=1, split=sp, ws=sk_ws, bm=bm), a.iters)
+                                                                  dp=dp, split=sp, ws=sk_ws, bm=bm), a.iters)
                             except (RuntimeError, ValueError) as e:  # a config the host rejects for this shape
-                                print(f"# skip bm={bm} bn={bn} split={sp}: {e}", file=sys.stderr)
+                                print(f"# skip bm={bm} bn={bn} dp={dp} split={sp}: {e}", file=sys.stderr)
                                 continue
-                            res.append((round(us, 2), bn, sp, bm))
+                            res.append((round(us, 2), bn, sp, bm, dp))
                 res.sort()
                 partial = None
                 if epi == hip.EPI_RESID and 128 < M <= hip.PARTIAL_MAX_ROWS and not a.no_partial:
@@ -99,10 +101,10 @@ def main():
                     # fused (EPI_RESID + rmsnorm) against EPI_PARTIAL + resid_rmsnorm_partials
                     xn = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
                     pbuf = torch.zeros(hip.PARTIAL_MAX_SPLIT, M, N, dtype=torch.float32, device=DEV)
-                    bbn, bsp, bbm = res[0][1], res[0][2], res[0][3]
+                    bbn, bsp, bbm, bdp = res[0][1], res[0][2], res[0][3], res[0][4]
 
                     def fused(i):
-                        hip.gemm_sk(x, ws[i % nbuf], M, N, K, epi, ep, bn=bbn, grid=hip.N_CU, dp=1, split=bsp, ws=sk_ws,
+                        hip.gemm_sk(x, ws[i % nbuf], M, N, K, epi, ep, bn=bbn, grid=hip.N_CU, dp=bdp, split=bsp, ws=sk_ws,
                                     bm=bbm)
                         hip.rmsnorm(out, None, xn, M, 1e-5, N)
                     t_fused = timeit(fused, a.iters)
@@ -124,10 +126,11 @@ def main():
                     pres.sort()
                     partial = {"fused_us": round(t_fused, 2), "best": pres[0] if pres else None, "all": pres}
                 plan = hip.gemm_sk_plan(M, N, K, tuned=False)
-                model_us = next((r[0] for r in res if (r[1], r[2], r[3]) == (plan[0], plan[3], plan[4])), None)
+                model_us = next((r[0] for r in res if (r[1], r[2], r[3], r[4]) == (plan[0], plan[3], plan[4], plan[2])),
+                                None)
                 fl = 2.0 * M * N * K
                 line = {"model": model, "shape": name, "N": N, "K": K, "M": M, "epi": epi,
-                        "best_us": res[0][0], "best": [res[0][1], hip.N_CU, 1, res[0][2], res[0][3]],
+                        "best_us": res[0][0], "best": [res[0][1], hip.N_CU, res[0][4], res[0][2], res[0][3]],
                         "best_tflops": round(fl / res[0][0] / 1e6, 1), "cost_model_us": model_us,
                         "all": res, "partial": partial}
                 print(json.dumps(line), flush=True)
