@@ -85,6 +85,38 @@ def main():
         return run
 
     full = masked_stream(range(N_CU))
+    if os.environ.get("CUMASK_TRACE"):
+        # concurrent configurations for a kernel trace: do the two streams' kernels overlap in
+        # time, and how fast does each run beside the other? (attention on C spread CUs, qkv on
+        # the rest; one round per C, 4 attention + 12 GEMM launches)
+        for C in [int(c) for c in os.environ["CUMASK_TRACE"].split(",")]:
+            att_cus = spread(C)
+            gem_cus = [c for c in range(N_CU) if c not in set(att_cus)]
+            sa, sg = masked_stream(att_cus), masked_stream(gem_cus)
+            sa_alone = time_on(sa, attn)
+            g = gemm("qkv", len(gem_cus))
+            print(json.dumps({"what": "alone", "attn_cus": C, "attn_us": round(sa_alone, 2),
+                              "attn_TBps": round(kv_bytes / sa_alone / 1e6, 3),
+                              "gemm_us": round(time_on(sg, g), 2)}), flush=True)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            cur = torch.cuda.current_stream()
+            e0.record(cur)
+            sa.wait_stream(cur)
+            sg.wait_stream(cur)
+            with torch.cuda.stream(sa):
+                for i in range(4):
+                    attn(i)
+            with torch.cuda.stream(sg):
+                for i in range(12):
+                    g(i)
+            cur.wait_stream(sa)
+            cur.wait_stream(sg)
+            e1.record(cur)
+            torch.cuda.synchronize()
+            print(json.dumps({"what": "trace", "attn_cus": C, "total_us": round(e0.elapsed_time(e1) * 1e3, 1)}),
+                  flush=True)
+        return
     t_attn_full = time_on(full, attn)
     print(json.dumps({"what": "attn", "cus": N_CU, "us": round(t_attn_full, 2),
                       "TBps": round(kv_bytes / t_attn_full / 1e6, 3)}), flush=True)
