@@ -345,30 +345,38 @@ def gemm(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep
 
 SK_BM = 256  # gemm_sk.hip row tile (default; 128-row tiles for small / odd M: plan field bm)
 
-# gemm_wr.hip (weights streamed into MFMA registers, 128 x bn tiles, one round of whole-K tiles)
-# where it measured faster than gemm_sk's best plan in the engine (profiles/r3_gemm_wr.md): one
-# round of 192-256 whole 128 x 192 tiles with a store / QKV epilogue. Measured only for the 7B qkv
-# projection (N 12288, K 4096): at 448-512 rows 54-55 us vs 59-81 us (engine and cold-weight
-# probes), at 384 rows (192 tiles) 55.4 vs 64.1-72.5 us and hipBLASLt 59.0 (cold weights,
-# profiles/r4_gemm_wr_depth.jsonl, r4_gemm_vs_hipblaslt.jsonl), so the route is limited to the
-# measured (N, K) pairs. LSA_GEMM_WR=0 turns it off (A/B runs).
-WR_TILES = (192, 256)
-WR_MEASURED_NK = {(12288, 4096)}
+# gemm_wr.hip (weights streamed into MFMA registers, 128 x bn tiles, whole-K tiles): the qkv
+# projections (store / QKV epilogue) where it measured faster than gemm_sk's best plan and than
+# hipBLASLt. Per (N, K): (first row, last row, bn) ranges, each bounded by measured row counts
+# (cold-weight probes, profiles/r4_gemm_wr_shapes.jsonl; the 7B range also in the engine,
+# profiles/r3_gemm_wr.md, and the 3B / 13B ranges in engine A/B runs, profiles/r4_gemm_wr_engine_ab.txt):
+#   Llama-2-7B qkv  12288 x 4096: 384-512 rows bn 192 (54-57 us vs gemm_sk 59-81, hipBLASLt 57-59)
+#   Llama-2-13B qkv 15360 x 5120: 320-384 rows bn 192 (69-72 us vs 88-94, hipBLASLt 80-86),
+#                                 448-512 rows bn 256 (78-82 us vs 91-95, hipBLASLt 98-102)
+#   Llama-3.2-3B qkv 5120 x 3072: 384-512 rows bn 128 (37-38 us vs 43-46, hipBLASLt 41-46)
+# (70B qkv, 10240 x 8192, measured a tie at 384 rows and slower at 448: not routed.)
+# LSA_GEMM_WR=0 turns the route off (A/B runs).
+WR_ROUTES = {
+    (12288, 4096): [(320, 512, 192)],
+    (15360, 5120): [(320, 384, 192), (448, 512, 256)],
+    (5120, 3072): [(384, 512, 128)],
+}
 
 
 def gemm_wr_plan(M: int, N: int, K: int, epi: int, ep: "EpiArgs") -> Optional[int]:
     """bn for :func:`gemm_wr`, or None when gemm_sk takes the shape."""
     if os.environ.get("LSA_GEMM_WR", "1") == "0" or ep.act or ep.bias or ep.ss_out:
         return None
-    if (N, K) not in WR_MEASURED_NK or epi not in (EPI_STORE, EPI_QKV):
+    if epi not in (EPI_STORE, EPI_QKV):
         return None
     mt = -(-M // 128)
     # the last row tile at least half full: the kernel computes whole 128-row tiles, gemm_sk's
     # 128-row plans do not (measured at 448 and 512 rows)
     if M - (mt - 1) * 128 < 64:
         return None
-    if K % 256 == 0 and N % 192 == 0 and WR_TILES[0] <= mt * (N // 192) <= WR_TILES[1]:
-        return 192
+    for lo, hi, bn in WR_ROUTES.get((N, K), ()):
+        if lo <= M <= hi and N % bn == 0 and K % 64 == 0:
+            return bn
     return None
 
 

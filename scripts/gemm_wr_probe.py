@@ -58,6 +58,8 @@ def main():
             eps_ = hip.make_epi(out=out, ldo=N)
             ws_sk = hip.SkWorkspace("cuda")
             res["gemm_sk"] = round(timeit(lambda r=0: hip.gemm_sk(x, wps[r % nbuf], M, N, K, hip.EPI_STORE, eps_, ws=ws_sk)), 2)
+            refo = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+            res["hipblaslt"] = round(timeit(lambda r=0: torch.matmul(x, ws[r % nbuf].t(), out=refo)), 2)
         print(json.dumps(res), flush=True)
         del ws, wps
         torch.cuda.empty_cache()

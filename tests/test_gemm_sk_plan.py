@@ -30,25 +30,28 @@ def test_cost_model_for_untuned_shapes():
 
 
 def test_gemm_wr_route(monkeypatch):
-    """hip.gemm sends a projection to gemm_wr.hip only where it measured faster than gemm_sk in the
-    engine: one round of 192-256 whole 128 x 192 tiles with a store / QKV epilogue, for the measured
-    (N, K) pairs only (the 7B qkv projection at 320-512 rows); everything else, and LSA_GEMM_WR=0,
-    stays on gemm_sk."""
+    """hip.gemm sends a qkv projection to gemm_wr.hip only inside its measured row ranges
+    (hip.WR_ROUTES: 7B 320-512 rows bn 192; 13B 320-384 bn 192 and 448-512 bn 256; 3B 384-512
+    bn 128) with a store / QKV epilogue; everything else, and LSA_GEMM_WR=0, stays on gemm_sk."""
     monkeypatch.delenv("LSA_GEMM_WR", raising=False)
     ep = hip.EpiArgs()
     assert hip.gemm_wr_plan(512, 12288, 4096, hip.EPI_QKV, ep) == 192
     assert hip.gemm_wr_plan(448, 12288, 4096, hip.EPI_STORE, ep) == 192
-    assert hip.gemm_wr_plan(384, 12288, 4096, hip.EPI_QKV, ep) == 192  # 3 row tiles: 192 tiles
+    assert hip.gemm_wr_plan(384, 12288, 4096, hip.EPI_QKV, ep) == 192
+    assert hip.gemm_wr_plan(384, 15360, 5120, hip.EPI_QKV, ep) == 192   # 13B
+    assert hip.gemm_wr_plan(512, 15360, 5120, hip.EPI_QKV, ep) == 256
+    assert hip.gemm_wr_plan(512, 5120, 3072, hip.EPI_QKV, ep) == 128    # 3B
     assert hip.gemm_wr_plan(447, 12288, 4096, hip.EPI_STORE, ep) is None  # last row tile < half full
-    assert hip.gemm_wr_plan(319, 12288, 4096, hip.EPI_STORE, ep) is None  # last row tile < half full
-    for M, N, K, epi in [(256, 12288, 4096, hip.EPI_QKV),   # 2 row tiles: 128 tiles
-                         (513, 12288, 4096, hip.EPI_QKV),   # 5 row tiles: 320 tiles
+    assert hip.gemm_wr_plan(319, 12288, 4096, hip.EPI_STORE, ep) is None
+    for M, N, K, epi in [(256, 12288, 4096, hip.EPI_QKV),   # below the measured range
+                         (513, 12288, 4096, hip.EPI_QKV),   # above it
                          (512, 12288, 4096, hip.EPI_SWIGLU),
                          (512, 4096, 4096, hip.EPI_RESID),
-                         (384, 15360, 5120, hip.EPI_QKV),   # 13B qkv: tiles by 192, never measured
-                         (1024, 6144, 4096, hip.EPI_QKV),   # 224 tiles, never measured
+                         (384, 10240, 8192, hip.EPI_QKV),   # 70B qkv: measured a tie, not routed
+                         (1024, 6144, 4096, hip.EPI_QKV),   # never measured
                          (512, 22016, 4096, hip.EPI_SWIGLU),
-                         (512, 12288, 4160, hip.EPI_QKV)]:  # K % 256 != 0
+                         (256, 5120, 3072, hip.EPI_QKV),    # 3B below its range
+                         (512, 12288, 4160, hip.EPI_QKV)]:  # another K
         assert hip.gemm_wr_plan(M, N, K, epi, ep) is None, (M, N, K, epi)
     monkeypatch.setenv("LSA_GEMM_WR", "0")
     assert hip.gemm_wr_plan(512, 12288, 4096, hip.EPI_QKV, ep) is None

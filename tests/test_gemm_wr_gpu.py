@@ -64,13 +64,17 @@ def _rope_ref(t, pos, cos, sin):
 @pytest.mark.parametrize("nh,nkv,hd", [(32, 32, 128), (8, 2, 64), (24, 8, 128)])
 @pytest.mark.parametrize("norm", [False, True])
 @pytest.mark.parametrize("M", [300, 512])
-def test_gemm_wr_qkv_rope_kv_append(nh, nkv, hd, norm, M):
+@pytest.mark.parametrize("bn", [0, 256])
+def test_gemm_wr_qkv_rope_kv_append(nh, nkv, hd, norm, M, bn):
+    """bn 0: 192 where N tiles by it, else 128 (the routed widths); 256: the 13B route's width."""
     from llm_sharding_amd.config import tiny
     from llm_sharding_amd.models.rope import rope_table
     h = hip()
     H, slots, T, eps = 1024, 3, 512, 1e-5
     N = (nh + 2 * nkv) * hd
-    bn = 192 if N % 192 == 0 else 128
+    bn = bn or (192 if N % 192 == 0 else 128)
+    if N % bn:
+        pytest.skip("N does not tile by bn")
     wq, wk, wv = _rnd(nh * hd, H, scale=0.05), _rnd(nkv * hd, H, scale=0.05), _rnd(nkv * hd, H, scale=0.05)
     x = _rnd(M, H)
     cos, sin = rope_table(tiny(head_dim=hd), T, DEV)
@@ -103,7 +107,7 @@ def test_gemm_dispatches_wr_for_one_round_of_192_tiles(monkeypatch):
     h = hip()
     ep = h.make_epi(out=torch.empty(1, 1, device=DEV))
     assert h.gemm_wr_plan(512, 12288, 4096, h.EPI_QKV, ep) == 192
-    assert h.gemm_wr_plan(384, 15360, 5120, h.EPI_QKV, ep) is None  # 13B qkv: tiles, not measured
+    assert h.gemm_wr_plan(384, 10240, 8192, h.EPI_QKV, ep) is None  # 70B qkv: measured a tie
     assert h.gemm_wr_plan(512, 12288, 4096, h.EPI_SWIGLU, ep) is None
     assert h.gemm_wr_plan(2048, 12288, 4096, h.EPI_QKV, ep) is None
     assert h.gemm_wr_plan(512, 4096, 4096, h.EPI_STORE, ep) is None
