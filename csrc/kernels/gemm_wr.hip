@@ -209,11 +209,12 @@ LSA_DEVICE void gemm_wr_body(unsigned char* smem, const bf16_raw* __restrict__ A
     wr_barrier();
 
     // epilogue: fp32 tile through a wave-private LDS image; one lane per (row, 16 columns)
-    // unit runs the row16 epilogues of epilogue.h (EPI_QKV: RoPE + KV-cache append; with
-    // ss_in, the fused RMSNorm's row scale first, computed once per workgroup in gemm_sk's
-    // summation order so both GEMMs produce the same bits)
+    // unit runs the row16 epilogues of epilogue.h (EPI_QKV: RoPE + KV-cache append), or per
+    // (row, gate/up tile pair) the SwiGLU; with ss_in, the fused RMSNorm's row scale first,
+    // computed once per workgroup in gemm_sk's summation order so both GEMMs produce the same bits
+    constexpr bool NORM_IN = EPI == EPI_QKV || EPI == EPI_SWIGLU;
     float* s_rs = reinterpret_cast<float*>(smem + G_::RS_OFF);
-    if (EPI == EPI_QKV && ep.ss_in) {
+    if (NORM_IN && ep.ss_in) {
       for (int r = threadIdx.x; r < WR_BM; r += WR_NTHR) {
         const int m = min(m0 + r, M - 1);
         const float* sp = ep.ss_in + (size_t)m * ep.ss_n;
@@ -240,6 +241,36 @@ LSA_DEVICE void gemm_wr_body(unsigned char* smem, const bf16_raw* __restrict__ A
         for (int r = 0; r < 4; ++r) img[(i * 16 + 4 * (lane >> 4) + r) * G_::ELD + j * 16 + (lane & 15)] = acc[i][j][r];
     __syncthreads();  // the image and the row scales are complete
     const int col_base = nt * BN + w * TN;
+    if constexpr (EPI == EPI_SWIGLU) {
+      // 16-column tiles interleave gate / up (packing.fuse_gate_up): this wave's FN tiles are
+      // FN / 2 (gate, up) pairs; pair p of the wave writes output columns col_base / 2 + 16 p
+      constexpr int FP = FN / 2, NUP = (WR_BM * FP) / 64;
+      static_assert(FN % 2 == 0, "SwiGLU needs whole gate / up tile pairs per wave");
+#pragma unroll
+      for (int s2 = 0; s2 < NUP; ++s2) {
+        const int u = lane + 64 * s2, row = u / FP, jp = u % FP;
+        const int m = m0 + row;
+        float g[16], up[16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          *reinterpret_cast<f32x4_t*>(g + 4 * q) = *reinterpret_cast<const f32x4_t*>(img + row * G_::ELD + (2 * jp) * 16 + 4 * q);
+          *reinterpret_cast<f32x4_t*>(up + 4 * q) =
+              *reinterpret_cast<const f32x4_t*>(img + row * G_::ELD + (2 * jp + 1) * 16 + 4 * q);
+        }
+        if (m < M) {
+          const float rsc = ep.ss_in ? s_rs[row] : 1.f;
+#pragma unroll
+          for (int q = 0; q < 16; ++q) g[q] = silu(g[q] * rsc) * (up[q] * rsc);
+          bf16_raw* o = ep.out + (size_t)m * ep.ldo + col_base / 2 + jp * 16;
+          st16(o, pack8(g));
+          st16(o + 8, pack8(g + 8));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      wr_vm_wait<0>();
+      wr_barrier();
+      continue;
+    }
     constexpr int NU = (WR_BM * FN) / 64;  // unit passes per wave
 #pragma unroll
     for (int s2 = 0; s2 < NU; ++s2) {
@@ -285,7 +316,8 @@ int wr_launch(const bf16_raw* A, int lda, const bf16_raw* W, int M, int N, int K
 }  // namespace
 
 // 128-row x bn tiles, weights straight into MFMA registers (see the header comment). epi:
-// EPI_STORE or EPI_QKV (with the fused-RMSNorm row scale when ep->ss_in is set: K == 64 ss_n).
+// EPI_STORE, EPI_QKV or EPI_SWIGLU (bn 128 / 256; gate / up tiles interleaved), the last two with
+// the fused-RMSNorm row scale when ep->ss_in is set (K == 64 ss_n).
 // bn: 128 / 192 / 256 with N % bn == 0; K % 64 == 0; grid: workgroups (tiles beyond it loop).
 // Returns LSA_BAD_SHAPE on any shape the kernel's indexing cannot take.
 // (Ring depth: 4 slots. 6 and 8 slots - weights prefetched 5 / 7 K-steps ahead - measured no
@@ -296,16 +328,21 @@ extern "C" int lsa_gemm_wr(const void* a, int lda, const void* wp, int M, int N,
   if (M < 1 || K < WR_BK || K % WR_BK || lda < K || lda % 8 || grid < 1 || !ep) return LSA_BAD_SHAPE;
   if (bn != 128 && bn != 192 && bn != 256) return LSA_UNSUPPORTED;
   if (N % bn) return LSA_BAD_SHAPE;
-  if (epi != EPI_STORE && epi != EPI_QKV) return LSA_UNSUPPORTED;
+  if (epi != EPI_STORE && epi != EPI_QKV && epi != EPI_SWIGLU) return LSA_UNSUPPORTED;
+  if (epi == EPI_SWIGLU && bn == 192) return LSA_UNSUPPORTED;  // 3 tiles per wave: no whole gate/up pairs
   if (epi == EPI_STORE && (!ep->out || ep->ldo < N || ep->ldo % 8)) return LSA_BAD_SHAPE;
+  if (epi == EPI_SWIGLU && (!ep->out || ep->ldo < N / 2 || ep->ldo % 8 || ep->act || ep->bias)) return LSA_BAD_SHAPE;
   if (epi == EPI_QKV && (!ep->k_cache || !ep->v_cache || !ep->slot || !ep->pos || !ep->out)) return LSA_BAD_SHAPE;
   if (ep->ss_out) return LSA_BAD_SHAPE;
-  if (ep->ss_in && (epi != EPI_QKV || ep->ss_n < 4 || ep->ss_n % 4 || K != 64 * ep->ss_n)) return LSA_BAD_SHAPE;
+  if (ep->ss_in && (epi == EPI_STORE || ep->ss_n < 4 || ep->ss_n % 4 || K != 64 * ep->ss_n)) return LSA_BAD_SHAPE;
   const bf16_raw* A = static_cast<const bf16_raw*>(a);
   const bf16_raw* W = static_cast<const bf16_raw*>(wp);
 #define LSA_WR(FN)                                                                                    \
   return epi == EPI_QKV ? wr_launch<FN, 4, EPI_QKV>(A, lda, W, M, N, K, *ep, grid, stream)         \
                         : wr_launch<FN, 4, EPI_STORE>(A, lda, W, M, N, K, *ep, grid, stream);
+  if (epi == EPI_SWIGLU)
+    return bn == 128 ? wr_launch<2, 4, EPI_SWIGLU>(A, lda, W, M, N, K, *ep, grid, stream)
+                     : wr_launch<4, 4, EPI_SWIGLU>(A, lda, W, M, N, K, *ep, grid, stream);
   if (bn == 128) { LSA_WR(2) }
   if (bn == 192) { LSA_WR(3) }
   LSA_WR(4)

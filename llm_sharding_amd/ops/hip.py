@@ -354,12 +354,15 @@ SK_BM = 256  # gemm_sk.hip row tile (default; 128-row tiles for small / odd M: p
 #   Llama-2-13B qkv 15360 x 5120: 320-384 rows bn 192 (69-72 us vs 88-94, hipBLASLt 80-86),
 #                                 448-512 rows bn 256 (78-82 us vs 91-95, hipBLASLt 98-102)
 #   Llama-3.2-3B qkv 5120 x 3072: 384-512 rows bn 128 (37-38 us vs 43-46, hipBLASLt 41-46)
+#   Llama-3.2-3B gate_up 16384 x 3072 (SwiGLU): 384-512 rows bn 256 (store epilogue 56-60 us vs
+#                                 gemm_sk 71-74, hipBLASLt 62-74)
 # (70B qkv, 10240 x 8192, measured a tie at 384 rows and slower at 448: not routed.)
 # LSA_GEMM_WR=0 turns the route off (A/B runs).
 WR_ROUTES = {
     (12288, 4096): [(320, 512, 192)],
     (15360, 5120): [(320, 384, 192), (448, 512, 256)],
     (5120, 3072): [(384, 512, 128)],
+    (16384, 3072): [(384, 512, 256)],
 }
 
 
@@ -367,7 +370,7 @@ def gemm_wr_plan(M: int, N: int, K: int, epi: int, ep: "EpiArgs") -> Optional[in
     """bn for :func:`gemm_wr`, or None when gemm_sk takes the shape."""
     if os.environ.get("LSA_GEMM_WR", "1") == "0" or ep.act or ep.bias or ep.ss_out:
         return None
-    if epi not in (EPI_STORE, EPI_QKV):
+    if epi not in (EPI_STORE, EPI_QKV, EPI_SWIGLU):
         return None
     mt = -(-M // 128)
     # the last row tile at least half full: the kernel computes whole 128-row tiles, gemm_sk's
@@ -375,7 +378,7 @@ def gemm_wr_plan(M: int, N: int, K: int, epi: int, ep: "EpiArgs") -> Optional[in
     if M - (mt - 1) * 128 < 64:
         return None
     for lo, hi, bn in WR_ROUTES.get((N, K), ()):
-        if lo <= M <= hi and N % bn == 0 and K % 64 == 0:
+        if lo <= M <= hi and N % bn == 0 and K % 64 == 0 and not (epi == EPI_SWIGLU and bn == 192):
             return bn
     return None
 
@@ -383,14 +386,16 @@ def gemm_wr_plan(M: int, N: int, K: int, epi: int, ep: "EpiArgs") -> Optional[in
 def gemm_wr(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int, ep: EpiArgs, bn: int = 192,
             grid: int = 0) -> None:
     """Projection GEMM with the weights fetched straight into MFMA B registers (gemm_wr.hip):
-    128 x ``bn`` tiles, one per workgroup per round, A staged by LDS-DMA, EPI_STORE / EPI_QKV
-    (with the fused RMSNorm row scale, ``ep.ss_in``). K % 64 == 0, N % bn == 0."""
+    128 x ``bn`` tiles, one per workgroup per round, A staged by LDS-DMA, EPI_STORE / EPI_QKV /
+    EPI_SWIGLU (the last two with the fused RMSNorm row scale, ``ep.ss_in``). K % 64 == 0,
+    N % bn == 0."""
     _req(_is_bf16_cuda(a, wp), "gemm_wr: bf16 cuda tensors required")
     _req(wp.numel() == N * K and K % 64 == 0, "gemm_wr: packed weight shape (K % 64 == 0)")
     _req(a.dim() == 2 and a.shape[0] >= M >= 1 and a.shape[1] >= K and a.stride(1) == 1 and a.stride(0) % 8 == 0
          and a.data_ptr() % 16 == 0, "gemm_wr: A must be [>=M, >=K] row-major with 16-B aligned rows")
     _req(bn in (128, 192, 256) and N % bn == 0, f"gemm_wr: N={N} does not tile by bn={bn}")
-    _req(epi in (EPI_STORE, EPI_QKV), "gemm_wr: EPI_STORE / EPI_QKV")
+    _req(epi in (EPI_STORE, EPI_QKV, EPI_SWIGLU), "gemm_wr: EPI_STORE / EPI_QKV / EPI_SWIGLU")
+    _req(epi != EPI_SWIGLU or bn != 192, "gemm_wr: SwiGLU needs bn 128 / 256 (whole gate/up pairs per wave)")
     _req(not ep.ss_out, "gemm_wr: no ss_out epilogue")
     _check_epi(epi, ep, N)
     rc = lib().lsa_gemm_wr(_p(a), a.stride(0), _p(wp), M, N, K, epi, ctypes.byref(ep), bn, grid or N_CU, _stream())

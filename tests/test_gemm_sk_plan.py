@@ -31,8 +31,8 @@ def test_cost_model_for_untuned_shapes():
 
 def test_gemm_wr_route(monkeypatch):
     """hip.gemm sends a qkv projection to gemm_wr.hip only inside its measured row ranges
-    (hip.WR_ROUTES: 7B 320-512 rows bn 192; 13B 320-384 bn 192 and 448-512 bn 256; 3B 384-512
-    bn 128) with a store / QKV epilogue; everything else, and LSA_GEMM_WR=0, stays on gemm_sk."""
+    (hip.WR_ROUTES: 7B 320-512 rows bn 192; 13B 320-384 bn 192 and 448-512 bn 256; 3B qkv 384-512
+    bn 128, 3B gate_up 384-512 bn 256 SwiGLU); everything else, and LSA_GEMM_WR=0, stays on gemm_sk."""
     monkeypatch.delenv("LSA_GEMM_WR", raising=False)
     ep = hip.EpiArgs()
     assert hip.gemm_wr_plan(512, 12288, 4096, hip.EPI_QKV, ep) == 192
@@ -41,6 +41,7 @@ def test_gemm_wr_route(monkeypatch):
     assert hip.gemm_wr_plan(384, 15360, 5120, hip.EPI_QKV, ep) == 192   # 13B
     assert hip.gemm_wr_plan(512, 15360, 5120, hip.EPI_QKV, ep) == 256
     assert hip.gemm_wr_plan(512, 5120, 3072, hip.EPI_QKV, ep) == 128    # 3B
+    assert hip.gemm_wr_plan(512, 16384, 3072, hip.EPI_SWIGLU, ep) == 256  # 3B gate_up
     assert hip.gemm_wr_plan(447, 12288, 4096, hip.EPI_STORE, ep) is None  # last row tile < half full
     assert hip.gemm_wr_plan(319, 12288, 4096, hip.EPI_STORE, ep) is None
     for M, N, K, epi in [(256, 12288, 4096, hip.EPI_QKV),   # below the measured range

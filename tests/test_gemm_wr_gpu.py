@@ -101,6 +101,30 @@ def test_gemm_wr_qkv_rope_kv_append(nh, nkv, hd, norm, M, bn):
     assert rel_err(vc[sl, :, pl], vr) < 1e-2
 
 
+@pytest.mark.parametrize("M,I,H", [(512, 8192, 3072), (300, 1024, 512), (129, 2048, 1024)])
+@pytest.mark.parametrize("bn", [128, 256])
+@pytest.mark.parametrize("norm", [False, True])
+def test_gemm_wr_swiglu(M, I, H, bn, norm):
+    """EPI_SWIGLU on gemm_wr (gate / up tiles interleaved by packing.fuse_gate_up), with and
+    without the fused-RMSNorm row scale (ss_in), against fp32 silu(x W_g^T) * (x W_u^T)."""
+    import torch.nn.functional as F
+    h = hip()
+    eps = 1e-5
+    x = _rnd(M, H)
+    wg, wu = _rnd(I, H, scale=0.05), _rnd(I, H, scale=0.05)
+    xf = x.float()
+    ss = None
+    if norm:
+        ss = torch.empty(M, H // 64, device=DEV)
+        h.row_ss(x, M, ss)
+        xf = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)
+    out = torch.full((M, I), float("nan"), dtype=torch.bfloat16, device=DEV)
+    ep = h.make_epi(out=out, ldo=I, ss_in=ss, ss_eps=eps)
+    h.gemm_wr(x, packing.pack_b(packing.fuse_gate_up(wg, wu)), M, 2 * I, H, h.EPI_SWIGLU, ep, bn=bn)
+    ref = F.silu(xf @ wg.float().T) * (xf @ wu.float().T)
+    assert rel_err(out, ref) < 1e-2
+
+
 def test_gemm_dispatches_wr_for_one_round_of_192_tiles(monkeypatch):
     """hip.gemm sends the 7B qkv shape at 384-512 rows to gemm_wr (one round of 192-256 whole tiles) and
     everything else to gemm_sk; LSA_GEMM_WR=0 turns it off."""
