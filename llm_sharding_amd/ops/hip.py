@@ -350,19 +350,22 @@ SK_BM = 256  # gemm_sk.hip row tile (default; 128-row tiles for small / odd M: p
 # hipBLASLt. Per (N, K): (first row, last row, bn) ranges, each bounded by measured row counts
 # (cold-weight probes, profiles/r4_gemm_wr_shapes.jsonl; the 7B range also in the engine,
 # profiles/r3_gemm_wr.md, and the 3B / 13B ranges in engine A/B runs, profiles/r4_gemm_wr_engine_ab.txt):
-#   Llama-2-7B qkv  12288 x 4096: 384-512 rows bn 192 (54-57 us vs gemm_sk 59-81, hipBLASLt 57-59)
+#   Llama-2-7B qkv  12288 x 4096: 384-512 rows bn 192 (54-57 us vs gemm_sk 59-81, hipBLASLt 57-59),
+#                                 256 rows bn 128 (49 vs 52, hipBLASLt 65)
 #   Llama-2-13B qkv 15360 x 5120: 320-384 rows bn 192 (69-72 us vs 88-94, hipBLASLt 80-86),
-#                                 448-512 rows bn 256 (78-82 us vs 91-95, hipBLASLt 98-102)
-#   Llama-3.2-3B qkv 5120 x 3072: 384-512 rows bn 128 (37-38 us vs 43-46, hipBLASLt 41-46)
-#   Llama-3.2-3B gate_up 16384 x 3072 (SwiGLU): 384-512 rows bn 256 (store epilogue 56-60 us vs
-#                                 gemm_sk 71-74, hipBLASLt 62-74)
+#                                 448-512 rows bn 256 (78-82 us vs 91-95, hipBLASLt 98-102),
+#                                 256 rows bn 128 (64 vs 69, hipBLASLt 80)
+#   Llama-3.2-3B qkv 5120 x 3072: 256-512 rows bn 128 (37-38 us vs 40-46, hipBLASLt 41-49)
+#   Llama-3.2-3B gate_up 16384 x 3072 (SwiGLU): 320-512 rows bn 256 (store epilogue 52-60 us vs
+#                                 gemm_sk 68-74, hipBLASLt 57-74), 256 rows bn 128 (41 vs 73, 58)
+# A range starting at 193 rows covers the same 2-row-tile grid as its measured 256-row point.
 # (70B qkv, 10240 x 8192, measured a tie at 384 rows and slower at 448: not routed.)
 # LSA_GEMM_WR=0 turns the route off (A/B runs).
 WR_ROUTES = {
-    (12288, 4096): [(320, 512, 192)],
-    (15360, 5120): [(320, 384, 192), (448, 512, 256)],
-    (5120, 3072): [(384, 512, 128)],
-    (16384, 3072): [(384, 512, 256)],
+    (12288, 4096): [(193, 256, 128), (320, 512, 192)],
+    (15360, 5120): [(193, 256, 128), (320, 384, 192), (448, 512, 256)],
+    (5120, 3072): [(193, 512, 128)],
+    (16384, 3072): [(193, 256, 128), (320, 512, 256)],
 }
 
 

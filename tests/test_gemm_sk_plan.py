@@ -31,8 +31,7 @@ def test_cost_model_for_untuned_shapes():
 
 def test_gemm_wr_route(monkeypatch):
     """hip.gemm sends a qkv projection to gemm_wr.hip only inside its measured row ranges
-    (hip.WR_ROUTES: 7B 320-512 rows bn 192; 13B 320-384 bn 192 and 448-512 bn 256; 3B qkv 384-512
-    bn 128, 3B gate_up 384-512 bn 256 SwiGLU); everything else, and LSA_GEMM_WR=0, stays on gemm_sk."""
+    (hip.WR_ROUTES); everything else, and LSA_GEMM_WR=0, stays on gemm_sk."""
     monkeypatch.delenv("LSA_GEMM_WR", raising=False)
     ep = hip.EpiArgs()
     assert hip.gemm_wr_plan(512, 12288, 4096, hip.EPI_QKV, ep) == 192
@@ -44,14 +43,16 @@ def test_gemm_wr_route(monkeypatch):
     assert hip.gemm_wr_plan(512, 16384, 3072, hip.EPI_SWIGLU, ep) == 256  # 3B gate_up
     assert hip.gemm_wr_plan(447, 12288, 4096, hip.EPI_STORE, ep) is None  # last row tile < half full
     assert hip.gemm_wr_plan(319, 12288, 4096, hip.EPI_STORE, ep) is None
-    for M, N, K, epi in [(256, 12288, 4096, hip.EPI_QKV),   # below the measured range
+    assert hip.gemm_wr_plan(256, 12288, 4096, hip.EPI_QKV, ep) == 128   # 2 row tiles
+    assert hip.gemm_wr_plan(256, 16384, 3072, hip.EPI_SWIGLU, ep) == 128
+    for M, N, K, epi in [(192, 12288, 4096, hip.EPI_QKV),   # below the measured range
                          (513, 12288, 4096, hip.EPI_QKV),   # above it
                          (512, 12288, 4096, hip.EPI_SWIGLU),
                          (512, 4096, 4096, hip.EPI_RESID),
                          (384, 10240, 8192, hip.EPI_QKV),   # 70B qkv: measured a tie, not routed
                          (1024, 6144, 4096, hip.EPI_QKV),   # never measured
                          (512, 22016, 4096, hip.EPI_SWIGLU),
-                         (256, 5120, 3072, hip.EPI_QKV),    # 3B below its range
+                         (128, 5120, 3072, hip.EPI_QKV),    # 3B below its range
                          (512, 12288, 4160, hip.EPI_QKV)]:  # another K
         assert hip.gemm_wr_plan(M, N, K, epi, ep) is None, (M, N, K, epi)
     monkeypatch.setenv("LSA_GEMM_WR", "0")
