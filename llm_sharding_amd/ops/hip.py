@@ -358,6 +358,8 @@ SK_BM = 256  # gemm_sk.hip row tile (default; 128-row tiles for small / odd M: p
 #   Llama-3.2-3B qkv 5120 x 3072: 256-512 rows bn 128 (37-38 us vs 40-46, hipBLASLt 41-49)
 #   Llama-3.2-3B gate_up 16384 x 3072 (SwiGLU): 320-512 rows bn 256 (store epilogue 52-60 us vs
 #                                 gemm_sk 68-74, hipBLASLt 57-74), 256 rows bn 128 (41 vs 73, 58)
+#   Llama-2-7B gate_up 22016 x 4096 (SwiGLU): 256 rows bn 256 (store 68 us vs gemm_sk 75, 76)
+#   Llama-2-13B gate_up 27648 x 5120 (SwiGLU): 256 rows bn 256 (94 us vs 101, 104)
 # A range starting at 193 rows covers the same 2-row-tile grid as its measured 256-row point.
 # (70B qkv, 10240 x 8192, measured a tie at 384 rows and slower at 448: not routed.)
 # LSA_GEMM_WR=0 turns the route off (A/B runs).
@@ -366,6 +368,8 @@ WR_ROUTES = {
     (15360, 5120): [(193, 256, 128), (320, 384, 192), (448, 512, 256)],
     (5120, 3072): [(193, 512, 128)],
     (16384, 3072): [(193, 256, 128), (320, 512, 256)],
+    (22016, 4096): [(193, 256, 256)],
+    (27648, 5120): [(193, 256, 256)],
 }
 
 
