@@ -1,7 +1,9 @@
 // Projection GEMM with the weights streamed straight into MFMA B registers.
-// hip.gemm routes it one round of 224-256 whole 128 x 192 tiles (the 7B qkv projection at
-// 448-512 rows: 57.9 vs 68.1 us per layer in the headline decode step, profiles/r3_gemm_wr.md);
-// gemm_sk.hip stays faster on every other measured shape.
+// hip.gemm routes to it from a measured per-shape table (ops/hip.py WR_ROUTES): the qkv and
+// SwiGLU gate_up projections at the row counts where its 128-row tiles fill about one round
+// (e.g. the 7B qkv at 448-512 rows: 57.9 vs 68.1 us per layer in the headline decode step,
+// profiles/r3_gemm_wr.md; 3B / 13B shapes in profiles/r4_gemm_wr_shapes.jsonl and the engine
+// A/B runs in profiles/r4_gemm_wr_engine_ab.txt). gemm_sk.hip keeps every other shape.
 //
 //   C[M, N] = A[M, K] @ W^T, bf16 in, fp32 accumulate.
 //
