@@ -100,11 +100,13 @@ def spawn_ranks(n: int) -> int:
     import subprocess
     port = _free_port()
     procs = []
+    _forward_termination(lambda: procs)
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PYTHONUNBUFFERED="1")
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
-                                      stdout=None if r == 0 else subprocess.DEVNULL, start_new_session=True))
+                                      stdout=None if r == 0 else subprocess.DEVNULL, start_new_session=True,
+                                      preexec_fn=_die_with_parent))
     rc = 0
     pending = list(range(n))
     while pending:
@@ -128,12 +130,59 @@ def spawn_ranks(n: int) -> int:
 PREFLIGHT_EXIT = 75  # = parallel.pipeline.PREFLIGHT_EXIT (not imported: the supervisor stays light)
 
 
+def _die_with_parent() -> None:
+    """preexec_fn of every child this script starts: the kernel sends the child SIGKILL when the
+    process that started it exits (PR_SET_PDEATHSIG), however that happens - a launcher's killpg
+    aimed at the parent's process group, a driver timeout, SIGKILL - so no GPU-holding worker
+    outlives its supervisor in its own session."""
+    import ctypes
+    import signal
+    try:
+        ctypes.CDLL(None, use_errno=True).prctl(1, int(signal.SIGKILL), 0, 0, 0)  # PR_SET_PDEATHSIG = 1
+    except Exception:  # noqa: BLE001 - not Linux: the signal handlers below still stop the children
+        pass
+
+
+def _stop_group(proc, grace_s: float = 10.0) -> None:
+    """SIGTERM the child's process group, then SIGKILL it if it is still there after ``grace_s``."""
+    import signal
+    if proc is None or proc.poll() is not None:
+        return
+    try:
+        os.killpg(proc.pid, signal.SIGTERM)
+        proc.wait(timeout=grace_s)
+    except ProcessLookupError:
+        return
+    except Exception:  # noqa: BLE001 - TimeoutExpired
+        try:
+            os.killpg(proc.pid, signal.SIGKILL)
+        except ProcessLookupError:
+            pass
+        proc.wait()
+
+
+def _forward_termination(children) -> None:
+    """SIGTERM / SIGINT / SIGHUP to this process stop every child process group it started
+    (``children()`` lists them), then exit with 128 + signal."""
+    import signal
+
+    def handler(signum, _frame):
+        signal.signal(signum, signal.SIG_DFL)
+        for p in children():
+            _stop_group(p)
+        os._exit(128 + signum)
+
+    for sig in (signal.SIGTERM, signal.SIGINT, signal.SIGHUP):
+        signal.signal(sig, handler)
+
+
 def _spawn_worker(argv: list, port: int, extra_env: dict):
     import subprocess
     env = dict(os.environ, MASTER_PORT=str(port), LSA_BENCH_ROLE="worker", PYTHONUNBUFFERED="1", **extra_env)
     # the workers rendezvous on their own store (rank 0's worker hosts it), not torchrun's agent store
     env.pop("TORCHELASTIC_USE_AGENT_STORE", None)
-    return subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env, start_new_session=True)
+    return subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env, start_new_session=True,
+                            preexec_fn=_die_with_parent)
 
 
 def _watch(proc, store, rank: int, world: int, attempt: int) -> int:
@@ -178,6 +227,8 @@ def supervise(a, argv: list) -> int:
     dist.init_process_group("gloo", timeout=datetime.timedelta(hours=2))
     store = dist.distributed_c10d._get_default_store()
     attempts = [([], {})]
+    current = []  # the running worker: stopped with this supervisor (signal handlers + PDEATHSIG)
+    _forward_termination(lambda: current)
     if a.transport == "rccl" and a.fallback:
         attempts.append((["--transport", "ipc"], {"LSA_BENCH_FALLBACK": "1"}))
     code = 0
@@ -189,6 +240,7 @@ def supervise(a, argv: list) -> int:
             print(f"[bench] ring preflight failed on the RCCL transport: restarting every rank once with "
                   f"--transport ipc", file=sys.stderr, flush=True)
         proc = _spawn_worker(argv + extra, port, env)
+        current[:] = [proc]
         code = _watch(proc, store, rank, world, i)
         store.set(f"lsa_bench/{i}/exit/{rank}", str(code))
         keys = [f"lsa_bench/{i}/exit/{r}" for r in range(world)]

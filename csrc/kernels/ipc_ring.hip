@@ -171,15 +171,41 @@ int grid_for(long long nbytes, int grid) {
 
 // ---- host API --------------------------------------------------------------------------------
 // Device buffer that another process can map: zero-filled, 256-B aligned; handle = 64 bytes.
-extern "C" int lsa_ipc_alloc(long long bytes, void** ptr, void* handle) {
-  if (bytes <= 0 || !ptr || !handle) return LSA_BAD_SHAPE;
-  if (hipMalloc(ptr, (size_t)bytes) != hipSuccess) return LSA_LAUNCH_FAILED;
-  if (hipMemset(*ptr, 0, (size_t)bytes) != hipSuccess) return LSA_LAUNCH_FAILED;
-  if (hipDeviceSynchronize() != hipSuccess) return LSA_LAUNCH_FAILED;
-  hipIpcMemHandle_t h;
-  if (hipIpcGetMemHandle(&h, *ptr) != hipSuccess) return LSA_LAUNCH_FAILED;
-  memcpy(handle, &h, sizeof(h));
-  return LSA_OK;
+//
+// Coherence rule the ring relies on: the inbox (flags + slots) is written by the PEER GPU over
+// xGMI while this GPU's receive kernel polls and reads it, and the ack box likewise. A plain
+// hipMalloc buffer is coarse-grained: the HIP memory model makes a remote agent's writes to it
+// visible only at kernel boundaries, because the owning GPU's L2 may keep a stale copy of a line
+// that a peer has since rewritten in HBM (the sc0 sc1 bits bypass L1 and write L2 through, but do
+// not make a stale local-L2 line coherent with a remote write). So these buffers are allocated
+// UNCACHED (hipDeviceMallocUncached: MTYPE UC, every access goes to memory, coherent across agents
+// during a kernel), falling back to fine-grained (hipDeviceMallocFinegrained: coherent across agents
+// at system scope) if the uncached kind cannot be allocated or exported, and to coarse-grained only
+// as a last resort. *kind reports what was used: 2 uncached, 1 fine-grained, 0 coarse (the pipeline
+// refuses 0 for an edge between two GPUs: parallel/ipc_ring.py). ``first`` skips the stronger kinds
+// (0 tries uncached first; 1 fine-grained first; 2 coarse only - the cost A/B of scripts/ipc_ring_check.py).
+extern "C" int lsa_ipc_alloc(long long bytes, void** ptr, void* handle, int* kind, int first) {
+  if (bytes <= 0 || !ptr || !handle || !kind || first < 0 || first > 2) return LSA_BAD_SHAPE;
+  const unsigned flags[3] = {hipDeviceMallocUncached, hipDeviceMallocFinegrained, hipDeviceMallocDefault};
+  for (int i = first; i < 3; ++i) {
+    *ptr = nullptr;
+    if (hipExtMallocWithFlags(ptr, (size_t)bytes, flags[i]) != hipSuccess || !*ptr) {
+      (void)hipGetLastError();
+      continue;
+    }
+    hipIpcMemHandle_t h;
+    if (hipMemset(*ptr, 0, (size_t)bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
+        hipIpcGetMemHandle(&h, *ptr) != hipSuccess) {
+      (void)hipGetLastError();
+      (void)hipFree(*ptr);
+      *ptr = nullptr;
+      continue;
+    }
+    memcpy(handle, &h, sizeof(h));
+    *kind = 2 - i;
+    return LSA_OK;
+  }
+  return LSA_LAUNCH_FAILED;
 }
 
 extern "C" int lsa_ipc_handle_bytes() { return (int)sizeof(hipIpcMemHandle_t); }

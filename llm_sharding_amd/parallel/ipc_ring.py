@@ -40,7 +40,7 @@ def _lib():
     L = hip.lib()
     if not getattr(L, "_ipc_typed", False):
         vp, ll, i = ctypes.c_void_p, ctypes.c_longlong, ctypes.c_int
-        L.lsa_ipc_alloc.argtypes = [ll, ctypes.POINTER(vp), vp]
+        L.lsa_ipc_alloc.argtypes = [ll, ctypes.POINTER(vp), vp, ctypes.POINTER(i), i]
         L.lsa_ipc_handle_bytes.argtypes = []
         L.lsa_ipc_open.argtypes = [vp, ctypes.POINTER(vp)]
         L.lsa_ipc_close.argtypes = [vp]
@@ -49,6 +49,14 @@ def _lib():
         L.lsa_ipc_recv.argtypes = [vp, ll, vp, ll, vp, vp, i, vp, vp, ll, i, vp]
         L._ipc_typed = True
     return L
+
+
+def _device_uuid(dev: torch.device) -> str:
+    """Identity of the physical GPU (two processes may share one: the 1-GPU test harness)."""
+    try:
+        return str(torch.cuda.get_device_properties(dev).uuid)
+    except Exception:  # noqa: BLE001 - older torch: fall back to the PCI bus id
+        return str(getattr(torch.cuda.get_device_properties(dev), "pci_bus_id", dev.index))
 
 
 def _ok(rc: int, what: str) -> None:
@@ -99,19 +107,30 @@ class IpcRingP2P:
         self._own, self._opened = [], []
         mine = {}  # (edge, "inbox" | "acks") -> handle bytes
         self.inbox, self.ackbox = {}, {}
+        # what each peer-written buffer was allocated as (csrc/kernels/ipc_ring.hip lsa_ipc_alloc:
+        # 2 uncached, 1 fine-grained, 0 coarse-grained); a peer GPU's writes into a coarse-grained
+        # buffer are guaranteed visible only at kernel boundaries, so an edge between two
+        # different GPUs refuses it (below, once the peers' devices are known)
+        # (env LSA_IPC_ALLOC=fine / coarse starts from a weaker kind: cost A/B on one GPU only)
+        self.alloc_kinds = {}
+        first = {"uncached": 0, "fine": 1, "coarse": 2}[os.environ.get("LSA_IPC_ALLOC", "uncached")]
+
+        def alloc(nbytes: int, key):
+            ptr, h, kind = ctypes.c_void_p(), ctypes.create_string_buffer(hb), ctypes.c_int(-1)
+            _ok(L.lsa_ipc_alloc(nbytes, ctypes.byref(ptr), h, ctypes.byref(kind), first), "lsa_ipc_alloc")
+            self._own.append(ptr.value)
+            self.alloc_kinds[key] = kind.value
+            mine[key] = h.raw
+            mine[(key, "dev")] = _device_uuid(self.dev)
+            return ptr.value
+
         for e in self.edges:
             if e[1] == rank:
-                ptr, h = ctypes.c_void_p(), ctypes.create_string_buffer(hb)
-                _ok(L.lsa_ipc_alloc(_FLAG_BYTES + self.R * self.slot_bytes, ctypes.byref(ptr), h), "lsa_ipc_alloc")
-                self._own.append(ptr.value)
-                self.inbox[e] = ptr.value
-                mine[(e, "inbox")] = h.raw
+                self.inbox[e] = alloc(_FLAG_BYTES + self.R * self.slot_bytes, (e, "inbox"))
             if e[0] == rank:
-                ptr, h = ctypes.c_void_p(), ctypes.create_string_buffer(hb)
-                _ok(L.lsa_ipc_alloc(_FLAG_BYTES, ctypes.byref(ptr), h), "lsa_ipc_alloc")
-                self._own.append(ptr.value)
-                self.ackbox[e] = ptr.value
-                mine[(e, "acks")] = h.raw
+                self.ackbox[e] = alloc(_FLAG_BYTES, (e, "acks"))
+        for key, kind in self.alloc_kinds.items():
+            mine[("kind", key)] = kind
         if group is None and dist.is_initialized():
             group = dist.new_group(backend="gloo")
         self.group = group
@@ -129,8 +148,10 @@ class IpcRingP2P:
                 self.peer_inbox[e], self.peer_acks[e] = self.inbox[e], self.ackbox[e]
                 continue
             if e[0] == rank:  # sender: map the receiver's inbox
+                self._check_coherent(e, theirs, "inbox")
                 self.peer_inbox[e] = self._open(theirs[(e, "inbox")])
             if e[1] == rank:  # receiver: map the sender's ack box
+                self._check_coherent(e, theirs, "acks")
                 self.peer_acks[e] = self._open(theirs[(e, "acks")])
         # per edge end: {count, ticket, fail}; one error word for every launch of this endpoint. Each edge
         # end issues on its own stream (ordered against the caller's by events), so sends of one
@@ -145,6 +166,18 @@ class IpcRingP2P:
         self.err = torch.zeros(1, dtype=torch.int32, device=self.dev)
         if dist.is_initialized():
             dist.barrier(group=group)  # every mapping is in place before anyone sends
+
+    def _check_coherent(self, e, theirs: dict, what: str) -> None:
+        """An edge between two different GPUs needs its peer-written buffers uncached or
+        fine-grained on BOTH ends (ours: ``alloc_kinds``; theirs: the kind they published)."""
+        other = (e, "acks") if what == "inbox" else (e, "inbox")
+        if theirs.get(((e, what), "dev")) == _device_uuid(self.dev):
+            return  # both ends on one GPU: one L2, coarse-grained memory is coherent
+        kinds = [theirs.get(("kind", (e, what)), 0)]
+        if other in self.alloc_kinds:
+            kinds.append(self.alloc_kinds[other])
+        hip._req(min(kinds) >= 1, f"ipc ring edge {e}: a cross-GPU ring needs uncached / fine-grained buffers, "
+                                  f"got allocation kinds {kinds} (0 = coarse-grained)")
 
     def _open(self, handle: bytes) -> int:
         ptr = ctypes.c_void_p()

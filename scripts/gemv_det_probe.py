@@ -1,0 +1,82 @@
+#!/usr/bin/env python3
+"""Determinism + accuracy of every instantiated decode-GEMV config (gemv.hip LSA_GEMV_CONFIGS):
+EPI_RESID with the fused RMSNorm (N 1024, K 4096), each config launched ``--launches`` times on
+the same inputs at the row counts of its row-block class; every launch must be bit-identical to
+the first and within 8e-3 of fp32. ``--lib PATH`` runs a probe build with the library's C API
+under the symbol ``lsa_gemv_body`` (scripts/probes/gemv_body_lib.hip) instead of the library.
+One JSON line per (config, rows)."""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from llm_sharding_amd.ops import hip, packing  # noqa: E402
+
+ROWS = {1: (1, 16), 2: (17, 32), 4: (33, 44, 64)}
+
+
+def run(lib_path=None, launches=3, n=1024, k=4096, seed=0):
+    L = hip.lib()
+    chk = None
+    fn = L.lsa_gemv
+    if lib_path:
+        P = ctypes.CDLL(lib_path)
+        fn = P.lsa_gemv_body
+        fn.argtypes = L.lsa_gemv.argtypes
+        fn.restype = ctypes.c_int
+        chk = getattr(P, "lsa_gemv_body_chk", None)
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    out_rows = []
+    for (tn, mb, nw, u) in packing.GEMV_CONFIGS:
+        for M in ROWS[mb]:
+            x = torch.randn(M, k, device="cuda", generator=g).to(torch.bfloat16)
+            gam = (1 + 0.1 * torch.randn(k, device="cuda", generator=g)).to(torch.bfloat16)
+            w = (0.02 * torch.randn(n, k, device="cuda", generator=g)).to(torch.bfloat16)
+            resid = torch.randn(M, n, device="cuda", generator=g).to(torch.bfloat16)
+            wp = packing.pack_b(packing.fold_norm(w, gam))
+            xf = x.float()
+            ref = resid.float() + (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-5) * gam.float()) @ w.float().T
+            outs = []
+            for _ in range(launches):
+                out = resid.clone()
+                ep = hip.make_epi(out=out, resid=out, ldo=n, ldr=n)
+                rc = fn(hip._p(x), x.stride(0), None, hip._p(wp), M, n, k, 1, 1e-5, hip.EPI_RESID, ctypes.byref(ep),
+                        tn, nw, u, hip._stream())
+                if rc != 0:
+                    raise RuntimeError(f"gemv rc {rc} at {(tn, mb, nw, u)} M={M}")
+                torch.cuda.synchronize()
+                outs.append(out)
+            errs = [((o.float() - ref).norm() / ref.norm()).item() for o in outs]
+            rowerr = ((outs[0].float() - ref).norm(dim=1) / ref.norm(dim=1))
+            rec = {"cfg": [tn, mb, nw, u], "M": M, "rel_err": max(errs), "worst_row": int(rowerr.argmax()),
+                   "worst_row_err": round(float(rowerr.max()), 5),
+                   "bit_identical": all(torch.equal(outs[0], o) for o in outs[1:])}
+            if chk is not None:
+                flag = ctypes.c_uint(0)
+                chk(ctypes.byref(flag))
+                rec["index_violation_bits"] = flag.value
+            out_rows.append(rec)
+    return out_rows
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--lib", default=None)
+    ap.add_argument("--launches", type=int, default=3)
+    a = ap.parse_args()
+    bad = 0
+    for r in run(a.lib, a.launches):
+        r["lib"] = os.path.basename(a.lib) if a.lib else "liblsa_kernels.so"
+        ok = r["bit_identical"] and r["rel_err"] < 8e-3 and not r.get("index_violation_bits")
+        bad += not ok
+        print(json.dumps(r), flush=True)
+    print(json.dumps({"summary": True, "failed": bad}), flush=True)
+    sys.exit(1 if bad else 0)
+
+
+if __name__ == "__main__":
+    main()

@@ -31,7 +31,7 @@ def main():
     torch.cuda.set_device(a.device)
     from llm_sharding_amd.parallel.ipc_ring import IpcRingP2P
     dev = torch.device("cuda", a.device)
-    R, slot = 3, 1 << 20
+    R, slot = 3, 4 << 20
     p2p = IpcRingP2P(a.rank, slot_bytes=slot, slots=R, timeout_s=20.0)
     peer = 1 - a.rank
     res = {"rank": a.rank, "ok": True}
@@ -41,7 +41,7 @@ def main():
         return torch.randint(-2 ** 31, 2 ** 31 - 1, (n // 4,), generator=g, device=dev, dtype=torch.int32)
 
     # every size a multiple of 4 B, some not of 16 B (the dword-tail path), up to the whole slot
-    sizes = [16 * (1 + (i * 7919) % (slot // 16)) - 4 * (i % 4) for i in range(a.messages)] + [4, 8, slot]
+    sizes = [16 * (1 + (i * 7919) % ((1 << 20) // 16)) - 4 * (i % 4) for i in range(a.messages)] + [4, 8, slot]
     # 1) messages 0 -> 1 in bursts of R (every slot of the ring in flight), echoed back 1 -> 0
     if a.rank == 0:
         outs = [pattern(i, n) for i, n in enumerate(sizes)]
@@ -99,6 +99,23 @@ def main():
     dt = time.perf_counter() - t0
     res["pingpong_ok"] = int(x[0].item()) == a.pingpong
     res["one_way_us"] = round(dt / a.pingpong / 2 * 1e6, 2)
+    # 4) 4 MiB messages (the 512-row Llama-2-7B decode hand-off), one way 0 -> 1, bursts of R
+    big = torch.ones(slot // 4, dtype=torch.int32, device=dev)
+    nbig = 30
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(nbig):  # the sender runs at most R ahead: its kernels wait for the acks in-kernel
+        if a.rank == 0:
+            p2p.isend(big, peer)
+        else:
+            p2p.recv(big, peer)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    res["bulk_4mib_us"] = round(dt / nbig * 1e6, 1)
+    res["bulk_gbps"] = round(slot * nbig / dt / 1e9, 2)
+    res["alloc_kinds"] = sorted(set(p2p.alloc_kinds.values()))
+    res["alloc"] = os.environ.get("LSA_IPC_ALLOC", "uncached")
     p2p.check()
     p2p.close()
     res["ok"] = bool(res["stream_ok"] and res["graph_ok"] and res["pingpong_ok"])

@@ -25,6 +25,18 @@
 #pragma once
 #include "epilogue.h"
 
+#ifdef LSA_GEMV_CHK  // probe build only: range-check every LDS reduction index (gemv_body_lib.hip)
+__device__ unsigned lsa_gemv_chk_flag;
+#define LSA_GCHK(idx, n, bit) \
+  do {                        \
+    if ((unsigned)(idx) >= (unsigned)(n)) atomicOr(&lsa_gemv_chk_flag, (bit)); \
+  } while (0)
+#else
+#define LSA_GCHK(idx, n, bit) \
+  do {                        \
+  } while (0)
+#endif
+
 // WT (EPI_QKV only): the q / k / v outputs leave through 16-B write-through stores (one thread
 // per 16-column tile row, epi_qkv_row16<true>) for an in-launch consumer (scripts/probes/qkv_attn.hip)
 template <int TN, int MB, int NW, int U, int EPI, bool NORM, bool WT = false>
@@ -135,14 +147,22 @@ LSA_DEVICE void gemv_packed_body(const bf16_raw* __restrict__ x, int ldx, const 
     for (int t = 0; t < TN; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        red[((w * TN + t) * MR + rb * 16 + kq * 4 + r) * 16 + (lane & 15)] = acc[rb][t][r];
+      {
+        const int ix = ((w * TN + t) * MR + rb * 16 + kq * 4 + r) * 16 + (lane & 15);
+        LSA_GCHK(ix, NW * TN * MR * 16, 1u);
+        red[ix] = acc[rb][t][r];
+      }
   if (NORM) {
 #pragma unroll
     for (int rb = 0; rb < MB; ++rb) {
       float v = ss[rb];
       v += __shfl_xor(v, 16, 64);
       v += __shfl_xor(v, 32, 64);
-      if (lane < 16) s_ss[w][rb * 16 + lane] = v;
+      if (lane < 16) {
+        LSA_GCHK(w, NW, 2u);
+        LSA_GCHK(rb * 16 + lane, MR, 2u);
+        s_ss[w][rb * 16 + lane] = v;
+      }
     }
   }
   __syncthreads();
@@ -150,14 +170,20 @@ LSA_DEVICE void gemv_packed_body(const bf16_raw* __restrict__ x, int ldx, const 
   auto rsum = [&](int t, int mm, int n) -> float {
     float v = 0.f;
 #pragma unroll
-    for (int i = 0; i < NW; ++i) v += red[((i * TN + t) * MR + mm) * 16 + n];
+    for (int i = 0; i < NW; ++i) {
+      LSA_GCHK(((i * TN + t) * MR + mm) * 16 + n, NW * TN * MR * 16, 4u);
+      v += red[((i * TN + t) * MR + mm) * 16 + n];
+    }
     return v;
   };
   auto rstd = [&](int mm) -> float {
     if (!NORM) return 1.f;
     float t = 0.f;
 #pragma unroll
-    for (int i = 0; i < NW; ++i) t += s_ss[i][mm];
+    for (int i = 0; i < NW; ++i) {
+      LSA_GCHK(mm, MR, 8u);
+      t += s_ss[i][mm];
+    }
     return rsqrtf(t / (float)K + eps);
   };
 

@@ -122,3 +122,48 @@ def test_bench_under_torchrun_supervised():
     assert len(lines) == 1, r.stdout
     line = json.loads(lines[0])
     assert line["n_gpus"] == 2 and line["fallback"] is False and sorted(line["preflight_us"]) == ["0->1", "1->0"]
+
+
+@pytest.mark.parametrize("how", ["sigterm-launcher", "sigkill-supervisor"])
+def test_bench_workers_do_not_outlive_their_supervisor(how):
+    """Killing the launcher (SIGTERM, as a driver timeout or a launcher's killpg would) or a
+    per-rank supervisor outright (SIGKILL: no handler runs) leaves no worker behind: the
+    supervisors forward termination to their workers' process groups, and every child dies with
+    its parent (PR_SET_PDEATHSIG) - the workers run in their own sessions, so nothing else would
+    reach them (advisor round 4)."""
+    import signal
+    import time
+
+    import psutil
+    p = subprocess.Popen([sys.executable, os.path.join(ROOT, "bench.py"), "--device", "cpu", "--gpus", "2",
+                          "--model", "tiny", "--steps", "100000", "--warmup", "1", "--batch", "2",
+                          "--prompt-len", "4", "--latency-steps", "2"], cwd=ROOT, env=_bench_env(),
+                         stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    try:
+        deadline = time.time() + 120
+        workers = []
+        while time.time() < deadline:
+            kids = psutil.Process(p.pid).children(recursive=True)
+            workers = [k for k in kids if _is_worker(k)]
+            if len(workers) == 2:
+                break
+            time.sleep(0.5)
+        assert len(workers) == 2, "the two bench workers did not start"
+        if how == "sigterm-launcher":
+            p.send_signal(signal.SIGTERM)
+        else:
+            workers[0].parent().kill()  # rank's supervisor, SIGKILL
+        gone, alive = psutil.wait_procs(workers, timeout=60)
+        assert not alive, f"workers outlived their supervisor: {[w.pid for w in alive]}"
+    finally:
+        for k in psutil.Process(p.pid).children(recursive=True) if p.poll() is None else []:
+            k.kill()
+        p.kill()
+        p.wait()
+
+
+def _is_worker(proc) -> bool:
+    try:
+        return proc.environ().get("LSA_BENCH_ROLE") == "worker"
+    except Exception:  # noqa: BLE001 - exited meanwhile
+        return False

@@ -1,0 +1,37 @@
+"""Every instantiated decode-GEMV config (csrc/kernels/gemv.hip LSA_GEMV_CONFIGS) launched three
+times on the same inputs - EPI_RESID with the fused RMSNorm, at the row counts of its row-block
+class - is bit-identical across launches and within 8e-3 of the fp32 reference
+(scripts/gemv_det_probe.py; round-4 verdict item 2: a config once computed wrong rows
+nondeterministically when built through a shared device-function body,
+profiles/r4_gemv_body_regression.md)."""
+import os
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def _check(rows):
+    bad = [r for r in rows if not (r["bit_identical"] and r["rel_err"] < 8e-3 and not r.get("index_violation_bits"))]
+    assert not bad, bad
+    return rows
+
+
+def test_gemv_every_config_deterministic_library():
+    from scripts.gemv_det_probe import run
+    rows = _check(run(None, launches=3))
+    assert len({tuple(r["cfg"]) for r in rows}) == 23
+
+
+@pytest.mark.parametrize("variant", ["liblsa_gemv_body.so", "liblsa_gemv_body_chk.so"])
+def test_gemv_every_config_deterministic_shared_body(variant):
+    """The same kernel built through the shared device-function body (probe build, made on the box by
+    scripts/probes/build_gemv_body.sh; skipped where it was not built)."""
+    path = os.path.join(ROOT, "build", "probes", variant)
+    if not os.path.exists(path):
+        pytest.skip(f"{variant} not built (scripts/probes/build_gemv_body.sh)")
+    from scripts.gemv_det_probe import run
+    _check(run(path, launches=3))

@@ -43,8 +43,12 @@ def _run_two(script, *extra):
 def test_ipc_ring_two_processes():
     res = _run_two("ipc_ring_check.py", "--world", "2")
     assert all(r["stream_ok"] and r["graph_ok"] and r["pingpong_ok"] for r in res), res
+    # the peer-written inbox / ack boxes are uncached (kind 2), coherent between GPUs during a
+    # kernel (csrc/kernels/ipc_ring.hip lsa_ipc_alloc), not coarse-grained hipMalloc memory
+    assert all(r["alloc_kinds"] == [2] for r in res), res
     # (both ranks time-share one GPU here, so this is not the xGMI latency between two GPUs)
-    print("ipc ring one-way latency (us):", [r["one_way_us"] for r in res])
+    print("ipc ring one-way latency (us):", [r["one_way_us"] for r in res],
+          "4 MiB message (us):", [r["bulk_4mib_us"] for r in res])
 
 
 @pytest.mark.parametrize("streams", [1, 2])
