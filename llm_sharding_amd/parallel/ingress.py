@@ -24,6 +24,16 @@ class Replies:
         self.verbose = verbose
         self.on_done = on_done
         self.socks: dict = {}
+        # __call__ runs on the serve thread, error() on the listener thread: one lock guards the
+        # socket table and the sends (one PushSocket per reply_to, never two racing creations)
+        self._lock = threading.Lock()
+
+    def _send(self, reply_to: str, payload: bytes) -> None:
+        with self._lock:
+            sock = self.socks.get(reply_to)
+            if sock is None:
+                sock = self.socks[reply_to] = PushSocket(reply_to)
+            sock.send_bytes(payload)
 
     def __call__(self, r, t) -> None:
         if not (t in r.eos_ids or len(r.output_ids) >= r.max_new_tokens):
@@ -35,9 +45,7 @@ class Replies:
         if self.on_done is not None:
             self.on_done(r, text)
         if r.reply_to:
-            if r.reply_to not in self.socks:
-                self.socks[r.reply_to] = PushSocket(r.reply_to)
-            self.socks[r.reply_to].send_bytes(protocol.encode({
+            self._send(r.reply_to, protocol.encode({
                 "request_id": r.rid, "output_ids": list(r.output_ids), "text": text,
                 "ttft_ms": r.ttft_ms, "tpot_ms": r.tpot_ms}))
 
@@ -48,17 +56,16 @@ class Replies:
         if not reply_to:
             return
         try:
-            if reply_to not in self.socks:
-                self.socks[reply_to] = PushSocket(reply_to)
-            self.socks[reply_to].send_bytes(protocol.encode({"request_id": request_id, "error": reason,
-                                                             "output_ids": [], "text": ""}))
+            self._send(reply_to, protocol.encode({"request_id": request_id, "error": reason,
+                                                  "output_ids": [], "text": ""}))
         except OSError as e:
             print(f"[WARNING] error reply to {reply_to} failed: {e}", flush=True)
 
     def close(self) -> None:
-        for s in self.socks.values():
-            s.close(linger_ms=2000)
-        self.socks.clear()
+        with self._lock:
+            for s in self.socks.values():
+                s.close(linger_ms=2000)
+            self.socks.clear()
 
 
 def decode_message(raw: bytes) -> dict:

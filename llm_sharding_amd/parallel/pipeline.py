@@ -152,14 +152,20 @@ def preflight_edges(p2p: "DistP2P", srank: int, pp: int, dev, timeout_s: Optiona
             torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         state["pending"] = f"{prv}->{me} (receive) and {me}->{nxt} (send)"
-        sw = None if fault == (me, nxt) else p2p.isend(out, (srank + 1) % pp)
-        rw = p2p.irecv(inp, (srank - 1) % pp)
-        rw.wait()
-        state["pending"] = f"{me}->{nxt} (send)"
-        if sw is not None:
-            sw.wait()
-        if dev.type == "cuda":
-            torch.cuda.synchronize(dev)
+        try:
+            sw = None if fault == (me, nxt) else p2p.isend(out, (srank + 1) % pp)
+            rw = p2p.irecv(inp, (srank - 1) % pp)
+            rw.wait()
+            state["pending"] = f"{me}->{nxt} (send)"
+            if sw is not None:
+                sw.wait()
+            if dev.type == "cuda":
+                torch.cuda.synchronize(dev)
+        except Exception as e:  # noqa: BLE001 - an edge that FAILS fast is as dead as one that hangs
+            wd.cancel()
+            print(f"[bench] PREFLIGHT FAILED on rank {me}: edge {state['pending']} raised "
+                  f"{type(e).__name__}: {e}; exiting {PREFLIGHT_EXIT}", file=sys.stderr, flush=True)
+            os._exit(PREFLIGHT_EXIT)
         times.append(time.perf_counter() - t0)
         if float(inp[0]) != float(prv * 1000 + it):
             wd.cancel()

@@ -41,6 +41,7 @@ reference default) and mapped to bfloat16 with a notice.
 from __future__ import annotations
 
 import json
+import threading
 import os
 import sys
 import time
@@ -337,10 +338,13 @@ class _StageRef:
         self._ctrl = ctrl
 
     def submit(self, *a, **kw):
-        srv = self._ctrl.server
-        if srv is None:
-            raise ValueError("pipeline dropped (a rank was lost)")
-        return srv.submit(*a, **kw)
+        # under the controller's submit lock: a request either reaches the live server before the
+        # drop starts (and is then answered by the drop's unfinished() sweep) or is rejected here
+        with self._ctrl._submit_lock:
+            srv = self._ctrl.server
+            if srv is None or self._ctrl._aborted or getattr(self._ctrl, "phase", "serving") != "serving":
+                raise ValueError("pipeline dropped (a rank was lost)")
+            return srv.submit(*a, **kw)
 
 
 class NodeController:
@@ -352,6 +356,7 @@ class NodeController:
         self.shards_path = shards_path
         self.device = device
         self.dtype = dtype
+        self._submit_lock = threading.Lock()  # ingress submits vs the pipeline drop (_StageRef)
         self.backend = backend
         self.poll_ms = poll_ms
         self.verbose = verbose
@@ -604,9 +609,11 @@ class NodeController:
             self._abort_timer.cancel()
         dropped = lost is not None or self._aborted
         if dropped:
-            self.phase = "dropping"  # the listener still answers pings and queues early configs
+            with self._submit_lock:  # no submit can slip in between the phase change and the sweep
+                self.phase = "dropping"  # the listener still answers pings and queues early configs
+                pending = self.server.unfinished() if replies is not None else []
             if replies is not None:
-                for r in self.server.unfinished():
+                for r in pending:
                     replies.error(r.reply_to, "pipeline dropped (a rank was lost) before the request finished",
                                   request_id=r.rid)
             self._drop_pipeline(lost or "aborted by the master")

@@ -18,6 +18,7 @@ from llm_sharding_amd.ops import hip, packing  # noqa: E402
 
 DEV = "cuda"
 N_CU = 256
+_RAW = []  # every CU-masked stream this process created: destroyed before exit (destroy_streams)
 
 
 def masked_stream(cus):
@@ -28,7 +29,19 @@ def masked_stream(cus):
     s = ctypes.c_void_p()
     rc = lib.hipExtStreamCreateWithCUMask(ctypes.byref(s), 8, words)
     assert rc == 0, rc
+    _RAW.append(s.value)
     return torch.cuda.ExternalStream(s.value)
+
+
+def destroy_streams():
+    """The streams were created outside torch (ExternalStream does not own them): left alive,
+    the HIP runtime's process-exit teardown raced the profiler's and crashed (SIGSEGV after the
+    last output line under rocprofv3, profiles/r4_attn_gemm_overlap.md). Drain, then destroy."""
+    lib = ctypes.CDLL("libamdhip64.so")
+    torch.cuda.synchronize()
+    while _RAW:
+        rc = lib.hipStreamDestroy(ctypes.c_void_p(_RAW.pop()))
+        assert rc == 0, rc
 
 
 def spread(n, offset=0):
@@ -158,4 +171,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    finally:
+        destroy_streams()

@@ -48,18 +48,29 @@ def model():
     torch.cuda.empty_cache()
 
 
-def _check_tokens(lg, got, tol=0.05):
-    """The engine's greedy token must be near-optimal under the golden logits (its golden logit
-    within ``tol`` x max|logit| of the golden maximum); returns (exact matches, rows). The bf16
-    hidden state is 3.4e-2 off the fp32 golden after 32 layers (rel err, asserted below), so a
-    near-tie may flip by a few % of the largest logit: tol = 0.05 (0.03 held for one GEMV
-    decomposition and failed at 3.3 % when the 64-row qkv projection moved to another
-    k-split order in round 4)."""
+def _check_tokens(lg, got, le, slack=0.01):
+    """The engine's greedy token ``got`` against the golden logits ``lg``, with a bound DERIVED
+    from the measured hidden-state error instead of a constant: ``le`` = the golden fp32 head
+    applied to the ENGINE's final hidden state. For the golden argmax m and the engine's choice c
+    (which its own logits l' rank first: l'[c] >= l'[m]),
+        lg[m] - lg[c] <= (lg[m] - le[m]) + (le[c] - lg[c]) + (le[m] - l'[m]) + (l'[c] - le[c]);
+    the first two terms are measured here, the last two are the engine head's own error on the
+    same hidden state (bf16-folded norm weight, bf16 inputs, fp32 accumulation): bounded by
+    ``slack`` x max|lg| (0.01; the head kernel alone is within 8e-3 rel of fp32 in
+    tests/test_kernels_gpu.py). A wrong in-graph argmax shows as a gap beyond that bound however
+    small the hidden-state error is; the hidden-state error itself is asserted by the caller.
+    Returns (exact matches, rows)."""
     got = got.to(lg.device).long()
-    chosen = lg.gather(1, got[:, None])[:, 0]
-    gap = (lg.max(-1).values - chosen) / lg.abs().amax(-1)
-    assert float(gap.max()) < tol, f"token gaps {gap.tolist()}: engine {got.tolist()} golden {lg.argmax(-1).tolist()}"
-    return int((got == lg.argmax(-1)).sum()), got.numel()
+    m = lg.argmax(-1)
+    lg_c, lg_m = lg.gather(1, got[:, None])[:, 0], lg.gather(1, m[:, None])[:, 0]
+    le_c, le_m = le.gather(1, got[:, None])[:, 0], le.gather(1, m[:, None])[:, 0]
+    scale = lg.abs().amax(-1)
+    gap = lg_m - lg_c
+    bound = (lg_m - le_m) + (le_c - lg_c) + slack * scale
+    assert bool((gap <= bound + 1e-6).all()), (
+        f"token gaps {(gap / scale).tolist()} exceed the derived bound {(bound / scale).tolist()} (x max|logit|): "
+        f"engine {got.tolist()} golden {m.tolist()}")
+    return int((got == m).sum()), got.numel()
 
 
 def _run(cfg, eng, ref, rows, prompt, steps, tol_prefill, tol_step):
@@ -76,7 +87,7 @@ def _run(cfg, eng, ref, rows, prompt, steps, tol_prefill, tol_step):
     assert e0 < tol_prefill, f"prefill rel err {e0:.3e}"
     lg = ref.logits(href[:, -1])
     first = eng.head(h, [r * prompt + prompt - 1 for r in range(rows)])
-    m, n = _check_tokens(lg, first)
+    m, n = _check_tokens(lg, first, ref.logits(h.reshape(rows, prompt, -1)[:, -1].float()))
     dg = DecodeGraph(eng, rows, "full")
     dg.capture()
     errs = []
@@ -88,7 +99,8 @@ def _run(cfg, eng, ref, rows, prompt, steps, tol_prefill, tol_step):
         href = ref.forward_hidden(ref.embed[tok[:, None]])[:, -1]
         errs.append(rel_err(dg.out_hidden, href))
         lg = ref.logits(href)
-        mi, ni = _check_tokens(lg, dg.tokens)  # the step's argmax, written in-graph
+        # the step's argmax, written in-graph
+        mi, ni = _check_tokens(lg, dg.tokens, ref.logits(dg.out_hidden.float().to(href.device)))
         m, n = m + mi, n + ni
     print(f"[full-depth] rows {rows}: prefill rel err {e0:.2e}, decode max {max(errs):.2e} "
           f"last {errs[-1]:.2e}, greedy tokens identical to golden {m}/{n}")
