@@ -35,6 +35,24 @@ __global__ __launch_bounds__(ATT_THR) void attn_split_kernel(
                                     min_chunk, part_o, part_lse, out, ldo, counters, blockIdx.x, blockIdx.y, blockIdx.z);
 }
 
+// Few (row, kv-head) work items (e.g. batch-1 decode: 32 workgroups on 256 CUs), one split: each
+// workgroup's time is its serial chain of dependent HBM round trips (KPI * U keys per trip; 150
+// keys took 3 trips with 4 waves x U 4: 6.4 us per layer, profiles/r4_b1_decode_kernels.txt).
+// 8 waves x U 8 keep 256 keys of one (row, kv head) in flight: one trip up to 256 keys.
+constexpr int ATT_SMALL_NW = 8, ATT_SMALL_U = 8;
+constexpr int ATT_SMALL_MAX_WGS = 128;  // rows * n_kv at or below which the small-grid kernel runs
+
+template <int HD, int G>
+__global__ __launch_bounds__(ATT_SMALL_NW * LSA_WAVE) void attn_small_kernel(
+    const bf16_raw* __restrict__ q, int ldq, const bf16_raw* __restrict__ kc,
+    const bf16_raw* __restrict__ vc, const int* __restrict__ slot, const int* __restrict__ pos,
+    const int* __restrict__ kv_len, int n_heads, int n_kv, int t_max, float scale_log2,
+    bf16_raw* __restrict__ out, int ldo) {
+  attn_split_body<HD, G, ATT_SMALL_U, 0, 1, false, ATT_SMALL_NW>(q, ldq, kc, vc, slot, pos, kv_len, n_heads, n_kv,
+                                                               t_max, scale_log2, 1, 1, nullptr, nullptr, out, ldo,
+                                                               nullptr, 0, blockIdx.y, blockIdx.z);
+}
+
 // U = 4 key groups in flight, non-temporal K/V loads (each cache line is read once per step;
 // 512 x 143-token 7B decode: 5.95 -> 6.79 TB/s over the plain-load / other-U variants,
 // profiles/r2_attn_decode_variants.jsonl)
@@ -44,6 +62,14 @@ int launch_split(const bf16_raw* q, int ldq, const bf16_raw* kc, const bf16_raw*
                  float scale_log2, int nsplit, int min_chunk, float* po, float* pl, bf16_raw* out,
                  int ldo, unsigned* cnt, hipStream_t s) {
   dim3 grid(nsplit, n_kv, rows);
+  if constexpr (G <= 4) {  // (G 6 / 8 would spill at U 8: the GQA models' batch-1 keeps the 4-wave kernel)
+    if (nsplit == 1 && rows * n_kv <= ATT_SMALL_MAX_WGS) {
+      attn_small_kernel<HD, G><<<grid, ATT_SMALL_NW * LSA_WAVE, 0, s>>>(q, ldq, kc, vc, slot, pos, kv_len, n_heads,
+                                                                        n_kv, t_max, scale_log2, out, ldo);
+      LSA_CHECK_LAUNCH();
+      return LSA_OK;
+    }
+  }
   attn_split_kernel<HD, G, 4, 0, 1><<<grid, ATT_THR, 0, s>>>(q, ldq, kc, vc, slot, pos, kv_len, n_heads, n_kv, t_max,
                                                              scale_log2, nsplit, min_chunk, po, pl, out, ldo, cnt);
   LSA_CHECK_LAUNCH();

@@ -14,7 +14,10 @@ constexpr int ATT_MAX_SPLIT = 16;  // split-KV factor limit (the merge keeps one
 // K/V loads issued before this one's math); NT: non-temporal K/V loads
 // SPLIT = false: the caller guarantees nsplit == 1 (one workgroup per (row, kv head), output
 // written directly); the partial / merge code is then not compiled in at all.
-template <int HD, int G, int U = 4, int PF = 0, int NT = 0, bool SPLIT = true>
+// NW: waves per workgroup (the caller launches NW * 64 threads). Few (row, kv-head) work items
+// (batch-1 decode: 32 workgroups for the whole chip) are latency-bound - one dependent HBM round
+// trip per KPI * U keys - so that case takes 8 waves x U 8 = 256 keys per round trip (attention.hip).
+template <int HD, int G, int U = 4, int PF = 0, int NT = 0, bool SPLIT = true, int NW = ATT_WAVES>
 LSA_DEVICE void attn_split_body(
     const bf16_raw* __restrict__ q, int ldq, const bf16_raw* __restrict__ kc,
     const bf16_raw* __restrict__ vc, const int* __restrict__ slot, const int* __restrict__ pos,
@@ -23,11 +26,12 @@ LSA_DEVICE void attn_split_body(
     bf16_raw* __restrict__ out, int ldo, unsigned* __restrict__ counters, int split, int kvh, int row) {
   constexpr int LPK = HD / 8;          // lanes per key row (8 bf16 = 16 B per lane)
   constexpr int KPW = LSA_WAVE / LPK;  // keys per wave-instruction
-  constexpr int KPI = KPW * ATT_WAVES; // keys per workgroup iteration
+  constexpr int KPI = KPW * NW;        // keys per workgroup iteration
+  constexpr int NTHR = NW * LSA_WAVE;
 
-  __shared__ float s_m[ATT_WAVES][G];
-  __shared__ float s_l[ATT_WAVES][G];
-  __shared__ float s_o[ATT_WAVES][G][HD];
+  __shared__ float s_m[NW][G];
+  __shared__ float s_l[NW][G];
+  __shared__ float s_o[NW][G][HD];
   __shared__ int s_last;
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -50,7 +54,7 @@ LSA_DEVICE void attn_split_body(
   const size_t pbase0 = pbase - split;  // split 0 of head 0 of this group
   // last-arriver merge of the nsplit partials of this (row, kv-head) group (sc1 loads)
   auto combine = [&]() {
-    for (int e = tid; e < G * HD; e += ATT_THR) {
+    for (int e = tid; e < G * HD; e += NTHR) {
       const int r = e / HD, d = e - r * HD;
       const int hb = (int)(pbase0 + (size_t)r * nsplit);  // index of split 0 of head r
       float lse[ATT_MAX_SPLIT];
@@ -208,14 +212,14 @@ LSA_DEVICE void attn_split_body(
     }
   }
   __syncthreads();
-  for (int e = tid; e < G * HD; e += ATT_THR) {
+  for (int e = tid; e < G * HD; e += NTHR) {
     const int r = e / HD, d = e - r * HD;
     float mm = s_m[0][r];
 #pragma unroll
-    for (int i = 1; i < ATT_WAVES; ++i) mm = fmaxf(mm, s_m[i][r]);
+    for (int i = 1; i < NW; ++i) mm = fmaxf(mm, s_m[i][r]);
     float ls = 0.f, os = 0.f;
 #pragma unroll
-    for (int i = 0; i < ATT_WAVES; ++i) {
+    for (int i = 0; i < NW; ++i) {
       const float a = __builtin_amdgcn_exp2f(s_m[i][r] - mm);
       ls += s_l[i][r] * a;
       os += s_o[i][r][d] * a;

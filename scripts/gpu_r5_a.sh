@@ -27,6 +27,12 @@ for alloc in uncached coarse; do
 done
 timeout -k 10 400 python3 bench.py --steps 20 --warmup 5 > $out/bench.log 2>&1 || { tail -20 $out/bench.log; exit 4; }
 grep '^{' $out/bench.log | tail -1
+timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d $out/prof_b1 -o run -- \
+    python3 -u bench.py --steps 4 --warmup 2 --latency-steps 32 --mid-batch 0 > $out/prof_b1.log 2>&1 || { tail -20 $out/prof_b1.log; exit 6; }
+f=$(find $out/prof_b1 -name "*kernel_trace.csv" | head -1)
+python3 scripts/kstats.py "$f" flash_prefill 14 > $out/kstats_b1.txt
+head -10 $out/kstats_b1.txt
+rm -f "$f"
 timeout -s KILL 60 rocprofv3 -L > $out/counters_list.txt 2>&1 || true
 P="python3 scripts/gemm_pmc_probe.py --rows 512 --launches 6"
 timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d $out/kt -o run -- $P > $out/probe_kt.log 2>&1 \

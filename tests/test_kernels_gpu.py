@@ -332,6 +332,28 @@ def test_attention_split(nh, nkv, hd, nsplit):
     assert rel_err(out, ref) < 1e-2
 
 
+@pytest.mark.parametrize("nh,nkv,hd", [(32, 32, 128), (24, 8, 128), (8, 2, 64)])
+@pytest.mark.parametrize("rows", [1, 3])
+def test_attention_small_grid(nh, nkv, hd, rows):
+    """rows * n_kv <= 128 with one split: the 8-wave, 256-keys-per-round-trip kernel
+    (attention.hip attn_small_kernel) - contexts of 1, 150 (one trip), 256, 257 (two) and 1100
+    keys against fp32; the explicit kv_len form too."""
+    h = hip()
+    slots, T = 3, 1100
+    q = _rnd(rows, nh * hd)
+    kc, vc = _rnd(slots, nkv, T, hd), _rnd(slots, nkv, T, hd)
+    for pos_list in ([0, 149, 1099], [255, 256, 600]):
+        slot = torch.tensor([0, 1, 2][:rows], dtype=torch.int32, device=DEV)
+        pos = torch.tensor(pos_list[:rows], dtype=torch.int32, device=DEV)
+        out = torch.zeros(rows, nh * hd, dtype=torch.bfloat16, device=DEV)
+        po, pl = torch.zeros(rows * nh * hd, device=DEV), torch.zeros(rows * nh, device=DEV)
+        h.attn(q, kc, vc, slot, pos, rows, nh, nkv, hd, 1, po, pl, out)
+        assert rel_err(out, _attn_ref(q, kc, vc, slot, pos + 1, nh, nkv, hd)) < 1e-2, pos_list
+        kvl = pos // 2 + 1
+        h.attn(q, kc, vc, slot, pos, rows, nh, nkv, hd, 1, po, pl, out, kv_len=kvl)
+        assert rel_err(out, _attn_ref(q, kc, vc, slot, kvl, nh, nkv, hd)) < 1e-2, pos_list
+
+
 def test_attention_kvlen_override():
     h = hip()
     nh, nkv, hd, rows, T = 8, 8, 128, 4, 64
