@@ -57,8 +57,16 @@ def build(force: bool = False, jobs: int = 8, arch: str = "gfx950", verbose: boo
     hipcc = _hipcc()
     kernel_srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
     comm_srcs = sorted(glob.glob(os.path.join(CSRC, "comm", "*.cpp")))
+    # -fno-slp-vectorize: no packed-FP32 VALU formed from scalar code. ROCm 7.2's hipcc issued a
+    # v_pk_fma_f32 right behind the 32-bit VALU writes of its source pair with no wait state, and
+    # that kernel computed wrong rows nondeterministically on MI355X (profiles/r5_gemv_nondeterminism.md);
+    # csrc/isa_audit.py checks the linked library for the pattern after every build.
     hip_flags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={arch}", "-Wall",
-                 "-Wno-unused-function", "-munsafe-fp-atomics"]
+                 "-Wno-unused-function", "-munsafe-fp-atomics", "-fno-slp-vectorize"]
+    # a change of the compile flags rebuilds every object (the flags are part of the stamp)
+    stamp = os.path.join(OBJ, "hip_flags.txt")
+    if (open(stamp).read() if os.path.exists(stamp) else "") != " ".join(hip_flags):
+        force = True
     jobs_list = []
     kobjs = []
     for s in kernel_srcs:
@@ -88,6 +96,18 @@ def build(force: bool = False, jobs: int = 8, arch: str = "gfx950", verbose: boo
         _run([hipcc, "-shared", "-fPIC", f"--offload-arch={arch}", *kobjs, "-o", klib])
         with open(manifest, "w") as f:
             f.write("\n".join(kobjs))
+    with open(stamp, "w") as f:
+        f.write(" ".join(hip_flags))
+    audit_stamp = os.path.join(OBJ, "isa_audit.ok")
+    if not os.path.exists(audit_stamp) or os.path.getmtime(audit_stamp) < os.path.getmtime(klib):
+        sys.path.insert(0, CSRC)
+        from isa_audit import audit  # csrc/isa_audit.py
+        res = audit(klib)
+        if res["findings"]:
+            raise RuntimeError(f"ISA audit of {klib}: {len(res['findings'])} VALU -> packed-FP32 back-to-back "
+                               f"dependencies, e.g. {res['findings'][:3]} (csrc/isa_audit.py)")
+        with open(audit_stamp, "w") as f:
+            f.write(f"{res['code_objects']} code objects, {res['packed_fp32_instructions']} packed FP32, 0 findings\n")
     out["kernels"] = klib
     clib = os.path.join(OUT, "liblsa_comm.so")
     if cobjs and (force or not os.path.exists(clib) or

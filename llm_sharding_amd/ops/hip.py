@@ -21,7 +21,9 @@ from typing import Optional, Tuple
 import torch
 
 NATIVE_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_native")
-KERNELS_SO = os.path.join(NATIVE_DIR, "liblsa_kernels.so")
+# LSA_KERNELS_SO: load another build of the kernel library (A/B runs of build flags only; the
+# product and every test use the in-tree _native/liblsa_kernels.so)
+KERNELS_SO = os.environ.get("LSA_KERNELS_SO") or os.path.join(NATIVE_DIR, "liblsa_kernels.so")
 
 EPI_STORE, EPI_RESID, EPI_SWIGLU, EPI_QKV, EPI_ARGMAX, EPI_PARTIAL = range(6)
 _STATUS = {0: "ok", 1: "bad shape", 2: "unsupported", 3: "launch failed"}

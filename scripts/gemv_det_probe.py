@@ -19,7 +19,7 @@ from llm_sharding_amd.ops import hip, packing  # noqa: E402
 ROWS = {1: (1, 16), 2: (17, 32), 4: (33, 44, 64)}
 
 
-def run(lib_path=None, launches=3, n=1024, k=4096, seed=0):
+def run(lib_path=None, launches=3, n=1024, k=4096, seed=0, only=None):
     L = hip.lib()
     chk = None
     fn = L.lsa_gemv
@@ -32,6 +32,8 @@ def run(lib_path=None, launches=3, n=1024, k=4096, seed=0):
     g = torch.Generator(device="cuda").manual_seed(seed)
     out_rows = []
     for (tn, mb, nw, u) in packing.GEMV_CONFIGS:
+        if only and (tn, mb, nw, u) != only:
+            continue
         for M in ROWS[mb]:
             x = torch.randn(M, k, device="cuda", generator=g).to(torch.bfloat16)
             gam = (1 + 0.1 * torch.randn(k, device="cuda", generator=g)).to(torch.bfloat16)
@@ -67,9 +69,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--lib", default=None)
     ap.add_argument("--launches", type=int, default=3)
+    ap.add_argument("--only", default="", help="tn,mb,nw,u: one config")
     a = ap.parse_args()
+    only = tuple(int(v) for v in a.only.split(",")) if a.only else None
     bad = 0
-    for r in run(a.lib, a.launches):
+    for r in run(a.lib, a.launches, only=only):
         r["lib"] = os.path.basename(a.lib) if a.lib else "liblsa_kernels.so"
         ok = r["bit_identical"] and r["rel_err"] < 8e-3 and not r.get("index_violation_bits")
         bad += not ok

@@ -9,12 +9,12 @@ out=gpurun_out/${LSA_OUT:-r5_a}
 mkdir -p $out
 rm -rf $out/*
 bash scripts/probes/build_gemv_body.sh > $out/probe_build.log 2>&1 || { tail -20 $out/probe_build.log; exit 1; }
-timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread -p no:cacheprovider \
+timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread -p no:cacheprovider \
     > $out/pytest.log 2>&1
 rc=$?
 tail -15 $out/pytest.log
 grep -q "Timeout\|Fatal Python\|core dumped" $out/pytest.log && exit 2
-[ $rc -eq 0 ] || exit 2
+[ $rc -le 1 ] || exit 2  # test failures (1) are read afterwards; anything else stops here
 for alloc in uncached coarse; do
   port=$((29600 + RANDOM % 1000))
   (LSA_IPC_ALLOC=$alloc timeout -k 10 120 python3 scripts/ipc_ring_check.py --rank 1 --port $port > $out/ipc_${alloc}_r1.log 2>&1) &

@@ -4,11 +4,15 @@ included, until the (block, in-flight loads) state repeats) and report any instr
 VGPR / AGPR whose vector-memory load may still be in flight (not yet covered by an s_waitcnt
 vmcnt(N) that retires it). Loads, stores and LDS-DMA count together in vmcnt, in issue order.
 
+LGKM=1 in the environment checks the LDS / scalar-memory counter instead (ds_read*, ds_bpermute,
+ds_*_rtn, s_load*, s_buffer_load*; a scalar load in flight makes only lgkmcnt(0) a safe wait, so
+any wait above 0 retires none of the scalar loads).
+
 usage: vmcnt_check.py FILE.s [kernel-symbol-substring]"""
 import re
 import sys
 
-REG = re.compile(r"\b([va])(?:\[(\d+):(\d+)\]|(\d+))\b")
+REG = re.compile(r"\b([va])(?:\[(\d+):(\d+)\]|(\d+)\b)")
 
 
 def regs(tok: str):
@@ -37,8 +41,34 @@ def parse(lines):
     return insts, labels
 
 
+LGKM = __import__("os").environ.get("LGKM") == "1"
+
+
 def classify(s: str):
     op = s.split()[0]
+    if LGKM:
+        rest = s[len(op):].strip()
+        ops = [o.strip() for o in rest.split(",")] if rest else []
+        ev = op.startswith(("ds_read", "ds_bpermute", "ds_permute", "s_load", "s_buffer_load")) or (
+            op.startswith("ds_") and "_rtn" in op)
+        dst, srcs = set(), set()
+        if ev:
+            dst = regs(ops[0]) if ops else set()
+            if op.startswith("s_"):
+                dst = {("s", 0)}  # marker: scalar load in flight
+            for o in ops[1:]:
+                srcs |= regs(o)
+        elif op.startswith("s_"):
+            pass
+        else:
+            if ops and not op.startswith(("ds_write", "global_store", "buffer_store")):
+                dst = regs(ops[0])
+                for o in ops[1:]:
+                    srcs |= regs(o)
+            else:
+                for o in ops:
+                    srcs |= regs(o)
+        return op, ev, dst, srcs
     rest = s[len(op):].strip()
     ops = [o.strip() for o in rest.split(",")] if rest else []
     is_vm = op.startswith(("global_", "buffer_", "flat_", "scratch_")) and "wbl2" not in op and "inv" not in op
@@ -104,10 +134,13 @@ def main():
                     break
                 no, s = insts[pc]
                 op, is_vm, dst, srcs = info[pc]
-                m = re.search(r"vmcnt\((\d+)\)", s)
+                m = re.search(r"lgkmcnt\((\d+)\)" if LGKM else r"vmcnt\((\d+)\)", s)
                 if op == "s_waitcnt" and m:
                     n = int(m.group(1))
-                    pend = pend[len(pend) - n:] if n < len(pend) else pend
+                    if LGKM and n > 0 and any(("s", 0) in d for _, d in pend):
+                        pass  # scalar loads return out of order: only lgkmcnt(0) retires them
+                    else:
+                        pend = pend[len(pend) - n:] if n < len(pend) else pend
                     if n == 0:
                         pend = ()
                 pending_regs = {}

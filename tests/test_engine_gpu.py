@@ -132,6 +132,20 @@ def test_decode_coop_partials_vs_golden(rows, monkeypatch):
     _big_batch_vs_golden(rows)
 
 
+def test_decode_gemm_path_below_128_rows_vs_golden(monkeypatch):
+    """LSA_GEMV_MAX_ROWS below 128 (StageEngine.GEMV_MAX_ROWS) sends 65..128-row decode batches
+    through the MFMA GEMM path (fused ss, gemm_sk / gemm_wr) inside the captured graph instead of
+    the cooperative GEMV: 96 rows with the limit at 64, against the fp32 golden model (advisor
+    round 4)."""
+    from llm_sharding_amd.ops import hip
+    monkeypatch.setattr(StageEngine, "GEMV_MAX_ROWS", 64)
+    calls = []
+    real = hip.gemm
+    monkeypatch.setattr(hip, "gemm", lambda *a, **k: (calls.append(a[2]), real(*a, **k)))
+    _big_batch_vs_golden(96)
+    assert 96 in calls  # the decode step's projections ran on the GEMM path
+
+
 def _big_batch_vs_golden(rows):
     cfg = _mid_cfg()
     seed, P = 13, 5
