@@ -26,6 +26,8 @@
 //    vectorised row16 epilogues of epilogue.h (16-B stores).
 #include "epilogue.h"
 
+#include <type_traits>
+
 namespace {
 
 constexpr int BK = 64, NTHR = 512;
@@ -178,6 +180,22 @@ struct Kern {
     for (int s = 0; s < BGL; ++s)
       if (s < BGL_LO || w < BHI_WAVES) glds16_w(base + boff[nh][s], dst + (s * 8 + w) * 1024);
   }
+  // the same for a wave group known at compile time (HI: a wave w < BHI_WAVES, which issues
+  // BGL B blocks per region; else BGL_LO): the main loop is instantiated per group, so neither
+  // the DMA issue nor the counted waits branch on the wave id inside it
+  template <bool HI>
+  LSA_DEVICE void stage_b_g(int buf, int nh, const unsigned (&boff)[2][BGL], int kt) {
+    unsigned char* dst = smem + buf * BUF + 2 * AREG + nh * BREG;
+    const unsigned char* base = b_seg + (size_t)kt * 2048;
+    if constexpr (LSA_SK_ABLATE == 7) return;
+#pragma unroll
+    for (int s = 0; s < BGL; ++s)
+      if (s < BGL_LO || HI) glds16_w(base + boff[nh][s], dst + (s * 8 + w) * 1024);
+  }
+  template <bool HI>
+  LSA_DEVICE void wait_tile_g() {
+    vm_wait<(HI ? NPT : NPT_LO)>();
+  }
   // counted wait keeping one K-tile of this wave's DMA in flight (+ EXTRA instructions)
   template <int EXTRA = 0>
   LSA_DEVICE void wait_tile() {
@@ -303,62 +321,88 @@ struct Kern {
       __builtin_amdgcn_s_setprio(0);
     };
 
-    if (NB == 2) {
-      // 2 buffers: RB1/RA1 of tile t+1 go into the other buffer, RA0/RB0 of tile t+2 into this
-      // one right after their last reads; each region lands 5-6 phases after its DMA issue and
-      // the counted wait keeps one K-tile of DMA in flight
-      for (int t = 0; t < n; ++t) {
-        const int cur = t & 1, nxt = cur ^ 1;
-        rd_a(cur, 0);
-        rd_b(cur, 0, b0);
-        if (t + 1 < n) { stage_b(nxt, 1, boff, t + 1); wait_tile(); } else vm_wait<0>();
-        loop_barrier();
-        mma(0, b0, 0);
-        loop_barrier();
-        rd_b(cur, 1, b1);
-        if (t + 1 < n) { stage_a(nxt, 1, aoff, t + 1); wait_tile(); } else vm_wait<0>();
-        loop_barrier();
-        mma(0, b1, 1);
-        loop_barrier();
-        rd_a(cur, 1);
-        if (t + 2 < n) { stage_a(cur, 0, aoff, t + 2); wait_tile(); } else vm_wait<0>();
-        loop_barrier();
-        mma(1, b1, 1);
-        loop_barrier();
-        if (t + 2 < n) { stage_b(cur, 0, boff, t + 2); wait_tile(); } else vm_wait<0>();
-        loop_barrier();
-        mma(1, b0, 0);
-        loop_barrier();
+    // The main loop with every condition resolved at compile time: the K-tiles that stage both
+    // later tiles (t + 2 < n), the one that stages only t + 1, and the last one are separate
+    // instantiations of the same tile body (same stages, waits and barriers in the same order
+    // as one loop with run-time tests - 18 branches and ~60 scalar instructions per K-tile
+    // fewer, profiles/r5_gemm_pmc.md), and the body is instantiated per wave group
+    const std::true_type T_{};
+    const std::false_type F_{};
+    auto main_loop = [&](auto hi_c) {
+      constexpr bool HI = decltype(hi_c)::value;
+      if constexpr (NB == 2) {
+        // 2 buffers: RB1/RA1 of tile t+1 go into the other buffer, RA0/RB0 of tile t+2 into this
+        // one right after their last reads; each region lands 5-6 phases after its DMA issue and
+        // the counted wait keeps one K-tile of DMA in flight
+        auto body = [&](int t, auto s1_c, auto s2_c) {
+          constexpr bool S1 = decltype(s1_c)::value, S2 = decltype(s2_c)::value;
+          const int cur = t & 1, nxt = cur ^ 1;
+          rd_a(cur, 0);
+          rd_b(cur, 0, b0);
+          if constexpr (S1) { stage_b_g<HI>(nxt, 1, boff, t + 1); wait_tile_g<HI>(); } else vm_wait<0>();
+          loop_barrier();
+          mma(0, b0, 0);
+          loop_barrier();
+          rd_b(cur, 1, b1);
+          if constexpr (S1) { stage_a(nxt, 1, aoff, t + 1); wait_tile_g<HI>(); } else vm_wait<0>();
+          loop_barrier();
+          mma(0, b1, 1);
+          loop_barrier();
+          rd_a(cur, 1);
+          if constexpr (S2) { stage_a(cur, 0, aoff, t + 2); wait_tile_g<HI>(); } else vm_wait<0>();
+          loop_barrier();
+          mma(1, b1, 1);
+          loop_barrier();
+          if constexpr (S2) { stage_b_g<HI>(cur, 0, boff, t + 2); wait_tile_g<HI>(); } else vm_wait<0>();
+          loop_barrier();
+          mma(1, b0, 0);
+          loop_barrier();
+        };
+        int t = 0;
+        for (; t + 2 < n; ++t) body(t, T_, T_);
+        if (t + 1 < n) {
+          body(t, T_, F_);
+          ++t;
+        }
+        body(t, F_, F_);
+      } else {
+        // 3 buffers: tile t+2 is staged during tile t into the buffer tile t-1 used, in read
+        // order; the counted wait keeps the last 6 phases of DMA (~1.5 K-tiles) in flight
+        int cur = 0, nx2 = 2;
+        auto body = [&](int t, auto st_c) {
+          constexpr bool ST = decltype(st_c)::value;
+          rd_a(cur, 0);
+          rd_b(cur, 0, b0);
+          if constexpr (ST) { stage_a(nx2, 0, aoff, t + 2); vm_wait<NPT + 2 * AGL>(); } else vm_wait<0>();
+          loop_barrier();
+          mma(0, b0, 0);
+          loop_barrier();
+          rd_b(cur, 1, b1);
+          if constexpr (ST) { stage_b_g<true>(nx2, 0, boff, t + 2); vm_wait<NPT + AGL + BGL>(); } else vm_wait<0>();
+          loop_barrier();
+          mma(0, b1, 1);
+          loop_barrier();
+          rd_a(cur, 1);
+          if constexpr (ST) { stage_b_g<true>(nx2, 1, boff, t + 2); vm_wait<NPT + 2 * BGL>(); } else vm_wait<0>();
+          loop_barrier();
+          mma(1, b1, 1);
+          loop_barrier();
+          if constexpr (ST) { stage_a(nx2, 1, aoff, t + 2); vm_wait<NPT + AGL + BGL>(); } else vm_wait<0>();
+          loop_barrier();
+          mma(1, b0, 0);
+          loop_barrier();
+          cur = cur == 2 ? 0 : cur + 1;
+          nx2 = nx2 == 2 ? 0 : nx2 + 1;
+        };
+        int t = 0;
+        for (; t + 2 < n; ++t) body(t, T_);
+        for (; t < n; ++t) body(t, F_);
       }
+    };
+    if constexpr (NPT == NPT_LO) {
+      main_loop(T_);
     } else {
-      // 3 buffers: tile t+2 is staged during tile t into the buffer tile t-1 used, in read
-      // order; the counted wait keeps the last 6 phases of DMA (~1.5 K-tiles) in flight
-      int cur = 0, nx2 = 2;
-      for (int t = 0; t < n; ++t) {
-        const bool st = t + 2 < n;
-        rd_a(cur, 0);
-        rd_b(cur, 0, b0);
-        if (st) { stage_a(nx2, 0, aoff, t + 2); vm_wait<NPT + 2 * AGL>(); } else vm_wait<0>();
-        loop_barrier();
-        mma(0, b0, 0);
-        loop_barrier();
-        rd_b(cur, 1, b1);
-        if (st) { stage_b(nx2, 0, boff, t + 2); vm_wait<NPT + AGL + BGL>(); } else vm_wait<0>();
-        loop_barrier();
-        mma(0, b1, 1);
-        loop_barrier();
-        rd_a(cur, 1);
-        if (st) { stage_b(nx2, 1, boff, t + 2); vm_wait<NPT + 2 * BGL>(); } else vm_wait<0>();
-        loop_barrier();
-        mma(1, b1, 1);
-        loop_barrier();
-        if (st) { stage_a(nx2, 1, aoff, t + 2); vm_wait<NPT + AGL + BGL>(); } else vm_wait<0>();
-        loop_barrier();
-        mma(1, b0, 0);
-        loop_barrier();
-        cur = cur == 2 ? 0 : cur + 1;
-        nx2 = nx2 == 2 ? 0 : nx2 + 1;
-      }
+      if (w < BHI_WAVES) main_loop(T_); else main_loop(F_);
     }
     if (!group) barrier();  // re-align the two wave groups; every LDS read has retired
   }
