@@ -40,7 +40,7 @@ __global__ __launch_bounds__(ATT_THR) void attn_split_kernel(
 // keys took 3 trips with 4 waves x U 4: 6.4 us per layer, profiles/r4_b1_decode_kernels.txt).
 // 8 waves x U 8 keep 256 keys of one (row, kv head) in flight: one trip up to 256 keys.
 constexpr int ATT_SMALL_NW = 8, ATT_SMALL_U = 8;
-constexpr int ATT_SMALL_MAX_WGS = 128;  // rows * n_kv at or below which the small-grid kernel runs
+int g_att_small_max_wgs = 128;  // rows * n_kv at or below which the small-grid kernel runs (lsa_attn_set_small_max_wgs)
 
 template <int HD, int G>
 __global__ __launch_bounds__(ATT_SMALL_NW * LSA_WAVE) void attn_small_kernel(
@@ -63,7 +63,7 @@ int launch_split(const bf16_raw* q, int ldq, const bf16_raw* kc, const bf16_raw*
                  int ldo, unsigned* cnt, hipStream_t s) {
   dim3 grid(nsplit, n_kv, rows);
   if constexpr (G <= 4) {  // (G 6 / 8 would spill at U 8: the GQA models' batch-1 keeps the 4-wave kernel)
-    if (nsplit == 1 && rows * n_kv <= ATT_SMALL_MAX_WGS) {
+    if (nsplit == 1 && rows * n_kv <= g_att_small_max_wgs) {
       attn_small_kernel<HD, G><<<grid, ATT_SMALL_NW * LSA_WAVE, 0, s>>>(q, ldq, kc, vc, slot, pos, kv_len, n_heads,
                                                                         n_kv, t_max, scale_log2, out, ldo);
       LSA_CHECK_LAUNCH();
@@ -91,6 +91,13 @@ int dispatch_g(int g, const bf16_raw* q, int ldq, const bf16_raw* kc, const bf16
 }
 
 }  // namespace
+
+// Host-side switch of the small-grid kernel's range (A/B runs; default 128 work items).
+extern "C" int lsa_attn_set_small_max_wgs(int n) {
+  if (n < 0) return LSA_BAD_SHAPE;
+  g_att_small_max_wgs = n;
+  return LSA_OK;
+}
 
 extern "C" int lsa_attn_decode(const void* q, int ldq, const void* k_cache, const void* v_cache,
                                const int* slot, const int* pos, const int* kv_len, int rows,

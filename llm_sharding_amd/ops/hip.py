@@ -83,6 +83,9 @@ def lib() -> ctypes.CDLL:
                  "lsa_resid_rmsnorm_partials", "lsa_row_ss",
                  "lsa_argmax_finalize", "lsa_pos_advance", "lsa_version"):
         getattr(L, name).restype = ctypes.c_int
+    if os.environ.get("LSA_ATTN_SMALL_MAX_WGS"):  # A/B runs of the small-grid decode attention's range
+        L.lsa_attn_set_small_max_wgs.argtypes = [i]
+        _check(L.lsa_attn_set_small_max_wgs(int(os.environ["LSA_ATTN_SMALL_MAX_WGS"])), "lsa_attn_set_small_max_wgs")
     _lib = L
     return L
 
