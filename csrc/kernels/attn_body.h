@@ -5,6 +5,8 @@
 #pragma once
 #include "common.h"
 
+#include <type_traits>
+
 constexpr int ATT_WAVES = 4;
 constexpr int ATT_THR = ATT_WAVES * LSA_WAVE;
 constexpr float NEG_BIG = -1e30f;
@@ -150,8 +152,7 @@ LSA_DEVICE void attn_split_body(
         float d = 0.f;
 #pragma unroll
         for (int j = 0; j < 8; ++j) d += qf[r][j] * kf[j];
-#pragma unroll
-        for (int off = LPK / 2; off > 0; off >>= 1) d += __shfl_xor(d, off, 64);
+        d = group_sum<LPK>(d);  // the key's LPK lanes (DPP; common.h)
         s[r][u] = valid[u] ? d : NEG_BIG;
       }
     }
@@ -185,21 +186,26 @@ LSA_DEVICE void attn_split_body(
     }
   }
 
-  // merge the KPW key-groups of this wave (same li, different grp)
-#pragma unroll
-  for (int off = LPK; off < LSA_WAVE; off <<= 1) {
+  // merge the KPW key-groups of this wave (same li, different grp): lane ^ LPK ... ^ 32 on DPP /
+  // permlane swaps (common.h lane_xor), no LDS crossbar round trips
+  auto merge_groups = [&](auto offc) {
+    constexpr int OFF = decltype(offc)::value;
 #pragma unroll
     for (int r = 0; r < G; ++r) {
-      const float mo = __shfl_xor(mx[r], off, 64);
-      const float lo = __shfl_xor(l[r], off, 64);
+      const float mo = lane_xor<OFF>(mx[r]);
+      const float lo = lane_xor<OFF>(l[r]);
       const float mn = fmaxf(mx[r], mo);
       const float a = __builtin_amdgcn_exp2f(mx[r] - mn), b = __builtin_amdgcn_exp2f(mo - mn);
       l[r] = l[r] * a + lo * b;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[r][j] = o[r][j] * a + __shfl_xor(o[r][j], off, 64) * b;
+      for (int j = 0; j < 8; ++j) o[r][j] = o[r][j] * a + lane_xor<OFF>(o[r][j]) * b;
       mx[r] = mn;
     }
-  }
+  };
+  static_assert(LPK == 8 || LPK == 16, "key lane groups");
+  if constexpr (LPK == 8) merge_groups(std::integral_constant<int, 8>{});
+  merge_groups(std::integral_constant<int, 16>{});
+  merge_groups(std::integral_constant<int, 32>{});
   if (grp == 0) {
 #pragma unroll
     for (int r = 0; r < G; ++r) {

@@ -67,6 +67,44 @@ LSA_DEVICE T wave_sum(T v) {
   return v;
 }
 
+// Sum over every aligned group of W (8 or 16) lanes, every lane receiving its group's total, on
+// DPP lane moves (quad_perm [1,0,3,2] / [2,3,0,1], row_half_mirror, row_mirror): VALU ops
+// instead of the ds_bpermute round trips through the LDS crossbar that __shfl_xor compiles to.
+template <int CTRL>
+LSA_DEVICE float dpp_mov(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
+}
+template <int W>
+LSA_DEVICE float group_sum(float v) {
+  static_assert(W == 8 || W == 16, "DPP row groups");
+  v += dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]: lane ^ 1
+  v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]: lane ^ 2
+  v += dpp_mov<0x141>(v);  // row_half_mirror: the other quad of the 8
+  if constexpr (W == 16) v += dpp_mov<0x140>(v);  // row_mirror: the other 8 of the 16
+  return v;
+}
+
+// v of lane (lane ^ OFF), OFF = 8 / 16 / 32, without the LDS crossbar: DPP row_ror:8 (exactly
+// lane ^ 8 inside a 16-lane row); v_permlane16_swap / v_permlane32_swap (gfx950) with both
+// operands = v leave {even-row, odd-row} (resp. {low-half, high-half}) copies in the pair.
+template <int OFF>
+LSA_DEVICE float lane_xor(float v) {
+  static_assert(OFF == 8 || OFF == 16 || OFF == 32, "lane_xor offsets");
+  if constexpr (OFF == 8) {
+    return dpp_mov<0x128>(v);
+  } else {
+    const unsigned u = __builtin_bit_cast(unsigned, v);
+    const bool upper = (__lane_id() & OFF) != 0;
+    if constexpr (OFF == 16) {
+      const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+      return __builtin_bit_cast(float, upper ? r[0] : r[1]);
+    } else {
+      const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+      return __builtin_bit_cast(float, upper ? r[0] : r[1]);
+    }
+  }
+}
+
 template <typename T>
 LSA_DEVICE T wave_max(T v) {
 #pragma unroll
