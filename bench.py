@@ -67,6 +67,10 @@ def parse():
     ap.add_argument("--mid-batch", type=int, default=128,
                     help="after the batch-1 pass, time --latency-steps decode steps of this many sequences "
                          "(<= 128, the fused-GEMV regime; mid_p50_tpot_ms / mid_tok_s); 0 = skip")
+    ap.add_argument("--ttft-lens", default="2048",
+                    help="one GPU: after the decode passes, batch-1 time-to-first-token (embed -> all layers -> "
+                         "lm_head argmax, median of 3 after a warm-up) at these prompt lengths on a separate "
+                         "engine of the same model (ttft_prompt_ms in the JSON line); '' or 0 = skip")
     ap.add_argument("--stage-layers", type=int, default=0,
                     help="profile one pipeline stage: the model cut to this many layers (NOT the headline metric)")
     ap.add_argument("--transport", default="rccl", choices=("rccl", "ipc"),
@@ -257,6 +261,40 @@ def supervise(a, argv: list) -> int:
     return code if code >= 0 else 1
 
 
+def ttft_probe(model: str, lengths: list, seed: int = 0, repeats: int = 3) -> dict:
+    """Batch-1 prefill latency of the whole model at each prompt length (outside the timed
+    decode region; scripts/latency_sweep.py is the full sweep). Returns {length: ms}."""
+    import statistics
+
+    import torch
+
+    from llm_sharding_amd.config import get_preset
+    from llm_sharding_amd.runtime.engine import RandomSource, StageEngine
+
+    cfg = get_preset(model)
+    dev = torch.device("cuda", 0)
+    eng = StageEngine(cfg, 0, cfg.num_hidden_layers, dev, torch.bfloat16, has_embed=True, has_head=True,
+                      source=RandomSource(cfg, seed), max_slots=1, max_seq=max(lengths) + 8,
+                      max_prefill_rows=max(lengths))
+    g = torch.Generator().manual_seed(seed)
+    out = {}
+    for P in lengths:
+        ts = []
+        for _ in range(repeats + 1):
+            ids = torch.randint(3, cfg.vocab_size, (P,), generator=g).to(dev)
+            eng.reset()
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            sl, po = eng.prefill_rows([0], [P])
+            tok = eng.head(eng.forward(eng.embed(ids), sl, po), [P - 1])
+            int(tok[0])
+            ts.append((time.perf_counter() - t) * 1e3)
+        out[str(P)] = round(statistics.median(ts[1:]), 3)
+    del eng
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -313,6 +351,13 @@ def main():
         line["transport"] = res["transport"]
         line["fallback"] = os.environ.get("LSA_BENCH_FALLBACK") == "1"
         line["preflight_us"] = res.get("preflight_us")
+    lens = [int(x) for x in str(a.ttft_lens).split(",") if x.strip() and int(x) > 0]
+    if lens and a.gpus == 1 and a.device == "cuda" and not a.stage_layers:
+        try:
+            line["ttft_prompt_ms"] = ttft_probe(a.model, lens, seed=a.seed)
+        except Exception as e:  # never lose the headline line to the side measurement
+            line["ttft_prompt_ms"] = None
+            line["ttft_error"] = f"{type(e).__name__}: {e}"[:200]
     if res.get("tokens_mb0"):  # parity digest across layouts (same prompts -> same tokens)
         import hashlib
         line["tokens_mb0_sha16"] = hashlib.sha256(json.dumps(res["tokens_mb0"]).encode()).hexdigest()[:16]
