@@ -39,7 +39,15 @@ LSA_DEVICE void attn_split_body(
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int grp = lane / LPK, li = lane % LPK;
 
-  int T = kv_len ? kv_len[row] : pos[row] + 1;
+  // the row's cache slot and length: two independent scalar loads, issued together (the empty
+  // asm keeps the compiler from sinking the slot load behind the length test's branch)
+  const int* lenp = kv_len ? kv_len : pos;
+  const int slot_r = slot[row], len_r = lenp[row];
+  asm volatile("" ::"s"(slot_r), "s"(len_r));
+  const size_t cbase = ((size_t)slot_r * n_kv + kvh) * (size_t)t_max * HD;
+  const bf16_raw* kb = kc + cbase + li * 8;
+  const bf16_raw* vb = vc + cbase + li * 8;
+  int T = len_r + (kv_len ? 0 : 1);
   T = T > t_max ? t_max : T;  // never read past the static cache
   int chunk = (T + nsplit - 1) / nsplit;
   chunk = chunk < min_chunk ? min_chunk : chunk;
@@ -94,18 +102,6 @@ LSA_DEVICE void attn_split_body(
     if (tid == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
 
-  float qf[G][8];
-#pragma unroll
-  for (int r = 0; r < G; ++r) {
-    unpack8(ld16(q + (size_t)row * ldq + (size_t)(kvh * G + r) * HD + li * 8), qf[r]);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) qf[r][j] *= scale_log2;
-  }
-
-  const size_t cbase = ((size_t)slot[row] * n_kv + kvh) * (size_t)t_max * HD;
-  const bf16_raw* kb = kc + cbase + li * 8;
-  const bf16_raw* vb = vc + cbase + li * 8;
-
   float mx[G], l[G], o[G][8];
 #pragma unroll
   for (int r = 0; r < G; ++r) {
@@ -130,13 +126,29 @@ LSA_DEVICE void attn_split_body(
     }
   };
   u32x4_t kr[U], vr[U];
+  // One-split grids (!SPLIT: batch-1 decode, 32 workgroups on the chip) are a chain of dependent
+  // round trips: the first trip's K/V loads go out before q is even requested (they need only
+  // slot[row] and the length), so q's load overlaps them instead of preceding them.
+  if constexpr (!SPLIT) {
+    if (k0 + w * KPW < k1) load(k0 + w * KPW, kr, vr);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+
+  float qf[G][8];
+#pragma unroll
+  for (int r = 0; r < G; ++r) {
+    unpack8(ld16(q + (size_t)row * ldq + (size_t)(kvh * G + r) * HD + li * 8), qf[r]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) qf[r][j] *= scale_log2;
+  }
+
   if (PF && k0 + w * KPW < k1) load(k0 + w * KPW, kr, vr);
   // loop bound is wave-uniform (the 16-lane key groups of a wave shuffle only internally)
   for (int base = k0 + w * KPW; base < k1; base += KPI * U) {
     u32x4_t kn[U], vn[U];
     if (PF) {
       if (base + KPI * U < k1) load(base + KPI * U, kn, vn);
-    } else {
+    } else if (SPLIT || base != k0 + w * KPW) {  // (!SPLIT: the first trip was issued above)
       load(base, kr, vr);
     }
     bool valid[U];
