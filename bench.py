@@ -71,6 +71,10 @@ def parse():
                     help="one GPU: after the decode passes, batch-1 time-to-first-token (embed -> all layers -> "
                          "lm_head argmax, median of 3 after a warm-up) at these prompt lengths on a separate "
                          "engine of the same model (ttft_prompt_ms in the JSON line); '' or 0 = skip")
+    ap.add_argument("--extras", default="llama3.2-3b,llama2-13b,llama2-70b:10",
+                    help="one GPU: after the headline, short decode runs of these models at the same batch "
+                         "(MODEL or MODEL:LAYERS = one stage of that many layers with 8 micro-batches, e.g. "
+                         "the 70B 8-stage plan's 10-layer stage) -> 'extra' in the JSON line; '' = skip")
     ap.add_argument("--stage-layers", type=int, default=0,
                     help="profile one pipeline stage: the model cut to this many layers (NOT the headline metric)")
     ap.add_argument("--transport", default="rccl", choices=("rccl", "ipc"),
@@ -295,6 +299,35 @@ def ttft_probe(model: str, lengths: list, seed: int = 0, repeats: int = 3) -> di
     return out
 
 
+def extra_runs(spec: str, a) -> dict:
+    """Operating-range points measured by the same run as the headline (outside its timed
+    region, one GPU): other model families at the bench batch, and one pipeline stage of a
+    model too big for one GPU (the 70B 10-layer stage of the 8-stage plan, 8 micro-batches)."""
+    import gc
+
+    import torch
+
+    from llm_sharding_amd.parallel.pipeline import run_decode_benchmark
+    out = {}
+    for item in [x.strip() for x in spec.split(",") if x.strip()]:
+        model, _, layers = item.partition(":")
+        nl = int(layers) if layers else 0
+        key = f"{model}_stage{nl}_mb8" if nl else model
+        try:
+            r = run_decode_benchmark(model=model, n_gpus=1, steps=8 if nl else 16, warmup=2 if nl else 4,
+                                     batch=a.batch, prompt_len=a.prompt_len, seed=a.seed, verbose=False,
+                                     stage_layers=nl, microbatches=8 if nl else 0)
+            out[key] = {"tok_s": round(r["tok_s"], 1), "ms_per_step": round(r["ms_per_step"], 3),
+                        "global_batch": r["global_batch"]}
+            if nl:  # tok_s = the whole pipeline's rate if every stage ran like this one
+                out[key]["kind"] = "stage_profile"
+        except Exception as e:  # a side measurement never costs the headline line
+            out[key] = {"error": f"{type(e).__name__}: {e}"[:200]}
+        gc.collect()
+        torch.cuda.empty_cache()
+    return out
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -358,6 +391,8 @@ def main():
         except Exception as e:  # never lose the headline line to the side measurement
             line["ttft_prompt_ms"] = None
             line["ttft_error"] = f"{type(e).__name__}: {e}"[:200]
+    if a.extras and a.gpus == 1 and a.device == "cuda" and not a.stage_layers:
+        line["extra"] = extra_runs(a.extras, a)
     if res.get("tokens_mb0"):  # parity digest across layouts (same prompts -> same tokens)
         import hashlib
         line["tokens_mb0_sha16"] = hashlib.sha256(json.dumps(res["tokens_mb0"]).encode()).hexdigest()[:16]
