@@ -59,6 +59,11 @@ LSA_DEVICE int sw_off(int r, int ch) {
 LSA_DEVICE void glds16(const void* src, unsigned char* lds_base) {
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
 }
+// non-temporal (aux nt): for bytes one workgroup reads once per step (decode K/V). Not for the
+// prefill, whose K/V blocks every query tile of the sequence re-reads from L2.
+LSA_DEVICE void glds16_nt(const void* src, unsigned char* lds_base) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_base, 16, 0, 2);
+}
 
 template <int HD, int HPW>
 __global__ __launch_bounds__(NTHR) void flash_prefill_kernel(
@@ -338,8 +343,8 @@ __global__ __launch_bounds__(NW * 64) void gqa_decode_kernel(
       const int r = s * RPP + lane / NC, cs = lane % NC;
       const int ch = cs ^ swz<HD>(r);
       const int key = min(sb * SB + r, kl - 1);  // clamped rows are masked in the softmax
-      glds16(kb_ptr + (size_t)key * HD + ch * 8, kd + s * 1024);
-      glds16(vb_ptr + (size_t)key * HD + ch * 8, kd + BLK + s * 1024);
+      glds16_nt(kb_ptr + (size_t)key * HD + ch * 8, kd + s * 1024);
+      glds16_nt(vb_ptr + (size_t)key * HD + ch * 8, kd + BLK + s * 1024);
     }
   };
 
