@@ -16,7 +16,7 @@ tail -1 $out/smoke.log
 timeout -k 10 400 python3 bench.py --steps 20 --warmup 5 > $out/bench.log 2>&1 || { tail -20 $out/bench.log; exit 4; }
 grep '^{' $out/bench.log | tail -1
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $out/prof -o run -- \
-    python3 -u bench.py --steps 20 --warmup 5 --latency-steps 0 --ttft-lens 0 > $out/prof_bench.log 2>&1 || { tail -20 $out/prof_bench.log; exit 5; }
+    python3 -u bench.py --steps 20 --warmup 5 --latency-steps 0 --ttft-lens 0 --extras= > $out/prof_bench.log 2>&1 || { tail -20 $out/prof_bench.log; exit 5; }
 f=$(find $out/prof -name "*kernel_trace.csv" | head -1)
 python3 scripts/kstats.py "$f" flash_prefill 14 > $out/kstats.txt
 head -12 $out/kstats.txt
