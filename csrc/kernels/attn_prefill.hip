@@ -307,9 +307,10 @@ __global__ __launch_bounds__(NW * 64) void gqa_decode_kernel(
   constexpr int SB = 32;                       // keys per sub-block (one 32-deep PV fragment)
   constexpr int KF = HD / 32, DT = HD / 16, NC = HD / 8;
   constexpr int BLK = SB * HD * 2;             // bytes of one K (or V) sub-block
-  constexpr int PPW = BLK / 1024;              // 1 KiB DMA pieces per operand and sub-block
+  constexpr int PPW = BLK / 1024;              // 1 KiB DMA pieces per V sub-block
   constexpr int RPP = 1024 / (HD * 2);         // rows per piece
-  constexpr int WREG = 2 * 2 * BLK;            // one wave's staging: [buffer][K | V]
+  constexpr int NKL = 2 * KF;                  // K fragment loads per lane and sub-block
+  constexpr int WREG = 2 * BLK;                // one wave's staging: [buffer] V only
   constexpr int MERGE = NW * (16 * HD + 32) * 4;
   constexpr int SMEM = NW * WREG > MERGE ? NW * WREG : MERGE;
   static_assert(PPW >= 1, "geometry");
@@ -336,15 +337,24 @@ __global__ __launch_bounds__(NW * 64) void gqa_decode_kernel(
   const bf16_raw* vb_ptr = vc + cache_base;
   unsigned char* my = smem + w * WREG;
 
-  auto stage = [&](int sb, int buf) {
-    unsigned char* kd = my + buf * (2 * BLK);
+  // Sub-block sb: V by LDS-DMA into this wave's buffer `buf` (the PV MFMA reads it transposed),
+  // K straight into registers - the S^T MFMA's A operand is 16 contiguous bytes of one key row
+  // per lane (key kt*16 + l16, dims kf*32 + 8g ..) - so the wave stages half the LDS bytes and a
+  // CU holds twice the waves (every byte is read once per step: non-temporal).
+  auto stage = [&](int sb, int buf, u32x4_t (&kr)[2][KF]) {
+    unsigned char* vd = my + buf * BLK;
 #pragma unroll
     for (int s = 0; s < PPW; ++s) {
       const int r = s * RPP + lane / NC, cs = lane % NC;
       const int ch = cs ^ swz<HD>(r);
       const int key = min(sb * SB + r, kl - 1);  // clamped rows are masked in the softmax
-      glds16_nt(kb_ptr + (size_t)key * HD + ch * 8, kd + s * 1024);
-      glds16_nt(vb_ptr + (size_t)key * HD + ch * 8, kd + BLK + s * 1024);
+      glds16_nt(vb_ptr + (size_t)key * HD + ch * 8, vd + s * 1024);
+    }
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      const int key = min(sb * SB + kt * 16 + l16, kl - 1);
+#pragma unroll
+      for (int kf = 0; kf < KF; ++kf) kr[kt][kf] = ld16_nt(kb_ptr + (size_t)key * HD + kf * 32 + g * 8);
     }
   };
 
@@ -352,38 +362,20 @@ __global__ __launch_bounds__(NW * 64) void gqa_decode_kernel(
 #pragma unroll
   for (int d = 0; d < DT; ++d) o[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   float m_run = -INFINITY, l_run = 0.f;
-  int k_off[KF], v_off[DT];
-#pragma unroll
-  for (int kf = 0; kf < KF; ++kf) k_off[kf] = sw_off<HD>(l16, kf * 4 + g);
+  int v_off[DT];
   const int key_lo = 4 * g + (l16 >> 2);
 #pragma unroll
   for (int d = 0; d < DT; ++d) v_off[d] = sw_off<HD>(key_lo, 2 * d + ((l16 & 3) >> 1)) + 8 * (l16 & 1);
 
-  const int nsb = (kl + SB - 1) / SB;
-  int buf = 0;
-  if (w < nsb) stage(w, 0);
-  for (int sb = w; sb < nsb; sb += NW) {
-    const bool more = sb + NW < nsb;
-    if (more) {
-      // the other buffer's previous sub-block was fully read (its ds_reads retired before the
-      // MFMAs that consumed them) - restage it, keep one sub-block in flight
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      stage(sb + NW, buf ^ 1);
-      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * PPW) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    const unsigned char* ks = my + buf * (2 * BLK);
-    const unsigned char* vs = ks + BLK;
+  // one sub-block: K from registers kr, V from buffer buf
+  auto compute = [&](int sb, int buf, const u32x4_t (&kr)[2][KF]) {
+    const unsigned char* vs = my + buf * BLK;
     f32x4_t s[2];
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
       s[kt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int kf = 0; kf < KF; ++kf)
-        s[kt] = mfma16(*reinterpret_cast<const u32x4_t*>(ks + kt * 16 * (HD * 2) + k_off[kf]), qf[kf], s[kt]);
+      for (int kf = 0; kf < KF; ++kf) s[kt] = mfma16(kr[kt][kf], qf[kf], s[kt]);
     }
     float mx = -INFINITY;
 #pragma unroll
@@ -434,7 +426,33 @@ __global__ __launch_bounds__(NW * 64) void gqa_decode_kernel(
       a[3] = __builtin_bit_cast(u32x2_t, hi)[1];
       o[d] = mfma16(a, b, o[d]);
     }
-    buf ^= 1;
+  };
+
+  // Two register / LDS buffers alternate with compile-time indices (the loop is unrolled by 2);
+  // before reading sub-block sb the wave restages the other buffer with sb + NW (its previous
+  // contents were consumed by the previous step) and waits for sb only: the later stage's
+  // PPW + NKL operations stay in flight (V DMA is ordered by this counted wait, K registers by
+  // the compiler's own waits).
+  const int nsb = (kl + SB - 1) / SB;
+  u32x4_t k0r[2][KF], k1r[2][KF];
+  auto step = [&](int sb, int cur, u32x4_t (&kcur)[2][KF], u32x4_t (&knext)[2][KF]) {
+    if (sb + NW < nsb) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the other buffer's V reads retired
+      __builtin_amdgcn_sched_barrier(0);
+      stage(sb + NW, cur ^ 1, knext);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PPW + 2 * NKL) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    compute(sb, cur, kcur);
+  };
+  int sb = w;
+  if (sb < nsb) stage(sb, 0, k0r);
+  for (; sb < nsb; sb += 2 * NW) {
+    step(sb, 0, k0r, k1r);
+    if (sb + NW >= nsb) break;
+    step(sb + NW, 1, k1r, k0r);
   }
   l_run += __shfl_xor(l_run, 16, 64);
   l_run += __shfl_xor(l_run, 32, 64);
