@@ -6,7 +6,7 @@ in a decode step). Run under ``rocprofv3 --pmc ...`` (one pass per counter group
 ``--kernel-trace``; scripts/gemm_pmc_summary.py attributes every dispatch to its (impl, shape)
 through the 1-element fill kernel launched before each block.
 
-usage: gemm_pmc_probe.py [--rows 512] [--launches 6] [--impls ours,blas] [--model llama2-7b]
+usage: gemm_pmc_probe.py [--rows 512] [--launches 6] [--impls ours,coop,blas] [--model llama2-7b]
 Prints the block order as one JSON line (the summary reads it from the log)."""
 import argparse
 import json
@@ -48,11 +48,13 @@ def main():
             for i in range(a.launches):
                 if impl == "ours":
                     hip.gemm(x, wps[(i + 1) % nbuf], M, N, K, hip.EPI_STORE, ep, sk_ws=sk_ws)
+                elif impl == "coop":  # the decode GEMV family at <= 128 rows (tuned config)
+                    hip.gemv(x, wps[(i + 1) % nbuf], M, N, K, hip.EPI_STORE, ep)
                 else:
                     torch.matmul(x, ws_[(i + 1) % nbuf].t(), out=out)
             torch.cuda.synchronize()
             blocks.append({"impl": impl, "shape": name, "M": M, "N": N, "K": K,
-                           "plan": plan if impl == "ours" else "hipblaslt"})
+                           "plan": plan if impl == "ours" else ("coop (gemv_tuning.json)" if impl == "coop" else "hipblaslt")})
         del ws_, wps
         torch.cuda.empty_cache()
     print(json.dumps({"blocks": blocks}), flush=True)
