@@ -19,16 +19,16 @@
 //  * waves 1..4 are CONSUMERS: per op they gather the input vector from the previous op's output
 //    granules (8 bytes = 2 bf16 + a 32-bit tag written by ONE write-through store; tag = epoch * 4 +
 //    op + 1, so no flag, counter or grid barrier exists), then reduce every published slot: lane l
-//    takes 32 consecutive weights of one row, dots them with x (v_dot2_f32_bf16) and adds the
+//    takes 32 consecutive weights of one row, dots them with x (fp32 FMAs) and adds the
 //    partial into an LDS row accumulator; each wave frees the slot after its reads retired.
 //  * every spin is bounded (SPIN_MAX polls with s_sleep): a missing producer sets *err and the
 //    workgroup runs to its end, so the grid always drains.
-// Row accumulation uses LDS float atomics (order not fixed): a probe, not bit-reproducible.
+// Row accumulation: a wave-level reduction, then LDS float atomics (order not fixed): a probe, not
+// bit-reproducible.
 #include "common.h"
 
 namespace {
 
-typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
 constexpr int P = 4;
 constexpr int NCW = 4;                  // consumer waves
 constexpr int NTHR = (NCW + 1) * 64;    // + the loader wave
@@ -45,8 +45,9 @@ struct ChainArgs {
   int N[P], K[P];
   const bf16_raw* x0;
   unsigned long long* gran[P];  // op p's output as N_p / 2 granules {2 x bf16 | tag << 32}
-  unsigned* err;
+  unsigned* err;  // [0] flags, [1] staged-weight mismatches, [2] staged-x mismatches (check)
   unsigned epoch;
+  int check;
 };
 
 LSA_DEVICE unsigned lds_load(unsigned* p) { return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP); }
@@ -154,20 +155,57 @@ __global__ __launch_bounds__(NTHR) void chain_kernel(ChainArgs a) {
         if (++spins > SPIN_MAX) { if (lane == 0) atomicOr(a.err, 8u); break; }
       }
       const long long e0 = (long long)j * (SLOT / 2) + cl * 32;
+      float d = 0.f;
+      int row = -1;
       if (e0 < nel) {
-        const int row = (int)(e0 / K), col = (int)(e0 - (long long)row * K);
+        row = (int)(e0 / K);
+        const int col = (int)(e0 - (long long)row * K);
         const u32x4_t* wv = reinterpret_cast<const u32x4_t*>(ring + i * SLOT + cl * 64);
         const u32x4_t* xv = reinterpret_cast<const u32x4_t*>(xs + col);
-        float d = 0.f;
+        if (a.check) {  // debug: the staged bytes against the same bytes read from memory
+          const u32x4_t* gv = reinterpret_cast<const u32x4_t*>(a.w[p] + (size_t)g * R * K + e0);
+          bool bad = false;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const u32x4_t x1 = wv[q], x2 = gv[q];
+            bad |= x1[0] != x2[0] || x1[1] != x2[1] || x1[2] != x2[2] || x1[3] != x2[3];
+          }
+          if (bad) atomicAdd(a.err + 1, 1u);
+          if (p == 0) {
+            const u32x4_t* gx = reinterpret_cast<const u32x4_t*>(a.x0 + col);
+            bool badx = false;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const u32x4_t x1 = xv[q], x2 = gx[q];
+              badx |= x1[0] != x2[0] || x1[1] != x2[1] || x1[2] != x2[2] || x1[3] != x2[3];
+            }
+            if (badx) atomicAdd(a.err + 2, 1u);
+          }
+        }
+        // fp32 FMAs on unpacked bf16 (hipcc 7.2 folded the four v_dot2c_f32_bf16 of a 16-B chunk onto
+        // its first dword pair - the first build of this probe computed wrong rows)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const u32x4_t wq = wv[q], xq = xv[q];
+          float wf[8], xf[8];
+          unpack8(wv[q], wf);
+          unpack8(xv[q], xf);
 #pragma unroll
-          for (int e = 0; e < 4; ++e)
-            d = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, wq[e]), __builtin_bit_cast(bf16x2_t, xq[e]), d, false);
+          for (int e = 0; e < 8; ++e) d = __builtin_fmaf(wf[e], xf[e], d);
         }
-        __hip_atomic_fetch_add(&acc[row], d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
+      // wave-level reduction first (a 4 KiB wave chunk spans at most two consecutive rows: rows are
+      // >= 8 KiB), then one LDS atomic per row and wave instead of 64 on one address
+      const int row0 = __builtin_amdgcn_readfirstlane(row);
+      const bool hasb = __builtin_amdgcn_ballot_w64(row0 >= 0 && row == row0 + 1) != 0;
+      float da = row == row0 ? d : 0.f, db = (row0 >= 0 && row == row0 + 1) ? d : 0.f;
+      da = group_sum<16>(da);
+      da += lane_xor<16>(da);
+      da += lane_xor<32>(da);
+      db = group_sum<16>(db);
+      db += lane_xor<16>(db);
+      db += lane_xor<32>(db);
+      if (row0 >= 0 && lane == 0) __hip_atomic_fetch_add(&acc[row0], da, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (hasb && lane == 0) __hip_atomic_fetch_add(&acc[row0 + 1], db, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's ring reads retired
       if (lane == 0) __hip_atomic_fetch_add(&free_cnt[i], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
@@ -187,7 +225,8 @@ __global__ __launch_bounds__(NTHR) void chain_kernel(ChainArgs a) {
 }  // namespace
 
 extern "C" int lsa_chain_probe(const void* const* w, const int* N, const int* K, const void* x0,
-                               unsigned long long* const* gran, unsigned* err, unsigned epoch, hipStream_t stream) {
+                               unsigned long long* const* gran, unsigned* err, unsigned epoch, int check,
+                               hipStream_t stream) {
   ChainArgs a;
   for (int p = 0; p < P; ++p) {
     if (N[p] % 256 || N[p] / 256 > MAXR || (N[p] / 256) % 2 || K[p] % 32 || K[p] > MAXK) return LSA_BAD_SHAPE;
@@ -200,6 +239,7 @@ extern "C" int lsa_chain_probe(const void* const* w, const int* N, const int* K,
   a.x0 = static_cast<const bf16_raw*>(x0);
   a.err = err;
   a.epoch = epoch;
+  a.check = check;
   chain_kernel<<<256, NTHR, 0, stream>>>(a);
   return hipGetLastError() == hipSuccess ? LSA_OK : LSA_LAUNCH_FAILED;
 }
