@@ -131,17 +131,30 @@ __global__ __launch_bounds__(NTHR) void chain_kernel(ChainArgs a) {
     } else {
       const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc((void*)a.gran[p - 1], (short)0, 0x7fffffff, 0x00020000);
       const unsigned want = a.epoch * P + (unsigned)p;  // tag of op p-1
-      for (int gi = cl; gi < K / 2; gi += NCW * 64) {
-        unsigned spins = 0;
-        for (;;) {
-          const u32x2_t v = __builtin_amdgcn_raw_buffer_load_b64(gr, gi * 8, 0, 16 /* sc1 */);
-          if (v[1] == want) {
-            *reinterpret_cast<unsigned*>(xs + 2 * gi) = v[0];
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-          if (++spins > SPIN_MAX) { atomicOr(a.err, 4u); break; }
+      // every granule of this lane requested in one pass (independent loads in flight together),
+      // then checked; a pass with any tag missing is repeated (bounded)
+      constexpr int GPL = (MAXK / 2 + NCW * 64 - 1) / (NCW * 64);
+      unsigned spins = 0;
+      for (;;) {
+        u32x2_t v[GPL];
+#pragma unroll
+        for (int t = 0; t < GPL; ++t) {
+          const int gi = cl + t * NCW * 64;
+          v[t] = gi < K / 2 ? __builtin_amdgcn_raw_buffer_load_b64(gr, gi * 8, 0, 16 /* sc1 */) : u32x2_t{0u, want};
         }
+        bool all = true;
+#pragma unroll
+        for (int t = 0; t < GPL; ++t) {
+          const int gi = cl + t * NCW * 64;
+          if (v[t][1] == want) {
+            if (gi < K / 2) *reinterpret_cast<unsigned*>(xs + 2 * gi) = v[t][0];
+          } else {
+            all = false;
+          }
+        }
+        if (all) break;
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > SPIN_MAX) { atomicOr(a.err, 4u); break; }
       }
     }
     cons_barrier();
