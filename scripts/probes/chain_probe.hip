@@ -31,11 +31,13 @@ namespace {
 
 constexpr int P = 4;
 constexpr int NCW = 4;                  // consumer waves
-constexpr int NTHR = (NCW + 1) * 64;    // + the loader wave
+constexpr int NLW = 2;                  // loader waves (each issues PIECES / NLW of every slot)
+constexpr int NTHR = (NCW + NLW) * 64;
 constexpr int SLOT = 16384;             // bytes per ring slot
 constexpr int PIECES = SLOT / 1024;     // 1 KiB DMA pieces per slot (64 lanes x 16 B)
-constexpr int D = 4;                    // slots the loader keeps in flight
+constexpr int D = 5;                    // slots the loaders keep in flight
 constexpr int NS = D + 3;               // ring slots (>= in flight + 3, 'ring-gemm')
+constexpr int PPL = PIECES / NLW;       // pieces per loader wave and slot
 constexpr int MAXK = 11008;
 constexpr int MAXR = 96;
 constexpr unsigned SPIN_MAX = 1u << 21;
@@ -68,11 +70,11 @@ __global__ __launch_bounds__(NTHR) void chain_kernel(ChainArgs a) {
   __syncthreads();  // the only whole-workgroup barrier
   const int g = blockIdx.x, G = gridDim.x;
 
-  if (w == 0) {
+  if (w < NLW) {
     // ------------------------------------------------------------------ loader
     int s = 0;
-    auto publish = [&](int sp) {  // slot sp landed (caller waited for it)
-      if (lane == 0) __hip_atomic_store(&full_gen[sp % NS], (unsigned)(sp / NS + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    auto publish = [&](int sp) {  // this wave's part of slot sp landed (caller waited for it)
+      if (lane == 0) __hip_atomic_fetch_add(&full_gen[sp % NS], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     };
     for (int p = 0; p < P; ++p) {
       const int R = a.N[p] / G, K = a.K[p];
@@ -88,14 +90,14 @@ __global__ __launch_bounds__(NTHR) void chain_kernel(ChainArgs a) {
           if (++spins > SPIN_MAX) { if (lane == 0) atomicOr(a.err, 1u); break; }
         }
 #pragma unroll
-        for (int q = 0; q < PIECES; ++q) {
+        for (int q = w * PPL; q < (w + 1) * PPL; ++q) {
           long long off = (long long)j * SLOT + q * 1024 + lane * 16;
           if (off >= bytes) off = 0;  // tail of the last slot: any valid address (never consumed)
           __builtin_amdgcn_global_load_lds(base + off, (__attribute__((address_space(3))) void*)(ring + i * SLOT + q * 1024),
                                            16, 0, 2 /* nt */);
         }
         if (s >= D - 1) {
-          asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PIECES * (D - 1)) : "memory");
+          asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PPL * (D - 1)) : "memory");
           publish(s - (D - 1));
         }
       }
@@ -106,7 +108,7 @@ __global__ __launch_bounds__(NTHR) void chain_kernel(ChainArgs a) {
   }
 
   // -------------------------------------------------------------------- consumers
-  const int cl = tid - 64;  // 0 .. NCW*64-1
+  const int cl = tid - NLW * 64;  // 0 .. NCW*64-1
   unsigned nbar = 0;
   auto cons_barrier = [&]() {  // the NCW consumer waves only (the loader never joins)
     ++nbar;
@@ -161,7 +163,7 @@ __global__ __launch_bounds__(NTHR) void chain_kernel(ChainArgs a) {
     // 2. reduce the op's slots
     for (int j = 0; j < nsl; ++j, ++s) {
       const int i = s % NS;
-      const unsigned gen = (unsigned)(s / NS + 1);
+      const unsigned gen = (unsigned)(NLW * (s / NS + 1));  // every loader wave's part landed
       unsigned spins = 0;
       while (lds_load(&full_gen[i]) < gen) {
         __builtin_amdgcn_s_sleep(1);
