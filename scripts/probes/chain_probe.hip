@@ -31,7 +31,7 @@ namespace {
 
 constexpr int P = 4;
 constexpr int NCW = 4;                  // consumer waves
-constexpr int NLW = 2;                  // loader waves (each issues PIECES / NLW of every slot)
+constexpr int NLW = 4;                  // loader waves (each issues PIECES / NLW of every slot)
 constexpr int NTHR = (NCW + NLW) * 64;
 constexpr int SLOT = 16384;             // bytes per ring slot
 constexpr int PIECES = SLOT / 1024;     // 1 KiB DMA pieces per slot (64 lanes x 16 B)
