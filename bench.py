@@ -111,10 +111,10 @@ def spawn_ranks(n: int) -> int:
     _forward_termination(lambda: procs)
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PYTHONUNBUFFERED="1")
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PYTHONUNBUFFERED="1",
+                   LSA_PARENT_PID=str(os.getpid()))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
-                                      stdout=None if r == 0 else subprocess.DEVNULL, start_new_session=True,
-                                      preexec_fn=_die_with_parent))
+                                      stdout=None if r == 0 else subprocess.DEVNULL, start_new_session=True))
     rc = 0
     pending = list(range(n))
     while pending:
@@ -139,16 +139,25 @@ PREFLIGHT_EXIT = 75  # = parallel.pipeline.PREFLIGHT_EXIT (not imported: the sup
 
 
 def _die_with_parent() -> None:
-    """preexec_fn of every child this script starts: the kernel sends the child SIGKILL when the
-    process that started it exits (PR_SET_PDEATHSIG), however that happens - a launcher's killpg
-    aimed at the parent's process group, a driver timeout, SIGKILL - so no GPU-holding worker
-    outlives its supervisor in its own session."""
+    """Run FIRST in every child this script starts (``LSA_PARENT_PID`` in its env): the kernel
+    sends this process SIGKILL when the process that started it exits (PR_SET_PDEATHSIG), however
+    that happens - a launcher's killpg aimed at the parent's process group, a driver timeout,
+    SIGKILL - so no GPU-holding worker outlives its supervisor in its own session. Set here in
+    the child rather than between fork and exec: the supervisor already runs gloo threads when it
+    starts a worker, and code run there in a multithreaded parent can deadlock on a lock another
+    thread held (advisor round 5). If the parent is already gone (it died before the prctl took
+    effect) the child exits at once."""
     import ctypes
     import signal
+    want = os.environ.pop("LSA_PARENT_PID", None)
+    if not want:
+        return
     try:
         ctypes.CDLL(None, use_errno=True).prctl(1, int(signal.SIGKILL), 0, 0, 0)  # PR_SET_PDEATHSIG = 1
     except Exception:  # noqa: BLE001 - not Linux: the signal handlers below still stop the children
-        pass
+        return
+    if os.getppid() != int(want):
+        os._exit(1)
 
 
 def _stop_group(proc, grace_s: float = 10.0) -> None:
@@ -186,11 +195,11 @@ def _forward_termination(children) -> None:
 
 def _spawn_worker(argv: list, port: int, extra_env: dict):
     import subprocess
-    env = dict(os.environ, MASTER_PORT=str(port), LSA_BENCH_ROLE="worker", PYTHONUNBUFFERED="1", **extra_env)
+    env = dict(os.environ, MASTER_PORT=str(port), LSA_BENCH_ROLE="worker", PYTHONUNBUFFERED="1",
+               LSA_PARENT_PID=str(os.getpid()), **extra_env)
     # the workers rendezvous on their own store (rank 0's worker hosts it), not torchrun's agent store
     env.pop("TORCHELASTIC_USE_AGENT_STORE", None)
-    return subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env, start_new_session=True,
-                            preexec_fn=_die_with_parent)
+    return subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env, start_new_session=True)
 
 
 def _watch(proc, store, rank: int, world: int, attempt: int) -> int:
@@ -329,6 +338,7 @@ def extra_runs(spec: str, a) -> dict:
 
 
 def main():
+    _die_with_parent()  # a child of spawn_ranks / supervise: die with that parent
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if a.gpus != world and world != 1:
@@ -384,6 +394,9 @@ def main():
         line["transport"] = res["transport"]
         line["fallback"] = os.environ.get("LSA_BENCH_FALLBACK") == "1"
         line["preflight_us"] = res.get("preflight_us")
+    topo = res.get("topology")
+    if topo:  # proof of placement: process-group size, each rank's device UUID / PCI id, edge transports
+        line["dist"] = topo
     lens = [int(x) for x in str(a.ttft_lens).split(",") if x.strip() and int(x) > 0]
     if lens and a.gpus == 1 and a.device == "cuda" and not a.stage_layers:
         try:

@@ -102,7 +102,9 @@ def build(force: bool = False, jobs: int = 8, arch: str = "gfx950", verbose: boo
     if not os.path.exists(audit_stamp) or os.path.getmtime(audit_stamp) < os.path.getmtime(klib):
         sys.path.insert(0, CSRC)
         from isa_audit import audit  # csrc/isa_audit.py
-        res = audit(klib)
+        res = audit(klib, arch)
+        if res["code_objects"] == 0:  # an audit that checked nothing must not pass (advisor round 5)
+            raise RuntimeError(f"ISA audit of {klib}: no {arch} code object found in the library's offload bundle")
         if res["findings"]:
             raise RuntimeError(f"ISA audit of {klib}: {len(res['findings'])} VALU -> packed-FP32 back-to-back "
                                f"dependencies, e.g. {res['findings'][:3]} (csrc/isa_audit.py)")

@@ -22,7 +22,7 @@ import tempfile
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 LLVM = os.path.join(ROCM, "lib", "llvm", "bin")
 MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
-TARGET = "hipv4-amdgcn-amd-amdhsa--gfx950"
+TARGET = "hipv4-amdgcn-amd-amdhsa--{arch}"
 PK = ("v_pk_fma_f32", "v_pk_mul_f32", "v_pk_add_f32", "v_pk_mov_b32")
 REG = re.compile(r"\bv(?:\[(\d+):(\d+)\]|(\d+)\b)")
 
@@ -37,8 +37,8 @@ def _vregs(tok: str) -> set:
     return out
 
 
-def disassemble(so_path: str) -> list:
-    """Disassembly text of every gfx950 code object bundled in the library's .hip_fatbin."""
+def disassemble(so_path: str, arch: str = "gfx950") -> list:
+    """Disassembly text of every ``arch`` code object bundled in the library's .hip_fatbin."""
     texts = []
     with tempfile.TemporaryDirectory() as td:
         fat = os.path.join(td, "fat.bin")
@@ -52,7 +52,7 @@ def disassemble(so_path: str) -> list:
             with open(cp, "wb") as f:
                 f.write(chunk)
             r = subprocess.run([os.path.join(LLVM, "clang-offload-bundler"), "--type=o", f"--input={cp}",
-                                f"--targets={TARGET}", f"--output={co}", "--unbundle"], capture_output=True)
+                                f"--targets={TARGET.format(arch=arch)}", f"--output={co}", "--unbundle"], capture_output=True)
             if r.returncode != 0 or not os.path.getsize(co):
                 continue
             d = subprocess.run([os.path.join(LLVM, "llvm-objdump"), "-d", co], check=True, capture_output=True,
@@ -88,9 +88,9 @@ def audit_text(text: str) -> tuple:
     return findings, n_pk
 
 
-def audit(so_path: str) -> dict:
+def audit(so_path: str, arch: str = "gfx950") -> dict:
     findings, n_pk, n_obj = [], 0, 0
-    for t in disassemble(so_path):
+    for t in disassemble(so_path, arch):
         f, n = audit_text(t)
         findings += f
         n_pk += n

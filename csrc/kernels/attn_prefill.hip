@@ -430,9 +430,10 @@ __global__ __launch_bounds__(NW * 64) void gqa_decode_kernel(
 
   // Two register / LDS buffers alternate with compile-time indices (the loop is unrolled by 2);
   // before reading sub-block sb the wave restages the other buffer with sb + NW (its previous
-  // contents were consumed by the previous step) and waits for sb only: the later stage's
-  // PPW + NKL operations stay in flight (V DMA is ordered by this counted wait, K registers by
-  // the compiler's own waits).
+  // contents were consumed by the previous step) and waits until only the later stage's
+  // PPW + NKL operations are in flight: the WHOLE older stage (V DMA and K loads) has retired,
+  // whatever order the compiler issued its V DMA and K loads in (compute() needs the K
+  // registers first anyway, so waiting for them here costs nothing; advisor round 5).
   const int nsb = (kl + SB - 1) / SB;
   u32x4_t k0r[2][KF], k1r[2][KF];
   auto step = [&](int sb, int cur, u32x4_t (&kcur)[2][KF], u32x4_t (&knext)[2][KF]) {
@@ -440,7 +441,7 @@ __global__ __launch_bounds__(NW * 64) void gqa_decode_kernel(
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the other buffer's V reads retired
       __builtin_amdgcn_sched_barrier(0);
       stage(sb + NW, cur ^ 1, knext);
-      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PPW + 2 * NKL) : "memory");
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PPW + NKL) : "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }

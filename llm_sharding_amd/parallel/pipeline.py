@@ -678,6 +678,59 @@ def _latency_pass(cfg, stage: "PipelineStage", srank: int, pp: int, st, dev, max
     return (_percentile(tp, 0.5) if tp else 0.0), el
 
 
+def rank_identity(rank: int, dev: torch.device) -> dict:
+    """Which device this rank really runs on: host, pid, visibility env and, on a GPU, the
+    device's UUID and PCI address (from the HIP runtime, not from the rank number) - so a
+    multi-GPU JSON line proves that its N ranks ran on N distinct GPUs."""
+    import socket
+    info = {"rank": rank, "host": socket.gethostname(), "pid": os.getpid(),
+            "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
+            "visible": next((os.environ[k] for k in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES",
+                                                      "CUDA_VISIBLE_DEVICES") if os.environ.get(k)), None)}
+    if dev.type == "cuda":
+        p = torch.cuda.get_device_properties(dev)
+        info.update(device=f"{p.name} ({getattr(p, 'gcnArchName', '?')})", device_index=dev.index,
+                    uuid=str(getattr(p, "uuid", "")),
+                    pci_bus_id="%04x:%02x:%02x" % (getattr(p, "pci_domain_id", 0), getattr(p, "pci_bus_id", 0),
+                                                   getattr(p, "pci_device_id", 0)))
+    else:
+        info.update(device="cpu", device_index=None, uuid=f"cpu:{info['host']}:{info['pid']}", pci_bus_id=None)
+    return info
+
+
+def gather_topology(dist, rank: int, dev: torch.device, rings: list, transport: str, gpu: bool,
+                    p2p=None) -> dict:
+    """World size / backend of the process group, every rank's identity and the transport of
+    every ring edge, gathered to all ranks. Raises when RCCL ranks share a device (a mis-set
+    HIP_VISIBLE_DEVICES would otherwise pass as an N-GPU measurement)."""
+    me = rank_identity(rank, dev)
+    if dist is not None:
+        allr = [None] * dist.get_world_size()
+        dist.all_gather_object(allr, me)
+        world, backend = dist.get_world_size(), str(dist.get_backend())
+    else:
+        allr, world, backend = [me], 1, None
+    edges = {}
+    for ring in rings:
+        for i in range(len(ring) if len(ring) > 1 else 0):
+            a, b = ring[i], ring[(i + 1) % len(ring)]
+            kind = "ipc" if transport == "ipc" and gpu else ("rccl" if gpu else "gloo")
+            edges[f"{a}->{b}"] = kind
+    if p2p is not None and getattr(p2p, "alloc_kinds", None):
+        edges["ipc_alloc"] = sorted(set(str(v) for v in p2p.alloc_kinds.values()))
+    uuids = [r["uuid"] for r in allr]
+    distinct = len(set(uuids)) == len(uuids)
+    shared_ok = gpu and transport == "ipc" and torch.cuda.device_count() < world  # 1-GPU IPC rehearsal
+    if gpu and not distinct and not shared_ok:
+        dup = sorted({u for u in uuids if uuids.count(u) > 1})
+        raise RuntimeError(f"[ERROR] {world} ranks but only {len(set(uuids))} distinct GPUs (shared: {dup}); "
+                           f"check HIP_VISIBLE_DEVICES / LOCAL_RANK")
+    return {"world_size": world, "backend": backend, "distinct_devices": distinct,
+            "shared_gpu_rehearsal": bool(shared_ok and not distinct),
+            "ranks": [{k: r[k] for k in ("rank", "host", "device_index", "uuid", "pci_bus_id", "visible")} for r in allr],
+            "edges": edges}
+
+
 def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int = 64, warmup: int = 8,
                          batch: int = 16, prompt_len: int = 128, max_seq: int = 0,
                          microbatches: int = 0, seed: int = 0, use_graph: bool = True,
@@ -792,6 +845,12 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
             print(f"[bench] preflight (us per ring edge): {preflight}", flush=True)
     if startup_wd is not None:
         startup_wd.cancel()
+    # which devices the ranks really hold (asserted distinct for RCCL before anything is timed)
+    topology = gather_topology(dist, rank, dev, rings, transport if pp > 1 else "local", gpu,
+                               p2p if ipc_only else None)
+    if verbose and rank == 0 and world > 1:
+        print(f"[bench] ranks on devices: {[(r['rank'], r['pci_bus_id'] or r['uuid']) for r in topology['ranks']]} "
+              f"edges {topology['edges']}", flush=True)
     t0 = time.perf_counter()
     stage = PipelineStage(cfg, srank, pp, st.start, st.end, dev, batch, M, max_seq,
                           RandomSource(cfg, seed), use_graph=use_graph,
@@ -911,6 +970,7 @@ def run_decode_benchmark(model: str = "llama2-7b", n_gpus: int = 1, steps: int =
         "tokens_mb0": tokens_mb0,  # rank 0 only when it holds the history (1 stage or split head)
         "transport": transport if pp > 1 else None,
         "preflight_us": preflight or None,
+        "topology": topology,
         "b1_p50_tpot_ms": lat_p50 if latency_steps > 0 else None,
         "b1_tok_s": (dp * latency_steps / lat_el) if latency_steps > 0 and lat_el > 0 else None,
         "mid_batch": mid_batch or None,

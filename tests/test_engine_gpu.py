@@ -6,14 +6,12 @@ from llm_sharding_amd.config import LlamaConfig, tiny
 from llm_sharding_amd.models import weights as W
 from llm_sharding_amd.models.reference import ReferenceLlama
 from llm_sharding_amd.runtime.engine import DecodeGraph, RandomSource, StageEngine
+from llm_sharding_amd.utils.numerics import rel_err  # global + per-16x16-tile + per-row
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-def rel_err(a, b):
-    a, b = a.float().cpu(), b.float().cpu()
-    return ((a - b).norm() / (b.norm() + 1e-12)).item()
 
 
 def _ref(cfg, seed, n_layers=None):

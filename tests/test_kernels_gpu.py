@@ -6,6 +6,7 @@ import torch
 import torch.nn.functional as F
 
 from llm_sharding_amd.ops import packing
+from llm_sharding_amd.utils.numerics import rel_err  # global + per-16x16-tile + per-row
 
 pytestmark = pytest.mark.gpu
 
@@ -18,9 +19,6 @@ def hip():
     return h
 
 
-def rel_err(a, b):
-    a, b = a.float(), b.float()
-    return ((a - b).norm() / (b.norm() + 1e-12)).item()
 
 
 def _rnd(*shape, scale=1.0, gen=None):

@@ -10,6 +10,7 @@ from hypothesis import HealthCheck, given, settings
 from hypothesis import strategies as st
 
 from llm_sharding_amd.ops import packing
+from llm_sharding_amd.utils.numerics import rel_err  # global + per-16x16-tile + per-row
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -22,9 +23,6 @@ def hip():
     return h
 
 
-def rel(a, b):
-    a, b = a.float(), b.float()
-    return ((a - b).norm() / (b.norm() + 1e-12)).item()
 
 
 @SET
@@ -45,7 +43,7 @@ def test_projection_random_shapes(M, nt, kc, norm, resid):
     wp = packing.pack_b(packing.fold_norm(w, g) if norm else w)
     ep = h.make_epi(out=out, resid=out if resid else None, ldo=N, ldr=N)
     h.gemv(x, wp, M, N, K, h.EPI_RESID if resid else h.EPI_STORE, ep, norm=norm)
-    assert rel(out, ref) < 1e-2
+    assert rel_err(out, ref) < 1e-2
 
 
 @SET
@@ -57,7 +55,7 @@ def test_gemm_random_shapes(M, nt, kc):
     w = (torch.randn(N, K, device=DEV) * 0.05).to(torch.bfloat16)
     out = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
     h.gemm(a, packing.pack_b(w), M, N, K, h.EPI_STORE, h.make_epi(out=out, ldo=N))
-    assert rel(out, a.float() @ w.float().T) < 1e-2
+    assert rel_err(out, a.float() @ w.float().T) < 1e-2
 
 
 @SET
@@ -83,7 +81,7 @@ def test_decode_attention_random(rows, heads, T, nsplit):
         Vr = vc[r, :, :t].float().repeat_interleave(g, 0)
         p = torch.softmax(q[r].float().view(nh, 1, hd) @ Kr.transpose(1, 2) / math.sqrt(hd), -1)
         ref[r] = (p @ Vr).reshape(-1)
-    assert rel(out, ref) < 1e-2
+    assert rel_err(out, ref) < 1e-2
 
 
 @SET
@@ -111,4 +109,4 @@ def test_flash_prefill_random(segs, heads, causal):
         Vr = vc[slot[r], :, :t].float().repeat_interleave(g, 0)
         p = torch.softmax(q[r].float().view(nh, 1, hd) @ Kr.transpose(1, 2) / math.sqrt(hd), -1)
         ref[r] = (p @ Vr).reshape(-1)
-    assert rel(out, ref) < 1e-2
+    assert rel_err(out, ref) < 1e-2

@@ -7,11 +7,9 @@ import torch
 from llm_sharding_amd.models import weights as W
 from llm_sharding_amd.models.reference import ReferenceLlama, rmsnorm
 from llm_sharding_amd.utils.shard_loader import LlamaShardPart
+from llm_sharding_amd.utils.numerics import rel_err  # global + per-16x16-tile + per-row
 
 
-def _rel(a, b):
-    a, b = a.float().cpu(), b.float().cpu()
-    return ((a - b).norm() / (b.norm() + 1e-12)).item()
 
 
 def _check(shards, device, dtype, tol):
@@ -27,17 +25,17 @@ def _check(shards, device, dtype, tol):
     b = LlamaShardPart(shards, [f"block_{i}.pth" for i in range(2, L)], 2, L, device=device, dtype=dtype,
                        add_final_norm=True, final_norm_weight="final_norm.pth")
     h = a(x.to(device, dtype))
-    assert _rel(h, want_mid) < tol
+    assert rel_err(h, want_mid) < tol
     out = b(h)
     assert out.shape == (1, 6, cfg.hidden_size)
-    assert _rel(out, want_all) < tol
+    assert rel_err(out, want_all) < tol
     # incremental decode through the KV-cache handles: prefill 5 tokens, then the 6th alone
     ca, cb = a.new_cache(1), b.new_cache(1)
     ha = a(x[:, :5].to(device, dtype), past_key_value=ca)
     b(ha, past_key_value=cb)
     assert ca.get_seq_length() == 5 and cb.get_seq_length() == 5
     last = b(a(x[:, 5:].to(device, dtype), past_key_value=ca), past_key_value=cb)
-    assert _rel(last[0, -1], want_all[0, -1]) < tol
+    assert rel_err(last[0, -1], want_all[0, -1]) < tol
 
 
 def test_shard_part_cpu(tiny_shards):
