@@ -57,10 +57,13 @@ def build(force: bool = False, jobs: int = 8, arch: str = "gfx950", verbose: boo
     hipcc = _hipcc()
     kernel_srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
     comm_srcs = sorted(glob.glob(os.path.join(CSRC, "comm", "*.cpp")))
-    # -fno-slp-vectorize: no packed-FP32 VALU formed from scalar code. ROCm 7.2's hipcc issued a
-    # v_pk_fma_f32 right behind the 32-bit VALU writes of its source pair with no wait state, and
-    # that kernel computed wrong rows nondeterministically on MI355X (profiles/r5_gemv_nondeterminism.md);
-    # csrc/isa_audit.py checks the linked library for the pattern after every build.
+    # -fno-slp-vectorize: no packed-FP32 VALU formed from scalar code (the remaining packed FP32
+    # comes from explicit vector code). Packed FP32 beside MFMAs is an anti-lever
+    # (MI355X_MICROARCH.md, filler prices; batch 1 -4.3 %: profiles/r5_slp_ab.md), and an SLP build
+    # of the round-5 shared GEMV body computed wrong rows (profiles/r5_gemv_nondeterminism.md). The
+    # SLP and no-SLP libraries differ bitwise only in the decode attention kernels, by FMA
+    # contraction (profiles/r6_isa_hazards.md). csrc/isa_audit.py checks the linked library for
+    # back-to-back hazards (rules measured on the hardware) after every build.
     hip_flags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={arch}", "-Wall",
                  "-Wno-unused-function", "-munsafe-fp-atomics", "-fno-slp-vectorize"]
     # a change of the compile flags rebuilds every object (the flags are part of the stamp)
@@ -106,10 +109,11 @@ def build(force: bool = False, jobs: int = 8, arch: str = "gfx950", verbose: boo
         if res["code_objects"] == 0:  # an audit that checked nothing must not pass (advisor round 5)
             raise RuntimeError(f"ISA audit of {klib}: no {arch} code object found in the library's offload bundle")
         if res["findings"]:
-            raise RuntimeError(f"ISA audit of {klib}: {len(res['findings'])} VALU -> packed-FP32 back-to-back "
-                               f"dependencies, e.g. {res['findings'][:3]} (csrc/isa_audit.py)")
+            raise RuntimeError(f"ISA audit of {klib}: back-to-back hazards {res['by_rule']}, e.g. "
+                               f"{res['findings'][:3]} (csrc/isa_audit.py)")
         with open(audit_stamp, "w") as f:
-            f.write(f"{res['code_objects']} code objects, {res['packed_fp32_instructions']} packed FP32, 0 findings\n")
+            f.write(f"{res['code_objects']} code objects, {res['packed_fp32_instructions']} packed FP32 (explicit "
+                    f"vector code), 0 findings under rules {sorted(res['by_rule'])}\n")
     out["kernels"] = klib
     clib = os.path.join(OUT, "liblsa_comm.so")
     if cobjs and (force or not os.path.exists(clib) or

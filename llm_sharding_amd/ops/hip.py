@@ -57,7 +57,15 @@ def lib() -> ctypes.CDLL:
         raise RuntimeError(
             f"HIP kernel library not built: {KERNELS_SO} missing. Run `python csrc/build.py` "
             "(or __graft_entry__.build()).")
-    L = ctypes.CDLL(KERNELS_SO, mode=ctypes.RTLD_GLOBAL)
+    _lib = load_library(KERNELS_SO, ctypes.RTLD_GLOBAL)
+    return _lib
+
+
+def load_library(path: str, mode: int = ctypes.RTLD_LOCAL) -> ctypes.CDLL:
+    """Load one build of the kernel library with every entry point's signature declared.
+    Two builds can live in one process when both are loaded RTLD_LOCAL (each resolves its own
+    kernels; scripts/slp_kernel_diff.py runs every kernel of a step from both)."""
+    L = ctypes.CDLL(path, mode=mode)
     vp, i, f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
     L.lsa_gemv.argtypes = [vp, i, vp, vp, i, i, i, i, f, i, ctypes.POINTER(EpiArgs), i, i, i, vp]
     L.lsa_gemv_coop.argtypes = [vp, i, vp, vp, i, i, i, i, f, i, ctypes.POINTER(EpiArgs), i, i, i, i, i, i, vp, vp, vp]
@@ -86,7 +94,6 @@ def lib() -> ctypes.CDLL:
     if os.environ.get("LSA_ATTN_SMALL_MAX_WGS"):  # A/B runs of the small-grid decode attention's range
         L.lsa_attn_set_small_max_wgs.argtypes = [i]
         _check(L.lsa_attn_set_small_max_wgs(int(os.environ["LSA_ATTN_SMALL_MAX_WGS"])), "lsa_attn_set_small_max_wgs")
-    _lib = L
     return L
 
 

@@ -27,8 +27,13 @@ WRITERS = {
     "dpp_lo": "v_mov_b32_dpp v40, %[e] quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf",
     "trans_lo": "v_exp_f32 v40, %[e]",
     "cvt_pk_lo": "v_cvt_pk_bf16_f32 v40, %[e], %[e]",
-    "pk_add": "v_pk_add_f32 v[40:41], v[40:41], v[42:43]",
+    "and_hi": "v_and_b32 v41, 0xffff0000, %[e]",
     "mov_lo": "v_mov_b32 v40, %[e]",
+    "pk_add": "v_pk_add_f32 v[40:41], v[40:41], v[42:43]",
+    "pk_fma_acc": "v_pk_fma_f32 v[40:41], v[42:43], v[42:43], v[40:41]",
+    # the round-5 GEMV site: both halves of the pair updated by 32-bit FMAs, then the packed read
+    "fma_lo_hi": "v_fma_f32 v40, v42, v42, v40\\n v_fma_f32 v41, v43, v43, v41",
+    "rsq_lo": "v_rsq_f32 v40, %[e]",
 }
 READERS = {
     "pk_add": "v_pk_add_f32 v[44:45], v[40:41], v[42:43]",
@@ -59,12 +64,22 @@ def seq(w, g, r):
 def gen() -> list:
     cases = list(itertools.product(WRITERS, GAPS, READERS))
     out = ['#include <hip/hip_runtime.h>', '#include <cstdio>', '#include <vector>', '#include <cstring>', '']
+    out.append('typedef float f32x4 __attribute__((ext_vector_type(4)));')
+    out.append('typedef unsigned u32x4 __attribute__((ext_vector_type(4)));')
+    out.append('typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));')
     out.append('#define CLOB "v40","v41","v42","v43","v44","v45","v46","v47","v48","v49","v50"')
     for ci, (w, g, r) in enumerate(cases):
         hz = seq(WRITERS[w], GAPS[g], READERS[r])
         sf = seq(WRITERS[w], SAFE, READERS[r])
-        out.append(f"""__global__ void case_{ci}(const float* __restrict__ in, unsigned* __restrict__ bad, int iters) {{
+        out.append(f"""__global__ void case_{ci}(const float* __restrict__ in, unsigned* __restrict__ bad, int iters, int partner) {{
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (partner && (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) & 1)) {{  // MFMA-issuing partner wave
+    f32x4 acc = {{0.f, 0.f, 0.f, 0.f}};
+    bf16x8 x = __builtin_bit_cast(bf16x8, u32x4{{(unsigned)i, 3u, 5u, 7u}});
+    for (int it = 0; it < iters * 16; ++it) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x, x, acc, 0, 0, 0);
+    bad[i] = acc[0] == 1234.5f ? 1u : 0u;
+    return;
+  }}
   unsigned nb = 0;
   for (int it = 0; it < iters; ++it) {{
     const float a = in[(i * 5 + it * 7) & 4095], b = in[(i * 3 + it * 11 + 1) & 4095], c = in[(i + it * 13 + 2) & 4095],
@@ -78,7 +93,7 @@ def gen() -> list:
   }}
   bad[i] = nb;
 }}""")
-    out.append("typedef void (*KFn)(const float*, unsigned*, int);")
+    out.append("typedef void (*KFn)(const float*, unsigned*, int, int);")
     out.append("static const KFn KS[] = {" + ", ".join(f"case_{i}" for i in range(len(cases))) + "};")
     out.append("static const char* NAMES[] = {" + ", ".join(f'"{w} {g} {r}"' for w, g, r in cases) + "};")
     out.append(f"""int main() {{
@@ -92,19 +107,23 @@ def gen() -> list:
   hipMalloc(&dbad, MAXT * 4);
   hipMemcpy(din, h.data(), N * 4, hipMemcpyHostToDevice);
   std::vector<unsigned> hb(MAXT);
-  // (blocks, threads): one wave per SIMD (1024 x 64) and 8 waves per SIMD (1024 x 512)
-  const int cfg[2][2] = {{{{1024, 64}}, {{1024, 512}}}};
+  // (blocks, threads, partner): one wave per SIMD (1024 x 64), 8 waves per SIMD (1024 x 512), and
+  // 8 waves per SIMD where every other wave issues MFMAs instead (the GEMV's two-waves-per-SIMD
+  // neighbourhood)
+  const int cfg[3][3] = {{{{1024, 64, 0}}, {{1024, 512, 0}}, {{1024, 512, 1}}}};
   for (int c = 0; c < {len(cases)}; ++c) {{
-    unsigned long long tot[2] = {{0, 0}}, tested[2] = {{0, 0}};
-    for (int k = 0; k < 2; ++k) {{
+    unsigned long long tot[3] = {{0, 0, 0}}, tested[3] = {{0, 0, 0}};
+    for (int k = 0; k < 3; ++k) {{
       const int nb = cfg[k][0], nt = cfg[k][1];
-      hipLaunchKernelGGL(KS[c], dim3(nb), dim3(nt), 0, 0, din, dbad, ITERS);
+      hipLaunchKernelGGL(KS[c], dim3(nb), dim3(nt), 0, 0, din, dbad, ITERS, cfg[k][2]);
       if (hipDeviceSynchronize() != hipSuccess) {{ printf("case %d failed\\n", c); return 2; }}
       hipMemcpy(hb.data(), dbad, (size_t)nb * nt * 4, hipMemcpyDeviceToHost);
       for (int i = 0; i < nb * nt; ++i) tot[k] += hb[i];
-      tested[k] = 2ull * nb * nt * ITERS;
+      tested[k] = 2ull * nb * nt * ITERS / (cfg[k][2] ? 2 : 1);
+      if (cfg[k][2]) {{ tot[k] = 0; for (int q = 0; q < nb * nt; ++q) if (((q % nt) >> 6) % 2 == 0) tot[k] += hb[q]; }}
     }}
-    printf("%-40s 1w/SIMD %llu/%llu  8w/SIMD %llu/%llu\\n", NAMES[c], tot[0], tested[0], tot[1], tested[1]);
+    printf("%-40s 1w/SIMD %llu/%llu  8w/SIMD %llu/%llu  4w+4mfma/SIMD %llu/%llu\\n", NAMES[c], tot[0], tested[0], tot[1],
+           tested[1], tot[2], tested[2]);
   }}
   hipFree(din); hipFree(dbad);
   return 0;

@@ -4,9 +4,11 @@ tests/fixtures/full_depth_7b.json; tests/test_fixture_fresh.py compares it with 
 import glob
 import hashlib
 import os
+import re
 
 NUMERICS_FILES = ("csrc/kernels/*.hip", "csrc/kernels/*.h", "llm_sharding_amd/ops/*.json", "llm_sharding_amd/ops/hip.py",
-                  "llm_sharding_amd/ops/packing.py", "llm_sharding_amd/runtime/engine.py", "csrc/build.py")
+                  "llm_sharding_amd/ops/packing.py", "llm_sharding_amd/runtime/engine.py")
+FLAGS_RE = re.compile(r"hip_flags = \[[^\]]*\]", re.S)  # csrc/build.py's compile flags (not its comments)
 
 
 def tree_hash(root: str) -> str:
@@ -16,4 +18,6 @@ def tree_hash(root: str) -> str:
             h.update(os.path.relpath(p, root).encode())
             with open(p, "rb") as fh:
                 h.update(fh.read())
+    with open(os.path.join(root, "csrc", "build.py")) as fh:
+        h.update(FLAGS_RE.search(fh.read()).group(0).encode())
     return h.hexdigest()[:16]
