@@ -20,6 +20,8 @@ from typing import Optional, Tuple
 
 import torch
 
+from . import routes
+
 NATIVE_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_native")
 # LSA_KERNELS_SO: load another build of the kernel library (A/B runs of build flags only; the
 # product and every test use the in-tree _native/liblsa_kernels.so)
@@ -84,10 +86,11 @@ def load_library(path: str, mode: int = ctypes.RTLD_LOCAL) -> ctypes.CDLL:
     L.lsa_argmax_finalize.argtypes = [vp, i, vp, vp, i, vp, i, i, vp, vp]
     L.lsa_pos_advance.argtypes = [vp, i, i, vp]
     L.lsa_gemm_wr.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(EpiArgs), i, i, vp]
+    L.lsa_gemm_w4.argtypes = [vp, i, vp, i, i, i, ctypes.POINTER(EpiArgs), i, i, vp]
     L.lsa_gemm_sk.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(EpiArgs), i, i, i, i, i, i, i, vp, vp, ctypes.c_longlong, i,
                               vp]
     for name in ("lsa_gemv", "lsa_gemv_coop", "lsa_gemv_fp8", "lsa_dequant_fp8_packed", "lsa_gemv_coop_fp8", "lsa_gemm",
-                 "lsa_gemm_sk", "lsa_gemm_wr", "lsa_attn_decode", "lsa_attn_prefill", "lsa_embed", "lsa_rmsnorm", "lsa_layernorm",
+                 "lsa_gemm_sk", "lsa_gemm_wr", "lsa_gemm_w4", "lsa_attn_decode", "lsa_attn_prefill", "lsa_embed", "lsa_rmsnorm", "lsa_layernorm",
                  "lsa_resid_rmsnorm_partials", "lsa_row_ss",
                  "lsa_argmax_finalize", "lsa_pos_advance", "lsa_version"):
         getattr(L, name).restype = ctypes.c_int
@@ -375,18 +378,9 @@ SK_BM = 256  # gemm_sk.hip row tile (default; 128-row tiles for small / odd M: p
 # A range starting at 193 rows covers the same 2-row-tile grid as its measured 256-row point.
 # (70B qkv, 10240 x 8192, measured a tie at 384 rows and slower at 448: not routed.)
 # LSA_GEMM_WR=0 turns the route off (A/B runs).
-WR_ROUTES = {
-    (12288, 4096): [(193, 256, 128), (320, 512, 192)],
-    (15360, 5120): [(193, 256, 128), (320, 384, 192), (448, 512, 256)],
-    (5120, 3072): [(193, 512, 128)],
-    (16384, 3072): [(193, 256, 128), (320, 512, 256)],
-    (22016, 4096): [(193, 256, 256)],
-    (27648, 5120): [(193, 256, 256)],
-}
-
-
 def gemm_wr_plan(M: int, N: int, K: int, epi: int, ep: "EpiArgs") -> Optional[int]:
-    """bn for :func:`gemm_wr`, or None when gemm_sk takes the shape."""
+    """bn for :func:`gemm_wr`, or None when gemm_sk takes the shape (the route table:
+    ops/routes.py)."""
     if os.environ.get("LSA_GEMM_WR", "1") == "0" or ep.act or ep.bias or ep.ss_out:
         return None
     if epi not in (EPI_STORE, EPI_QKV, EPI_SWIGLU):
@@ -396,9 +390,12 @@ def gemm_wr_plan(M: int, N: int, K: int, epi: int, ep: "EpiArgs") -> Optional[in
     # 128-row plans do not (measured at 448 and 512 rows)
     if M - (mt - 1) * 128 < 64:
         return None
-    for lo, hi, bn in WR_ROUTES.get((N, K), ()):
-        if lo <= M <= hi and N % bn == 0 and K % 64 == 0 and not (epi == EPI_SWIGLU and bn == 192):
-            return bn
+    r = routes.route(M, N, K, epi)
+    if r.kernel != "gemm_wr":
+        return None
+    bn = r.params["bn"]
+    if N % bn == 0 and K % 64 == 0 and not (epi == EPI_SWIGLU and bn == 192):
+        return bn
     return None
 
 
@@ -419,6 +416,19 @@ def gemm_wr(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int,
     _check_epi(epi, ep, N)
     rc = lib().lsa_gemm_wr(_p(a), a.stride(0), _p(wp), M, N, K, epi, ctypes.byref(ep), bn, grid or N_CU, _stream())
     _check(rc, "lsa_gemm_wr")
+
+
+def gemm_w4(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, ep: EpiArgs, grid: int = 0,
+            variant: int = 0) -> None:
+    """Plain-store projection GEMM on the one-wave-per-SIMD 256 x 256 kernel (gemm_w4.hip).
+    N % 256 == 0, K % 64 == 0."""
+    _req(_is_bf16_cuda(a, wp), "gemm_w4: bf16 cuda tensors required")
+    _req(wp.numel() == N * K and K % 64 == 0 and N % 256 == 0, "gemm_w4: packed weight shape (N % 256, K % 64)")
+    _req(a.dim() == 2 and a.shape[0] >= M >= 1 and a.shape[1] >= K and a.stride(1) == 1 and a.stride(0) % 8 == 0
+         and a.data_ptr() % 16 == 0, "gemm_w4: A must be [>=M, >=K] row-major with 16-B aligned rows")
+    _req(ep.out is not None, "gemm_w4: out")
+    rc = lib().lsa_gemm_w4(_p(a), a.stride(0), _p(wp), M, N, K, ctypes.byref(ep), grid, variant, _stream())
+    _check(rc, "lsa_gemm_w4")
 
 
 class SkWorkspace:

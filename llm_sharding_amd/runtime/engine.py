@@ -176,12 +176,9 @@ def keys_max_torch(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
 class StageEngine:
     DECODE_MAX_ROWS = packing.GEMV_MAX_ROWS  # rows handled by the decode attention / graph paths (128)
     # rows above which the projections run on the MFMA GEMMs instead of the weight-streaming GEMVs
+    # (per instance: the route table, ops/routes.py, may send a model's 65-128-row decode to the
+    # MFMA GEMMs - Llama-2-13B, profiles/r5_gemv_max_rows_ab.md; LSA_GEMV_MAX_ROWS overrides)
     GEMV_MAX_ROWS = int(os.environ.get("LSA_GEMV_MAX_ROWS", str(packing.GEMV_MAX_ROWS)))
-    # (hidden, intermediate) of the models whose 65-128-row decode steps measured faster on the
-    # MFMA GEMMs than on the coop GEMV: Llama-2-13B's batch-128 step -5 % on two boxes; the 7B
-    # (+6 %), 3B (+65 %) and 70B stage (+6-10 %) stay on the GEMV (profiles/r5_gemv_max_rows_ab.md).
-    # LSA_GEMV_MAX_ROWS overrides.
-    MID_GEMM_SHAPES = frozenset({(5120, 13824)})
     # split-KV chunks never shorter than this many keys: below ~256 keys per split the merge
     # costs more than the extra parallelism buys (profiles/r1_bench_kernels_sweep.jsonl, attn)
     ATTN_MIN_CHUNK = int(os.environ.get("LSA_ATTN_MIN_CHUNK", "256"))  # keys per decode split, at least
@@ -196,8 +193,9 @@ class StageEngine:
         self.cfg = cfg
         self.start, self.end = start, end
         self.n_layers = end - start
-        if "LSA_GEMV_MAX_ROWS" not in os.environ and (cfg.hidden_size, cfg.intermediate_size) in self.MID_GEMM_SHAPES:
-            self.GEMV_MAX_ROWS = 64
+        if "LSA_GEMV_MAX_ROWS" not in os.environ:  # the class value (env / tests) bounds the route table's
+            from ..ops import routes
+            self.GEMV_MAX_ROWS = min(type(self).GEMV_MAX_ROWS, routes.gemv_max_rows(self.proj_shapes(cfg)))
         self.device = torch.device(device)
         self.gpu = _is_gpu(self.device)
         if self.gpu and dtype != torch.bfloat16:
@@ -238,6 +236,12 @@ class StageEngine:
             self.load()
 
     # ------------------------------------------------------------------------- loading
+    @staticmethod
+    def proj_shapes(cfg: LlamaConfig) -> list:
+        """(N, K) of a layer's four projections: qkv, o, gate_up (or GPT-2's c_fc), down."""
+        return [(cfg.qkv_size, cfg.hidden_size), (cfg.hidden_size, cfg.q_size),
+                (cfg.mlp_in_size, cfg.hidden_size), (cfg.hidden_size, cfg.intermediate_size)]
+
     def _log(self, msg: str) -> None:
         if self.verbose:
             print(msg, flush=True)

@@ -15,6 +15,55 @@ import torch
 BACKENDS = ("tcp", "rccl", "local")
 
 
+# Every LSA_* switch in the package, kernels and entry points, in one place.
+# kind: "env" (read at run time) or "define" (a -D compile flag of csrc/kernels, never set by
+# csrc/build.py: only probe builds under probe_bin/ use them). role: "product" (changes what a
+# deployment runs or how it reports), "diagnostic" (A/B and ablation switches; the default is the
+# shipped behaviour, measured in the profile named), "test" (test harness only).
+# tests/test_runtime_config.py::test_every_lsa_knob_is_listed keeps this table complete.
+KNOBS = {
+    # ---- product
+    "LSA_LOG_LEVEL": ("env", "product", "INFO", "log level of utils/log.py"),
+    "LSA_LOG_JSON": ("env", "product", "", "1 = JSON log lines"),
+    "LSA_TRACE": ("env", "product", "", "directory for per-rank Chrome-trace timelines (bench --trace, serve)"),
+    "LSA_DIST_TIMEOUT_S": ("env", "product", "300", "torch.distributed collective timeout of the pipeline"),
+    "LSA_STARTUP_TIMEOUT_S": ("env", "product", "180", "RCCL bring-up watchdog (exit PREFLIGHT_EXIT when exceeded)"),
+    "LSA_PREFLIGHT_TIMEOUT_S": ("env", "product", "30", "per-edge receive timeout of the ring preflight"),
+    "LSA_IPC_TIMEOUT_S": ("env", "product", "30", "bounded spin of an IPC-ring hand-off before it poisons"),
+    "LSA_IPC_ALLOC": ("env", "product", "uncached", "IPC ring buffer kind: uncached | fine (coarse is refused across GPUs)"),
+    "LSA_PP_STREAMS": ("env", "product", "1", "pipeline: concurrent micro-batch streams per stage"),
+    "LSA_GRAPH_COMM": ("env", "product", "1", "capture IPC-ring hand-offs inside the decode hipGraph"),
+    "LSA_BENCH_ROLE": ("env", "product", "", "set by bench.py's supervisor for its worker process"),
+    "LSA_BENCH_FALLBACK": ("env", "product", "", "set by bench.py when it restarted on --transport ipc"),
+    "LSA_PARENT_PID": ("env", "product", "", "set by bench.py for its children (PR_SET_PDEATHSIG check)"),
+    # ---- diagnostic (A/B switches; defaults = the shipped routes)
+    "LSA_KERNELS_SO": ("env", "diagnostic", "_native/liblsa_kernels.so", "load another build of the kernel library"),
+    "LSA_GEMV_MAX_ROWS": ("env", "diagnostic", "128 (64 for MID_GEMM_SHAPES)",
+                          "rows up to which decode projections stay on the GEMVs (profiles/r5_gemv_max_rows_ab.md)"),
+    "LSA_GEMM_WR": ("env", "diagnostic", "1", "0 = no gemm_wr routes (profiles/r4_gemm_wr_engine_ab.txt)"),
+    "LSA_ATTN_MIN_CHUNK": ("env", "diagnostic", "256", "shortest split-KV chunk in keys"),
+    "LSA_ATTN_MFMA": ("env", "diagnostic", "1", "0 = no MFMA GQA decode kernel"),
+    "LSA_ATTN_MFMA_MIN_ITEMS": ("env", "diagnostic", "512", "rows x kv-heads from which GQA decode uses MFMA"),
+    "LSA_ATTN_GQA_NW": ("env", "diagnostic", "0", "waves of the GQA decode kernel (0 = planner)"),
+    "LSA_ATTN_SMALL_MAX_WGS": ("env", "diagnostic", "", "grid size limit of the small-grid decode attention"),
+    "LSA_PREFLIGHT_FAULT": ("env", "diagnostic", "", "fault injection: 'a->b' drops the preflight message of edge a->b"),
+    "LSA_SK_ABLATE": ("define", "diagnostic", "0", "gemm_sk ablation builds (scripts/sk_ablate.py)"),
+    "LSA_COOP_ABLATE": ("define", "diagnostic", "0", "coop GEMV ablation builds"),
+    "LSA_GEMM_STAMPS": ("define", "diagnostic", "", "gemm_sk per-phase s_memrealtime stamps"),
+    "LSA_COOP_STAMPS": ("define", "diagnostic", "", "coop GEMV per-phase stamps"),
+    # ---- tests
+    "LSA_RECORD_FULL_DEPTH": ("env", "test", "", "1 = record tests/fixtures/full_depth_7b.json instead of checking it"),
+    "LSA_FULL_DEPTH_FIXTURE": ("env", "test", "tests/fixtures/full_depth_7b.json", "where the full-depth fixture lives"),
+    "LSA_VARIANT_SLP": ("env", "diagnostic", "", "scripts/probes/build_kernels_variant.sh: build with SLP on"),
+}
+
+
+def knobs_in_effect() -> dict:
+    """The run-time knobs set in this process's environment (for logs / bench lines)."""
+    import os
+    return {k: os.environ[k] for k, v in KNOBS.items() if v[0] == "env" and k in os.environ}
+
+
 @dataclass
 class RuntimeConfig:
     model: str = "llama2-7b"      # preset for random-init weights (when no shards are given)
