@@ -86,11 +86,10 @@ def load_library(path: str, mode: int = ctypes.RTLD_LOCAL) -> ctypes.CDLL:
     L.lsa_argmax_finalize.argtypes = [vp, i, vp, vp, i, vp, i, i, vp, vp]
     L.lsa_pos_advance.argtypes = [vp, i, i, vp]
     L.lsa_gemm_wr.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(EpiArgs), i, i, vp]
-    L.lsa_gemm_w4.argtypes = [vp, i, vp, i, i, i, ctypes.POINTER(EpiArgs), i, i, vp]
     L.lsa_gemm_sk.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(EpiArgs), i, i, i, i, i, i, i, vp, vp, ctypes.c_longlong, i,
                               vp]
     for name in ("lsa_gemv", "lsa_gemv_coop", "lsa_gemv_fp8", "lsa_dequant_fp8_packed", "lsa_gemv_coop_fp8", "lsa_gemm",
-                 "lsa_gemm_sk", "lsa_gemm_wr", "lsa_gemm_w4", "lsa_attn_decode", "lsa_attn_prefill", "lsa_embed", "lsa_rmsnorm", "lsa_layernorm",
+                 "lsa_gemm_sk", "lsa_gemm_wr", "lsa_attn_decode", "lsa_attn_prefill", "lsa_embed", "lsa_rmsnorm", "lsa_layernorm",
                  "lsa_resid_rmsnorm_partials", "lsa_row_ss",
                  "lsa_argmax_finalize", "lsa_pos_advance", "lsa_version"):
         getattr(L, name).restype = ctypes.c_int
@@ -416,19 +415,6 @@ def gemm_wr(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, epi: int,
     _check_epi(epi, ep, N)
     rc = lib().lsa_gemm_wr(_p(a), a.stride(0), _p(wp), M, N, K, epi, ctypes.byref(ep), bn, grid or N_CU, _stream())
     _check(rc, "lsa_gemm_wr")
-
-
-def gemm_w4(a: torch.Tensor, wp: torch.Tensor, M: int, N: int, K: int, ep: EpiArgs, grid: int = 0,
-            variant: int = 0) -> None:
-    """Plain-store projection GEMM on the one-wave-per-SIMD 256 x 256 kernel (gemm_w4.hip).
-    N % 256 == 0, K % 64 == 0."""
-    _req(_is_bf16_cuda(a, wp), "gemm_w4: bf16 cuda tensors required")
-    _req(wp.numel() == N * K and K % 64 == 0 and N % 256 == 0, "gemm_w4: packed weight shape (N % 256, K % 64)")
-    _req(a.dim() == 2 and a.shape[0] >= M >= 1 and a.shape[1] >= K and a.stride(1) == 1 and a.stride(0) % 8 == 0
-         and a.data_ptr() % 16 == 0, "gemm_w4: A must be [>=M, >=K] row-major with 16-B aligned rows")
-    _req(ep.out is not None, "gemm_w4: out")
-    rc = lib().lsa_gemm_w4(_p(a), a.stride(0), _p(wp), M, N, K, ctypes.byref(ep), grid, variant, _stream())
-    _check(rc, "lsa_gemm_w4")
 
 
 class SkWorkspace:

@@ -54,11 +54,11 @@ step() {
       done ;;
     trace)
       [ $# -eq 0 ] && set -- --steps 20 --warmup 5
-      timeout -k 10 "$LIMIT" rocprofv3 --kernel-trace --stats -d "$OUT/trace$n" -o run -- python3 bench.py "$@" \
+      timeout -k 10 "$LIMIT" rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace$n" -o run -- python3 bench.py "$@" \
           > "$log" 2>&1 || rc=$? ;;
     pmc)
       local ctr=$1; shift
-      timeout -s KILL 120 rocprofv3 --pmc ${ctr//,/ } -d "$OUT/pmc$n" -o run -- python3 "$@" > "$log" 2>&1 || rc=$? ;;
+      timeout -s KILL 120 rocprofv3 --pmc ${ctr//,/ } --output-format csv -d "$OUT/pmc$n" -o run -- python3 "$@" > "$log" 2>&1 || rc=$? ;;
     py)
       timeout -k 10 "$LIMIT" python -u "$@" > "$log" 2>&1 || rc=$? ;;
     exe)

@@ -23,7 +23,7 @@
 // is in flight. Slot (s+3)%4 = (s-1)%4 is free: its fragments were read during s-2 and retired
 // (lgkmcnt(0)) before the barrier that ended s-2.
 // Reference op: the nn.Linear calls of HF LlamaDecoderLayer (/root/reference/utils/shard_loader.py:66-74).
-#include "epilogue.h"
+#include "../../csrc/kernels/epilogue.h"
 
 namespace {
 

@@ -2,7 +2,9 @@
 audit's rules, each rule flags its pattern (and not the same pattern one wait state apart), and
 the rules agree with the hardware: on the hazard probe's own ISA (scripts/probes/pk_hazard_gen.py)
 the trans and DPP rules flag exactly the cases that read stale values on an MI355X
-(profiles/r6_pk_hazard_probe.txt). CPU-only (the disassembler runs here)."""
+(profiles/r6_pk_hazard_probe.txt); and the bit_cast-of-a-vector-element miscompile behind the
+round-5 "fdot2" report is reproduced and kept out of the product kernels. CPU-only (the
+disassembler runs here)."""
 import os
 import re
 import shutil
@@ -97,3 +99,40 @@ def test_rules_match_the_hardware(tmp_path):
     assert by_hw_rules == stale, (sorted(stale - by_hw_rules), sorted(by_hw_rules - stale))
     pk_only = {c for c, r in flagged.items() if r == {"valu32->pk"}}
     assert pk_only and not (pk_only & stale)
+
+
+def test_product_kernels_avoid_the_bit_cast_element_miscompile():
+    """ROCm 7.2's hipcc reads element 0 for ``__builtin_bit_cast(T, v[k])`` when ``v`` is an
+    ext_vector and ``k`` a (constant) index: four fdot2 calls on the four dwords of a 16-byte
+    operand all read dword 0 (scripts/probes/fdot2_repro.hip, profiles/r6_fdot2_miscompile.md; the
+    round-5 persistent-chain probe hit it). Product kernels never bit_cast a single-subscript
+    element (copy it to a scalar first); the double-subscript uses (arrays OF vectors, e.g.
+    acc[i][j]) are whole objects and compile correctly."""
+    import glob
+    pat = re.compile(r"__builtin_bit_cast\(\s*[\w:]+\s*,\s*\w+\s*\[[^\]]+\]\s*\)")
+    hits = []
+    for p in glob.glob(os.path.join(ROOT, "csrc", "kernels", "*")):
+        hits += [(os.path.basename(p), m.group(0)) for m in pat.finditer(open(p).read())]
+    assert not hits, hits
+
+
+@pytest.mark.skipif(not shutil.which("/opt/rocm/bin/hipcc"), reason="hipcc not available")
+def test_fdot2_repro_isa(tmp_path):
+    """The minimal repro's ISA: the bit_cast kernel loads ONE dword per operand and feeds it to all four
+    v_dot2 (the miscompile); the pointer-punned kernel loads 16 bytes and uses four distinct dwords.
+    If a toolchain update fixes the bit_cast form this test says so (and the note can go)."""
+    s = str(tmp_path / "fdot2.s")
+    subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "--offload-arch=gfx950", "--cuda-device-only", "-S",
+                    os.path.join(ROOT, "scripts", "probes", "fdot2_repro.hip"), "-o", s], check=True, capture_output=True)
+    text = open(s).read()
+    bodies = re.split(r"^_Z\w+:", text, flags=re.M)
+    dots = {}
+    for name, body in zip(re.findall(r"^(_Z\w+):", text, flags=re.M), bodies[1:]):
+        dots[name] = re.findall(r"v_dot2c?_f32_bf16\S*\s+(v\d+),\s*(v\d+),\s*(v\d+)", body)
+    bc = next(v for k, v in dots.items() if "bitcast" in k)
+    pn = next(v for k, v in dots.items() if "punned" in k)
+    assert len(pn) == 4 and len({(a, b) for _, a, b in pn}) == 4, pn
+    assert len(bc) == 4
+    if len({(a, b) for _, a, b in bc}) == 4:
+        pytest.skip("this hipcc compiles the bit_cast form correctly (miscompile fixed)")
+    assert len({(a, b) for _, a, b in bc}) == 1, bc  # all four dot products on dword 0
