@@ -30,6 +30,7 @@ namespace {
 constexpr int W4_BM = 256, W4_BN = 256, W4_BK = 32, W4_NTHR = 256, W4_NS = 4;
 constexpr int W4_STAGE = (W4_BM + W4_BN) * W4_BK * 2;  // 32 KiB: 16 A fragments + 16 W fragments
 constexpr int W4_SMEM = W4_NS * W4_STAGE;              // 128 KiB
+constexpr int W4_GM = 16;                                // row tiles per group (tile order)
 
 LSA_DEVICE void w4_barrier() {
   __builtin_amdgcn_sched_barrier(0);
@@ -132,7 +133,16 @@ __global__ __launch_bounds__(W4_NTHR, 1) void gemm_w4_kernel(const bf16_raw* __r
   const unsigned char* Wb = reinterpret_cast<const unsigned char*>(Wp);
 
   for (int tile = g; tile < MT * NT; tile += G) {
-    const int mt = tile % MT, nt = tile / MT;  // row tiles fastest: tiles running together share W panels
+    // grouped order: W4_GM row tiles sweep all column tiles together, so one round of 256 tiles
+    // touches W4_GM A panels and every W panel (at M = 16,384: 32 + 32 MB, Infinity-Cache
+    // resident) instead of every A panel (128 MB, re-streamed from HBM once per column round)
+    int mt, nt;
+    {
+      const int per = W4_GM * NT, grp = tile / per, first = grp * W4_GM;
+      const int gm = min(W4_GM, MT - first), r = tile - grp * per;
+      mt = first + r % gm;
+      nt = r / gm;
+    }
     const int m0 = mt * W4_BM, n0 = nt * W4_BN;
     // DMA sources: A fragment w*4+p = rows m0 + (w*4+p)*16 + lane%16, 16-B chunk lane/16 of the
     // stage's 64 B; W fragment w*4+p = 16-col tile n0/16 + w*4 + p, the stage's 1 KiB block
