@@ -718,15 +718,22 @@ def gather_topology(dist, rank: int, dev: torch.device, rings: list, transport: 
             edges[f"{a}->{b}"] = kind
     if p2p is not None and getattr(p2p, "alloc_kinds", None):
         edges["ipc_alloc"] = sorted(set(str(v) for v in p2p.alloc_kinds.values()))
-    uuids = [r["uuid"] for r in allr]
-    distinct = len(set(uuids)) == len(uuids)
+    # a device is named by its PCI address where the runtime reports one, else by its UUID; a rank
+    # with neither (some runtimes report zeros) is not judged (distinct_devices: None)
+    def ident(r):
+        if r.get("pci_bus_id") and r["pci_bus_id"] != "0000:00:00":
+            return (r["host"], r["pci_bus_id"])
+        u = str(r.get("uuid") or "")
+        return (r["host"], u) if u.strip("0-") else None
+    ids = [ident(r) for r in allr]
+    distinct = None if any(i is None for i in ids) else len(set(ids)) == len(ids)
     shared_ok = gpu and transport == "ipc" and torch.cuda.device_count() < world  # 1-GPU IPC rehearsal
-    if gpu and not distinct and not shared_ok:
-        dup = sorted({u for u in uuids if uuids.count(u) > 1})
-        raise RuntimeError(f"[ERROR] {world} ranks but only {len(set(uuids))} distinct GPUs (shared: {dup}); "
+    if gpu and distinct is False and not shared_ok:
+        dup = sorted({str(i) for i in ids if ids.count(i) > 1})
+        raise RuntimeError(f"[ERROR] {world} ranks but only {len(set(ids))} distinct GPUs (shared: {dup}); "
                            f"check HIP_VISIBLE_DEVICES / LOCAL_RANK")
     return {"world_size": world, "backend": backend, "distinct_devices": distinct,
-            "shared_gpu_rehearsal": bool(shared_ok and not distinct),
+            "shared_gpu_rehearsal": bool(shared_ok and distinct is False),
             "ranks": [{k: r[k] for k in ("rank", "host", "device_index", "uuid", "pci_bus_id", "visible")} for r in allr],
             "edges": edges}
 

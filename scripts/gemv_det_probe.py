@@ -15,6 +15,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from llm_sharding_amd.ops import hip, packing  # noqa: E402
+from llm_sharding_amd.utils.numerics import rel_err  # noqa: E402
 
 ROWS = {1: (1, 16), 2: (17, 32), 4: (33, 44, 64)}
 
@@ -52,10 +53,13 @@ def run(lib_path=None, launches=3, n=1024, k=4096, seed=0, only=None):
                     raise RuntimeError(f"gemv rc {rc} at {(tn, mb, nw, u)} M={M}")
                 torch.cuda.synchronize()
                 outs.append(out)
-            errs = [((o.float() - ref).norm() / ref.norm()).item() for o in outs]
-            rowerr = ((outs[0].float() - ref).norm(dim=1) / ref.norm(dim=1))
-            rec = {"cfg": [tn, mb, nw, u], "M": M, "rel_err": max(errs), "worst_row": int(rowerr.argmax()),
-                   "worst_row_err": round(float(rowerr.max()), 5),
+            # every launch: global + worst-tile + worst-row error (utils/numerics.py): the worst row is
+            # BOUNDED (3 x 8e-3), not only reported - one wrong row of a 64-row output passes a global gate
+            errs = [rel_err(o, ref) for o in outs]
+            worst = max(errs, key=lambda e: e.local)
+            rec = {"cfg": [tn, mb, nw, u], "M": M, "rel_err": max(e.global_ for e in errs),
+                   "worst_row": worst.row_at, "worst_row_err": round(worst.row, 5),
+                   "worst_tile_err": round(worst.tile, 5), "ok": all(e < 8e-3 for e in errs),
                    "bit_identical": all(torch.equal(outs[0], o) for o in outs[1:])}
             if chk is not None:
                 flag = ctypes.c_uint(0)
@@ -75,7 +79,7 @@ def main():
     bad = 0
     for r in run(a.lib, a.launches, only=only):
         r["lib"] = os.path.basename(a.lib) if a.lib else "liblsa_kernels.so"
-        ok = r["bit_identical"] and r["rel_err"] < 8e-3 and not r.get("index_violation_bits")
+        ok = r["bit_identical"] and r["ok"] and not r.get("index_violation_bits")
         bad += not ok
         print(json.dumps(r), flush=True)
     print(json.dumps({"summary": True, "failed": bad}), flush=True)

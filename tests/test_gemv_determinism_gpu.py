@@ -15,7 +15,8 @@ sys.path.insert(0, ROOT)
 
 
 def _check(rows):
-    bad = [r for r in rows if not (r["bit_identical"] and r["rel_err"] < 8e-3 and not r.get("index_violation_bits"))]
+    # "ok": global < 8e-3 AND worst 16x16 tile / worst row < 3 x 8e-3 on every launch
+    bad = [r for r in rows if not (r["bit_identical"] and r["ok"] and not r.get("index_violation_bits"))]
     assert not bad, bad
     return rows
 
@@ -28,9 +29,9 @@ def test_gemv_every_config_deterministic_library():
 
 @pytest.mark.parametrize("variant", ["liblsa_gemv_body.so", "liblsa_gemv_body_chk.so"])
 def test_gemv_every_config_deterministic_shared_body(variant):
-    """The same kernel built through the shared device-function body (probe build, made on the box by
+    """The same kernel built through the shared device-function body (probe build in probe_bin/,
     scripts/probes/build_gemv_body.sh; skipped where it was not built)."""
-    path = os.path.join(ROOT, "build", "probes", variant)
+    path = os.path.join(ROOT, "probe_bin", variant)
     if not os.path.exists(path):
         pytest.skip(f"{variant} not built (scripts/probes/build_gemv_body.sh)")
     from scripts.gemv_det_probe import run
