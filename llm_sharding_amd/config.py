@@ -119,6 +119,12 @@ class LlamaConfig:
                 raise ValueError(f"unsupported GPT-2 activation {d.get('activation_function')!r}")
             d = {**{k: v for k, v in d.items() if k not in ("n_embd", "n_layer", "n_head", "n_inner",
                                                               "n_positions", "layer_norm_epsilon")}, **m}
+        rp = d.get("rope_parameters")
+        if isinstance(rp, dict):  # transformers >= 5 writes theta + scaling as one "rope_parameters" dict
+            d = dict(d)
+            d.setdefault("rope_theta", rp.get("rope_theta", cls.rope_theta))
+            if rp.get("rope_type", "default") != "default" and not d.get("rope_scaling"):
+                d["rope_scaling"] = {k: v for k, v in rp.items() if k != "rope_theta"}
         fields = {f.name for f in dataclasses.fields(cls)}
         kw = {k: v for k, v in d.items() if k in fields}
         if "num_key_value_heads" not in d or d.get("num_key_value_heads") is None:
