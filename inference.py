@@ -4,6 +4,12 @@ whole model on one device through the MI355X engine (hipGraph decode on GPU).
 
     python inference.py --shards DIR [--prompt "..."] [--max-new-tokens 128]
     python inference.py --random llama2-7b --max-new-tokens 64     # random-init weights
+    python inference.py --shards DIR --hf-compare HF_DIR           # + the reference's own path
+
+``--hf-compare HF_DIR`` also runs what the reference's inference.py runs
+(/root/reference/inference.py:16-45: transformers' AutoModelForCausalLM + greedy generate) on the
+HF checkpoint the shards were cut from, in fp32 on the CPU, and reports where the two greedy
+decodes agree (tests/test_llama_hf_parity.py pins the same parity in the test suite).
 """
 import argparse
 import os
@@ -25,6 +31,8 @@ def main():
     ap.add_argument("--prompt", default="Write a poem about the blue sky.")
     ap.add_argument("--max-new-tokens", type=int, default=128)
     ap.add_argument("--device", default="cuda:0" if torch.cuda.is_available() else "cpu")
+    ap.add_argument("--hf-compare", default="", help="HF checkpoint dir: also run transformers' greedy generate "
+                                                     "(the reference inference.py's path, fp32 CPU) and compare tokens")
     a = ap.parse_args()
     if a.shards:
         cfg = LlamaConfig.from_pretrained(a.shards)
@@ -66,6 +74,22 @@ def main():
         out = out[:eos[0] + 1]
     print(tok.decode(ids.tolist() + out, skip_special_tokens=True))
     print(f"[INFO] {len(out)} new tokens, {max(1, len(out) - 1) / max(dt_s, 1e-9):.1f} tok/s decode")
+    if a.hf_compare:
+        hf = hf_greedy(a.hf_compare, ids, len(out))
+        same = next((i for i, (x, y) in enumerate(zip(out, hf)) if x != y), len(out))
+        print(f"[INFO] HF greedy (transformers, fp32 CPU) agrees on the first {same}/{len(out)} tokens"
+              + ("" if same == len(out) else f"; first divergence at token {same}: ours {out[same]}, HF {hf[same]}"))
+    return out
+
+
+def hf_greedy(hf_dir: str, ids: torch.Tensor, n_new: int) -> list:
+    """The reference's single-process path: AutoModelForCausalLM.from_pretrained + greedy
+    generate (/root/reference/inference.py:16-45), here fp32 on the CPU as the oracle."""
+    from transformers import AutoModelForCausalLM
+    m = AutoModelForCausalLM.from_pretrained(hf_dir, dtype=torch.float32).eval()
+    with torch.no_grad():
+        g = m.generate(ids[None].cpu(), max_new_tokens=n_new, min_new_tokens=n_new, do_sample=False)
+    return g[0, ids.numel():].tolist()
 
 
 if __name__ == "__main__":

@@ -14,6 +14,8 @@ decode. It must equal HF's greedy decode token for token, and the golden fp32 mo
 transformers here is 5.x, not the reference's 4.53 pin. Its per-layer ``past_key_value=`` kwarg
 differs, so it cannot stand in for the reference's per-layer calls. Its
 full-model forward and generate are still HF's Llama math, and that is what is compared here."""
+import os
+
 import pytest
 import torch
 
@@ -200,3 +202,18 @@ def test_hip_engine_matches_hf_llama(tmp_path, variant):
         h = eng.forward(eng.embed(torch.tensor([t], device="cuda")), slot, pos)
         eng.advance([0], [1])
     assert clear >= 3
+
+
+def test_inference_cli_hf_compare(hf, capsys, monkeypatch):
+    """inference.py --hf-compare: our engine's greedy decode next to the reference's own path
+    (transformers generate) on the checkpoint the shards were cut from."""
+    import sys
+    import inference
+    m, shards = hf
+    hf_dir = os.path.join(os.path.dirname(shards), "hf_llama")
+    monkeypatch.setattr(sys, "argv", ["inference.py", "--shards", shards, "--hf-compare", hf_dir, "--device", "cpu",
+                                      "--max-new-tokens", "10", "--prompt", "abc xyz"])
+    out = inference.main()
+    text = capsys.readouterr().out
+    assert "agrees on the first 10/10 tokens" in text, text
+    assert len(out) == 10
