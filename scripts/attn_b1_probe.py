@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Batch-1..16 decode attention (Llama-2-7B heads, 32 x 128, MHA) at short / mid contexts: the
 split-KV kernel's split count and minimum chunk swept, hipGraph-timed (20 launches per graph),
-to set StageEngine.decode_nsplit for latency-bound decode. One JSON line per (rows, T)."""
+to set StageEngine.decode_nsplit for latency-bound decode. One JSON line per (rows, T).
+
+usage: attn_b1_probe.py [rows,rows,...] [T,T,...] [t_max]   (defaults 1,4,16  150,600,2048  4096)"""
 import json
 import os
 import sys
@@ -17,9 +19,12 @@ DEV = "cuda"
 hip.lib()
 nh = nkv = 32
 hd = 128
-for rows in (1, 4, 16):
-    for T in (150, 600, 2048):
-        tmax = 4096
+ROWS = [int(x) for x in sys.argv[1].split(",")] if len(sys.argv) > 1 else [1, 4, 16]
+TS = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [150, 600, 2048]
+TMAX = int(sys.argv[3]) if len(sys.argv) > 3 else 4096
+for rows in ROWS:
+    for T in TS:
+        tmax = TMAX
         kc = torch.randn(rows, nkv, tmax, hd, device=DEV).to(torch.bfloat16)
         vc = torch.randn_like(kc)
         q = torch.randn(rows, nh * hd, device=DEV).to(torch.bfloat16)
