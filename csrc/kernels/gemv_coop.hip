@@ -104,11 +104,30 @@ __global__ __launch_bounds__(NW * KW * 64) void gemv_coop_kernel(
   const int wt = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int w = wt % NW, kg = wt / NW;          // tile wave within the k-group, k-group
   const int KT = K >> 5;
-  const int G = N / 16 / TG;                    // column groups
-  const int g = blockIdx.x % G, s = blockIdx.x / G;
-  const int nt0 = g * TG + w * TNW;             // this wave's first tile
+  // SK == 0 ("ragged"): no K split; the column tiles (gate / up PAIRS for SwiGLU) are dealt out
+  // evenly to the grid's workgroups (one per CU), tcnt <= TG each - a tile count that is not a
+  // multiple of TG still fills every CU (Llama-2-7B gate_up at 128 rows: 1,376 tiles = 172 groups
+  // of 8 on 172 CUs, or 5-6 tiles on each of 256). Waves past tcnt re-stream the last tile
+  // (nothing of theirs is stored). Otherwise: column group g of TG tiles, K split s of SK.
+  const bool ragged = SK == 0;
+  const int SKe = ragged ? 1 : SK;
+  int g = 0, s = 0, tlo, tcnt;
+  if (ragged) {
+    constexpr int P = EPI == EPI_SWIGLU ? 2 : 1;
+    const int units = N / 16 / P;
+    tlo = P * (int)(((long long)blockIdx.x * units) / gridDim.x);
+    tcnt = P * (int)((((long long)blockIdx.x + 1) * units) / gridDim.x) - tlo;
+  } else {
+    const int G = N / 16 / TG;                  // column groups
+    g = blockIdx.x % G;
+    s = blockIdx.x / G;
+    tlo = g * TG;
+    tcnt = TG;
+  }
+  const int G = ragged ? 1 : N / 16 / TG;
+  const int nt0 = tlo + (w * TNW < tcnt - TNW ? w * TNW : tcnt - TNW);  // this wave's first tile
   const int nch_all = KT / KF;                  // KC-k chunks; split s owns [c_lo, c_hi)
-  const int c_lo = s * nch_all / SK, c_hi = (s + 1) * nch_all / SK;
+  const int c_lo = s * nch_all / SKe, c_hi = (s + 1) * nch_all / SKe;
   // k-group q owns chunks [q*nchunk, (q+1)*nchunk) of the split (host: divisible by KW)
   const int kt0 = c_lo * KF, nchunk = (c_hi - c_lo) / KW;
 
@@ -307,7 +326,7 @@ __global__ __launch_bounds__(NW * KW * 64) void gemv_coop_kernel(
   }
   LSA_CSTAMP(3);
   float* red = reinterpret_cast<float*>(smem);  // [TG][MR][RS]
-  if (SK == 1 || EPI == EPI_PARTIAL) {  // EPI_PARTIAL: every split stores its own fp32 tile
+  if (SKe == 1 || EPI == EPI_PARTIAL) {  // EPI_PARTIAL: every split stores its own fp32 tile
     if (kg == 0)
 #pragma unroll
     for (int rb = 0; rb < MB; ++rb)
@@ -411,7 +430,7 @@ __global__ __launch_bounds__(NW * KW * 64) void gemv_coop_kernel(
 
   LSA_CSTAMP(7);
   auto rstd = [&](int mm) -> float { return NORM ? rsqrtf(s_ss[mm] / (float)K + eps) : 1.f; };
-  const int ntg0 = g * TG;
+  const int ntg0 = tlo;
   // rows RS = 20 floats apart: the 16 rows one ds_read_b128 lane group reads start 20 banks
   // apart (all 64 banks, conflict-free) with the quads in static order - a row-dependent quad
   // rotation made v[] dynamically indexed (~1,200 v_cndmask per epilogue, 2.5-5.5 us per launch)
@@ -435,7 +454,7 @@ __global__ __launch_bounds__(NW * KW * 64) void gemv_coop_kernel(
   };
   if (EPI == EPI_SWIGLU) {
     // gate tile 2tp / up tile 2tp+1 -> 16 outputs per thread, two 16-B stores
-    for (int e = tid; e < (TG / 2) * MR; e += NTHR) {
+    for (int e = tid; e < (tcnt / 2) * MR; e += NTHR) {
       const int tp = e / MR, mm = e % MR;
       if (mm >= M) continue;
       const float r = rstd(mm);
@@ -450,7 +469,7 @@ __global__ __launch_bounds__(NW * KW * 64) void gemv_coop_kernel(
     }
   } else {
     // one thread per finished 16-column tile row (epilogue.h epi_row16)
-    for (int e = tid; e < TG * MR; e += NTHR) {
+    for (int e = tid; e < tcnt * MR; e += NTHR) {
       const int t = e / MR, mm = e % MR;
       if (mm >= M) continue;
       if constexpr (LSA_COOP_ABLATE == 4) {
@@ -489,11 +508,23 @@ __global__ __launch_bounds__(NW * KW * 64) void gemv_coop_kernel(
   LSA_CSTAMP(8);
 }
 
+// compute units of the current device (the ragged mode's grid: one workgroup per CU)
+int n_cu() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cached[dev]) {
+    int v = 0;
+    cached[dev] = hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0 ? v : 256;
+  }
+  return cached[dev];
+}
+
 template <int MB, int TNW, int NW, int KF, int KW, int D, int EPI, bool FP8>
 int launch(bool norm, const bf16_raw* x, int ldx, const int* a_rows, const bf16_raw* wp, int M, int N, int K, int SK, float eps,
            const EpiArgs& ep, float* slab, unsigned* cnt, const float* wscale, hipStream_t s) {
   const int G = N / 16 / (NW * TNW);
-  dim3 grid(G * SK), block(NW * KW * 64);
+  dim3 grid(SK ? G * SK : n_cu()), block(NW * KW * 64);
   if (norm)
     gemv_coop_kernel<MB, TNW, NW, KF, KW, D, EPI, true, FP8><<<grid, block, 0, s>>>(x, ldx, a_rows, wp, M, N, K, SK, eps, ep, slab, cnt, wscale);
   else
@@ -545,12 +576,19 @@ template <bool FP8>
 int coop_entry(const void* x, int ldx, const int* a_rows, const void* wp, int M, int N, int K, int norm, float eps,
                int epi, const EpiArgs* ep, int tnw, int nw, int kf, int sk, int kw, int d, float* slab,
                unsigned* counters, const float* wscale, hipStream_t stream) {
-  if (M < 1 || M > 128 || kf < 1 || K % (32 * kf) || ldx < K || sk < 1 || kw < 1) return LSA_BAD_SHAPE;
-  if (kw > 1 && (K / (32 * kf)) % (sk * kw)) return LSA_BAD_SHAPE;  // every k-group: same chunk count
+  if (M < 1 || M > 128 || kf < 1 || K % (32 * kf) || ldx < K || sk < 0 || kw < 1) return LSA_BAD_SHAPE;
+  if (kw > 1 && (K / (32 * kf)) % ((sk ? sk : 1) * kw)) return LSA_BAD_SHAPE;  // every k-group: same chunk count
   if (FP8 && (kf % 2 || !wscale)) return LSA_BAD_SHAPE;
   const int mb = M <= 32 ? 2 : (M <= 64 ? 4 : 8);
   const int tg = nw * tnw;
-  if (N % (16 * tg) || sk > K / (32 * kf)) return LSA_BAD_SHAPE;
+  if (sk == 0) {  // ragged: tiles (SwiGLU: pairs) dealt to one workgroup per CU, at most tg each
+    const int P = epi == EPI_SWIGLU ? 2 : 1, cu = n_cu();
+    if (FP8 || epi == EPI_PARTIAL || N % (16 * P) || P % tnw) return LSA_BAD_SHAPE;
+    const int units = N / 16 / P;
+    if (units < cu || P * ((units + cu - 1) / cu) > tg) return LSA_BAD_SHAPE;
+  } else if (N % (16 * tg) || sk > K / (32 * kf)) {
+    return LSA_BAD_SHAPE;
+  }
   if (epi == EPI_SWIGLU && tg % 2) return LSA_BAD_SHAPE;  // gate / up tile pairs stay in one workgroup
   if (sk > 1 && (!slab || !counters)) return LSA_BAD_SHAPE;
   const bf16_raw* xx = static_cast<const bf16_raw*>(x);

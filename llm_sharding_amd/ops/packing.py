@@ -156,7 +156,9 @@ GEMV_CONFIGS = [
 ]
 
 _TUNED = None
-TUNING_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemv_tuning.json")
+# LSA_GEMV_TUNING (diagnostic): another table, for A/B runs of a candidate table against this one
+TUNING_FILE = os.environ.get("LSA_GEMV_TUNING") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                                "gemv_tuning.json")
 
 
 def row_blocks(rows: int) -> int:
@@ -188,7 +190,12 @@ COOP_SPLITS = (1, 2, 4, 8, 16)
 def coop_candidates(n_tiles: int, k: int, rows: int, need_even: bool = False) -> list:
     """(tnw, nw, kf, sk, kw, d) for the cooperative split-K GEMV (rows 17..128): every split
     (and every k-group of a split) keeps at least one K chunk of 32*kf, and kw > 1 needs the
-    chunks to divide evenly over sk*kw. need_even (SwiGLU): an even tile count per workgroup."""
+    chunks to divide evenly over sk*kw. need_even (SwiGLU): an even tile count per workgroup.
+
+    sk = 0 is the ragged mode (gemv_coop.hip): no K split, the tiles (SwiGLU: gate / up pairs)
+    dealt evenly to one workgroup per CU, at most nw * tnw each - for tile counts that are not a
+    multiple of a workgroup's tiles (Llama-2-7B gate_up: 1,376 tiles fill 172 CUs as groups of 8).
+    Not for EPI_PARTIAL or fp8 weights; chosen only through the tuning table."""
     if rows <= 16:
         return []
     mb = row_blocks(rows)
@@ -202,6 +209,12 @@ def coop_candidates(n_tiles: int, k: int, rows: int, need_even: bool = False) ->
                 continue
             if (n_tiles // (tnw * nw)) * sk <= 4 * N_CU:
                 out.append((tnw, nw, kf, sk, kw, d))
+    for (b, tnw, nw, kf, kw, d) in COOP_CONFIGS:  # ragged (sk = 0)
+        p = 2 if need_even else 1
+        units = n_tiles // p
+        if (b == mb and kw == 1 and k % (32 * kf) == 0 and n_tiles % p == 0 and p % tnw == 0 and units >= N_CU
+                and p * -(-units // N_CU) <= tnw * nw):
+            out.append((tnw, nw, kf, 0, kw, d))
     return out
 
 
@@ -237,7 +250,7 @@ def coop_norm(cfg) -> tuple:
 
 def coop_slab_floats(n: int, rows: int, tnw: int, nw: int, kf: int, sk: int, kw: int = 1) -> int:
     """fp32 workspace a coop launch needs (0 when sk == 1)."""
-    if sk == 1:
+    if sk <= 1:  # one split, or the ragged mode (sk = 0): no slab
         return 0
     mr = 16 * row_blocks(rows)
     return sk * n * mr + sk * (n // 16 // (tnw * nw)) * mr
@@ -286,7 +299,7 @@ def partial_config(n_tiles: int, rows: int, k: int = 4096) -> Optional[tuple]:
     if t is None or rows <= 16:
         return None
     cfg = tuple(t[1])
-    return cfg if cfg in coop_candidates(n_tiles, k, rows) and cfg[3] <= 8 else None
+    return cfg if cfg in coop_candidates(n_tiles, k, rows) and 1 <= cfg[3] <= 8 else None
 
 
 def proj_config(n_tiles: int, rows: int, need_even: bool = False, k: int = 4096) -> tuple:
@@ -304,10 +317,10 @@ def proj_config(n_tiles: int, rows: int, need_even: bool = False, k: int = 4096)
         allc = coop_candidates(n_tiles, k, rows, need_even)
         cands = []
         for pref in ((1, 8, 8), (1, 8, 4), (1, 8, 2)):
-            cands = [c for c in allc if c[:3] == pref and c[4] == 1 and c[5] == 3]
+            cands = [c for c in allc if c[:3] == pref and c[3] >= 1 and c[4] == 1 and c[5] == 3]
             if cands:
                 break
-        cands = cands or allc
+        cands = cands or [c for c in allc if c[3] >= 1]
         for c in cands:
             if (n_tiles // 8) * c[3] >= N_CU:
                 return ("coop", c)

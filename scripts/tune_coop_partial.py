@@ -46,7 +46,7 @@ def main():
                 res = []
                 for c in packing.coop_candidates(N // 16, K, M):
                     sk = c[3]
-                    if sk > 8:
+                    if not 1 <= sk <= 8:  # sk = 0 (ragged): no split partials
                         continue
 
                     def run(i, c=c, sk=sk):

@@ -117,6 +117,60 @@ def test_gemv_coop_every_config(cfg):
     assert tested > 0, cfg
 
 
+@pytest.mark.parametrize("M", [40, 100, 128])
+def test_gemv_coop_ragged(M):
+    """coop ragged mode (sk = 0): no K split, tiles (SwiGLU: gate / up pairs) dealt evenly to one
+    workgroup per CU, at most nw * tnw each, with the same fused epilogues: SwiGLU on Llama-2-7B's
+    gate_up (1,376 tiles: 5-6 per workgroup), residual + RMSNorm on 300 tiles (1-2 per workgroup)
+    and argmax on a 2,000-tile head (7-8), every ragged candidate; bitwise equal on a repeat."""
+    h = hip()
+    H = 4096
+    x = _rnd(M, H)
+    g = (1 + 0.1 * torch.randn(H, device=DEV)).to(torch.bfloat16)
+    ws = h.CoopWorkspace(DEV, slab_floats=1 << 22)
+    tested = 0
+    # SwiGLU, gate_up of Llama-2-7B
+    I = 11008
+    wg, wu = _rnd(I, H, scale=0.05), _rnd(I, H, scale=0.05)
+    wgu = packing.pack_b(packing.fold_norm(packing.fuse_gate_up(wg, wu), g))
+    xn = _rmsnorm(x, g, 1e-5)
+    ref = F.silu(xn @ wg.float().T) * (xn @ wu.float().T)
+    for c in [c for c in packing.coop_candidates(2 * I // 16, H, M, True) if c[3] == 0]:
+        outs = []
+        for _ in range(2):
+            out = torch.zeros(M, I, dtype=torch.bfloat16, device=DEV)
+            h.gemv(x, wgu, M, 2 * I, H, h.EPI_SWIGLU, h.make_epi(out=out, ldo=I), norm=True, coop=c, ws=ws)
+            outs.append(out)
+        assert rel_err(outs[0], ref) < 1e-2, c
+        assert torch.equal(outs[0], outs[1]), c
+        tested += 1
+    # residual + fused RMSNorm, 300 tiles
+    N = 4800
+    w = _rnd(N, H, scale=0.02)
+    wp = packing.pack_b(packing.fold_norm(w, g))
+    resid = _rnd(M, N)
+    ref = resid.float() + xn @ w.float().T
+    for c in [c for c in packing.coop_candidates(N // 16, H, M) if c[3] == 0]:
+        out = resid.clone()
+        h.gemv(x, wp, M, N, H, h.EPI_RESID, h.make_epi(out=out, resid=out, ldo=N, ldr=N), norm=True, coop=c, ws=ws)
+        assert rel_err(out, ref) < 8e-3, c
+        tested += 1
+    # argmax over a 32,000-column head
+    V = 32000
+    lm = _rnd(V, H, scale=0.02)
+    wlm = packing.pack_b(lm)
+    logits = x.float() @ lm.float().T
+    keys = torch.zeros(M, dtype=torch.int64, device=DEV)
+    tok = torch.zeros(M, dtype=torch.int32, device=DEV)
+    for c in [c for c in packing.coop_candidates(V // 16, H, M) if c[3] == 0][:3]:
+        h.gemv(x, wlm, M, V, H, h.EPI_ARGMAX, h.make_epi(keys=keys), coop=c, ws=ws)
+        h.argmax_finalize(keys, M, tok)
+        chosen = logits.gather(1, tok.long()[:, None])[:, 0]
+        assert torch.all(logits.max(-1).values - chosen < 2e-2 * logits.abs().max()), c
+        tested += 1
+    assert tested >= 3
+
+
 @pytest.mark.parametrize("M", [17, 40, 64, 100, 128])
 @pytest.mark.parametrize("N,K", [(4096, 4096), (4096, 11008)])
 def test_gemv_coop_partials_resid(M, N, K):
@@ -132,7 +186,7 @@ def test_gemv_coop_partials_resid(M, N, K):
     part = torch.empty(8 * M * N, dtype=torch.float32, device=DEV)
     tested = 0
     for c in packing.coop_candidates(N // 16, K, M):
-        if c[3] > 8:
+        if not 1 <= c[3] <= 8:  # sk = 0 (ragged) has no split partials
             continue
         out = resid.clone()
         p3 = part[:c[3] * M * N].view(c[3], M, N)
