@@ -19,7 +19,9 @@ constexpr int ATT_MAX_SPLIT = 16;  // split-KV factor limit (the merge keeps one
 // NW: waves per workgroup (the caller launches NW * 64 threads). Few (row, kv-head) work items
 // (batch-1 decode: 32 workgroups for the whole chip) are latency-bound - one dependent HBM round
 // trip per KPI * U keys - so that case takes 8 waves x U 8 = 256 keys per round trip (attention.hip).
-template <int HD, int G, int U = 4, int PF = 0, int NT = 0, bool SPLIT = true, int NW = ATT_WAVES>
+// WT: the final output is stored write-through (sc1), for a consumer on another CU / XCD that
+// reads it after an arrival counter in the same launch (attn_oproj.hip).
+template <int HD, int G, int U = 4, int PF = 0, int NT = 0, bool SPLIT = true, int NW = ATT_WAVES, bool WT = false>
 LSA_DEVICE void attn_split_body(
     const bf16_raw* __restrict__ q, int ldq, const bf16_raw* __restrict__ kc,
     const bf16_raw* __restrict__ vc, const int* __restrict__ slot, const int* __restrict__ pos,
@@ -243,7 +245,13 @@ LSA_DEVICE void attn_split_body(
       os += s_o[i][r][d] * a;
     }
     if (!SPLIT || nact == 1) {  // lone active split: final output directly, no merge
-      out[(size_t)row * ldo + (size_t)(kvh * G + r) * HD + d] = f2bf(os / ls);
+      const size_t oi = (size_t)row * ldo + (size_t)(kvh * G + r) * HD + d;
+      if constexpr (WT)
+        __builtin_amdgcn_raw_buffer_store_b16(f2bf(os / ls),
+                                              __builtin_amdgcn_make_buffer_rsrc(out, (short)0, 0x7fffffff, 0x00020000),
+                                              (int)(oi * 2), 0, 16 /* sc1 */);
+      else
+        out[oi] = f2bf(os / ls);
     } else {
       const int pi = (int)(pbase + (size_t)r * nsplit);
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(os / ls), por, (pi * HD + d) * 4, 0, 16 /* sc1 */);

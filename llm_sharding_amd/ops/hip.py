@@ -29,6 +29,7 @@ KERNELS_SO = os.environ.get("LSA_KERNELS_SO") or os.path.join(NATIVE_DIR, "libls
 
 EPI_STORE, EPI_RESID, EPI_SWIGLU, EPI_QKV, EPI_ARGMAX, EPI_PARTIAL = range(6)
 _STATUS = {0: "ok", 1: "bad shape", 2: "unsupported", 3: "launch failed"}
+_UNSUPPORTED = 2  # LSA_UNSUPPORTED: no kernel instantiation for the shape
 
 
 class EpiArgs(ctypes.Structure):
@@ -88,7 +89,9 @@ def load_library(path: str, mode: int = ctypes.RTLD_LOCAL) -> ctypes.CDLL:
     L.lsa_gemm_wr.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(EpiArgs), i, i, vp]
     L.lsa_gemm_sk.argtypes = [vp, i, vp, i, i, i, i, ctypes.POINTER(EpiArgs), i, i, i, i, i, i, i, vp, vp, ctypes.c_longlong, i,
                               vp]
-    for name in ("lsa_gemv", "lsa_gemv_coop", "lsa_gemv_fp8", "lsa_dequant_fp8_packed", "lsa_gemv_coop_fp8", "lsa_gemm",
+    L.lsa_attn_oproj.argtypes = [vp, i, vp, vp, vp, vp, vp, i, i, i, i, f, vp, vp, i, i, ctypes.POINTER(EpiArgs), vp, i,
+                                 vp]
+    for name in ("lsa_gemv", "lsa_gemv_coop", "lsa_attn_oproj", "lsa_gemv_fp8", "lsa_dequant_fp8_packed", "lsa_gemv_coop_fp8", "lsa_gemm",
                  "lsa_gemm_sk", "lsa_gemm_wr", "lsa_attn_decode", "lsa_attn_prefill", "lsa_embed", "lsa_rmsnorm", "lsa_layernorm",
                  "lsa_resid_rmsnorm_partials", "lsa_row_ss",
                  "lsa_argmax_finalize", "lsa_pos_advance", "lsa_version"):
@@ -604,6 +607,36 @@ def attn(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, slot: to
                                _p(part_o), _p(part_lse), _p(out), out.stride(0),
                                _p(counters) if nsplit > 1 else None, _stream())
     _check(rc, "lsa_attn_decode")
+
+
+def attn_oproj(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, slot: torch.Tensor,
+               pos: torch.Tensor, n_heads: int, n_kv: int, head_dim: int, attn_out: torch.Tensor,
+               wp: torch.Tensor, N: int, ep: EpiArgs, sync: torch.Tensor, kv_len: Optional[torch.Tensor] = None,
+               scale: Optional[float] = None, max_wg: int = 0) -> bool:
+    """Batch-1 decode attention fused with the o projection and its residual add
+    (attn_oproj.hip): ``attn_out`` [1][K] gets the attention output, ``ep`` (EPI_RESID: out, resid)
+    gets resid + attn_out @ Wo^T, ``wp`` = pack_b(Wo) [N, K], K = n_heads * head_dim. ``sync``:
+    >= 4 zeroed int32, left zeroed; sync[2] != 0 afterwards means an arrival poll timed out.
+    ``max_wg`` caps the grid (0: one workgroup per CU). False when no instantiation covers the
+    shape (the caller then runs :func:`attn` + :func:`gemv`)."""
+    K = n_heads * head_dim
+    _req(_is_bf16_cuda(q, k_cache, v_cache, attn_out, wp), "attn_oproj: bf16 cuda tensors")
+    _req(k_cache.dim() == 4 and k_cache.shape == v_cache.shape, "attn_oproj: cache [slots, n_kv, T, hd]")
+    _req(k_cache.shape[1] == n_kv and k_cache.shape[3] == head_dim, "attn_oproj: cache dims")
+    _req(q.shape[0] >= 1 and q.shape[1] >= K and q.stride(1) == 1, "attn_oproj: q shape")
+    _req(attn_out.is_contiguous() and attn_out.numel() >= K, "attn_oproj: attn_out")
+    _req(wp.numel() == N * K and N % 16 == 0, "attn_oproj: packed weight shape")
+    _req(slot.dtype == torch.int32 and pos.dtype == torch.int32, "attn_oproj: int32 slot/pos")
+    _req(sync.dtype == torch.int32 and sync.is_cuda and sync.numel() >= 4, "attn_oproj: sync")
+    _req(bool(ep.out) and bool(ep.resid), "attn_oproj: EPI_RESID epilogue needs out and resid")
+    sc = head_dim ** -0.5 if scale is None else scale
+    rc = lib().lsa_attn_oproj(_p(q), q.stride(0), _p(k_cache), _p(v_cache), _p(slot), _p(pos), _p(kv_len),
+                              n_heads, n_kv, head_dim, k_cache.shape[2], float(sc), _p(attn_out), _p(wp), N, K,
+                              ctypes.byref(ep), _p(sync), int(max_wg), _stream())
+    if rc == _UNSUPPORTED:
+        return False
+    _check(rc, "lsa_attn_oproj")
+    return True
 
 
 # GQA decode attention on MFMA (lsa_attn_decode_mfma) from this many (row, kv-head) items up;

@@ -182,6 +182,10 @@ class StageEngine:
     # split-KV chunks never shorter than this many keys: below ~256 keys per split the merge
     # costs more than the extra parallelism buys (profiles/r1_bench_kernels_sweep.jsonl, attn)
     ATTN_MIN_CHUNK = int(os.environ.get("LSA_ATTN_MIN_CHUNK", "256"))  # keys per decode split, at least
+    # batch-1 decode: attention and the o projection in one launch, the o weights streamed while
+    # the attention runs (attn_oproj.hip). Off: measured 6 % slower at batch 1 than the two
+    # launches (profiles/r6_attn_oproj.md); LSA_ATTN_OPROJ=1 turns it on
+    ATTN_OPROJ = os.environ.get("LSA_ATTN_OPROJ", "0") == "1"
 
     def __init__(self, cfg: LlamaConfig, start: int, end: int, device="cpu",
                  dtype=torch.bfloat16, *, has_embed: bool = False, has_head: bool = False,
@@ -360,6 +364,7 @@ class StageEngine:
             self.part_lse = torch.zeros(ws_rows * cfg.num_attention_heads, dtype=torch.float32, device=dev)
             # per-(row, kv-head) arrival tickets of the in-kernel split-KV merge (self-resetting)
             self.attn_cnt = torch.zeros(ws_rows * cfg.num_key_value_heads, dtype=torch.int32, device=dev)
+            self.ao_sync = torch.zeros(4, dtype=torch.int32, device=dev)  # attn_oproj arrival counters
             self.ws_rows = ws_rows
             self.keys = torch.zeros(R, dtype=torch.int64, device=dev)
             self.tokens = torch.zeros(R, dtype=torch.int32, device=dev)
@@ -399,7 +404,7 @@ class StageEngine:
 
     # buffers a forward pass writes besides the KV cache: one set per concurrently running graph
     SCRATCH_ATTRS = ("buf_h", "buf_xn", "buf_q", "buf_attn", "buf_act", "part_o", "part_lse", "attn_cnt",
-                     "coop_ws", "sk_ws", "part_k", "ss_buf", "w_scratch", "keys", "tokens", "ws_rows")
+                     "ao_sync", "coop_ws", "sk_ws", "part_k", "ss_buf", "w_scratch", "keys", "tokens", "ws_rows")
 
     def decode_scratch(self, k: int, rows: Optional[int] = None) -> dict:
         """Scratch set ``k`` for forward passes that run CONCURRENTLY on different streams (a
@@ -426,6 +431,7 @@ class StageEngine:
                 "part_o": torch.zeros(ws_rows * nh * hd, dtype=torch.float32, device=dev),
                 "part_lse": torch.zeros(ws_rows * nh, dtype=torch.float32, device=dev),
                 "attn_cnt": torch.zeros(ws_rows * cfg.num_key_value_heads, dtype=torch.int32, device=dev),
+                "ao_sync": torch.zeros(4, dtype=torch.int32, device=dev),
                 "coop_ws": hip.CoopWorkspace(dev, slab_floats=self.coop_ws.slab.numel(),
                                              groups=self.coop_ws.counters.numel()),
                 "sk_ws": hip.SkWorkspace(dev) if R > self.DECODE_MAX_ROWS else None,
@@ -708,6 +714,9 @@ class StageEngine:
         # row by its rstd in the epilogue - no standalone norm kernel between projections
         fuse = proj_gemm and self.ss_buf is not None and rows <= self.ss_buf.shape[0]
         ss = self.ss_buf[:rows] if fuse else None
+        # one decode row, one split: attention + o projection + residual in one launch
+        ao = (self.ATTN_OPROJ and rows == 1 and tiles is None and nsplit == 1 and not proj_gemm and not native_fp8
+              and self.ao_sync is not None)
         ss_valid = False  # ss holds the partials of hbuf's current values
         pending = 0  # down-projection partials not yet added to hbuf
         for li, lw in enumerate(self.layers):
@@ -737,15 +746,18 @@ class StageEngine:
                 else:
                     hip.rmsnorm(hbuf, None, xn, rows, eps, H)
                     pre(xn, lw.qkv, lw.qkv_s, cfg.qkv_size, H, hip.EPI_QKV, ep_qkv)
+            ep_o = hip.make_epi(out=hbuf, resid=hbuf, ldo=hbuf.stride(0), ldr=hbuf.stride(0))
+            fused_o = ao and lw.o_s is None and hip.attn_oproj(q, kc, vc, slot, pos, nh, nkv, hd, attn_o, lw.o, H, ep_o,
+                                                               self.ao_sync, kv_len=kv_len)
             if tiles is not None:
                 hip.attn_prefill(q, kc, vc, tiles[1], nh, nkv, hd, attn_o, causal=kv_len is None, tiles_host=tiles[0])
-            else:
+            elif not fused_o:
                 hip.attn(q, kc, vc, slot, pos, rows, nh, nkv, hd, nsplit, self.part_o, self.part_lse, attn_o,
                          kv_len=kv_len, counters=self.attn_cnt, min_chunk=self.ATTN_MIN_CHUNK)
-            ep_o = hip.make_epi(out=hbuf, resid=hbuf, ldo=hbuf.stride(0), ldr=hbuf.stride(0))
             ep_gu = hip.make_epi(out=act, ldo=act.stride(0))
             if not proj_gemm:
-                dec_resid(attn_o, lw.o, lw.o_s, H, cfg.q_size, ep_o)
+                if not fused_o:
+                    dec_resid(attn_o, lw.o, lw.o_s, H, cfg.q_size, ep_o)
                 dec(hbuf, lw.gate_up, lw.gate_up_s, 2 * I, H, hip.EPI_SWIGLU, ep_gu, norm=True)
                 dec_resid(act, lw.down, lw.down_s, H, I, ep_o)
             else:

@@ -46,6 +46,8 @@ KNOBS = {
     "LSA_ATTN_MFMA_MIN_ITEMS": ("env", "diagnostic", "512", "rows x kv-heads from which GQA decode uses MFMA"),
     "LSA_ATTN_GQA_NW": ("env", "diagnostic", "0", "waves of the GQA decode kernel (0 = planner)"),
     "LSA_ATTN_SMALL_MAX_WGS": ("env", "diagnostic", "", "grid size limit of the small-grid decode attention"),
+    "LSA_ATTN_OPROJ": ("env", "diagnostic", "0", "1 = batch-1 attention + o projection in one launch (profiles/r6_attn_oproj.md)"),
+    "LSA_AO_ABLATE": ("define", "diagnostic", "0", "attn_oproj ablation builds (scripts/probes/build_attn_oproj_ab.sh)"),
     "LSA_PREFLIGHT_FAULT": ("env", "diagnostic", "", "fault injection: 'a->b' drops the preflight message of edge a->b"),
     "LSA_SK_ABLATE": ("define", "diagnostic", "0", "gemm_sk ablation builds (scripts/sk_ablate.py)"),
     "LSA_COOP_ABLATE": ("define", "diagnostic", "0", "coop GEMV ablation builds"),

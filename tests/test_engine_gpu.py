@@ -144,6 +144,20 @@ def test_decode_gemm_path_below_128_rows_vs_golden(monkeypatch):
     assert 96 in calls  # the decode step's projections ran on the GEMM path
 
 
+@pytest.mark.parametrize("fused", [True, False])
+def test_b1_decode_attn_oproj_vs_golden(fused, monkeypatch):
+    """Batch-1 decode on 7B-shaped layers with attention + o projection in one launch
+    (attn_oproj.hip, StageEngine.ATTN_OPROJ) and as two launches, against the fp32 golden model;
+    the fused launch is asserted to have run (or not)."""
+    from llm_sharding_amd.ops import hip
+    monkeypatch.setattr(StageEngine, "ATTN_OPROJ", fused)
+    calls = []
+    real = hip.attn_oproj
+    monkeypatch.setattr(hip, "attn_oproj", lambda *a, **k: (calls.append(real(*a, **k)), calls[-1])[1])
+    test_engine_prefill_then_decode_vs_golden(_mid_cfg, 5)
+    assert (len(calls) > 0 and all(calls)) if fused else not calls
+
+
 def _big_batch_vs_golden(rows):
     cfg = _mid_cfg()
     seed, P = 13, 5

@@ -421,6 +421,92 @@ def test_attention_kvlen_override():
     assert rel_err(out, _attn_ref(q, kc, vc, slot, kvl, nh, nkv, hd)) < 1e-2
 
 
+@pytest.mark.parametrize("nh,nkv,hd,N,max_wg", [(32, 32, 128, 4096, 0), (40, 40, 128, 5120, 0), (24, 8, 128, 3072, 0),
+                                                 (8, 4, 64, 512, 0), (8, 4, 64, 512, 24), (8, 8, 64, 512, 0),
+                                                 (4, 2, 64, 256, 0)])
+def test_attn_oproj_fused(nh, nkv, hd, N, max_wg):
+    """Batch-1 attention + o projection + residual in one launch (attn_oproj.hip) against fp32,
+    and against the two-launch path (small-grid attention + GEMV): contexts of 1, 150 and 1100
+    keys, the explicit kv_len form. max_wg 24 on the 512-column shape forces two tiles on some o
+    workgroups (the 7B / 13B layout at 256 CUs)."""
+    h = hip()
+    K = nh * hd
+    T = 1100
+    g = torch.Generator(device=DEV).manual_seed(nh * 131 + N + max_wg)
+    q = _rnd(1, K, gen=g)
+    kc, vc = _rnd(2, nkv, T, hd, gen=g), _rnd(2, nkv, T, hd, gen=g)
+    w = _rnd(N, K, scale=K ** -0.5, gen=g)
+    wp = packing.pack_b(w)
+    sync = torch.zeros(4, dtype=torch.int32, device=DEV)
+    slot = torch.tensor([1], dtype=torch.int32, device=DEV)
+    for p_, kvl in ((0, None), (149, None), (1099, None), (1099, 300)):
+        pos = torch.tensor([p_], dtype=torch.int32, device=DEV)
+        kv_len = None if kvl is None else torch.tensor([kvl], dtype=torch.int32, device=DEV)
+        resid = _rnd(1, N, scale=0.01, gen=g)  # the projection's size (long contexts average V down)
+        out = resid.clone()
+        att = torch.zeros(1, K, dtype=torch.bfloat16, device=DEV)
+        ep = h.make_epi(out=out, resid=out, ldo=N, ldr=N)
+        assert h.attn_oproj(q, kc, vc, slot, pos, nh, nkv, hd, att, wp, N, ep, sync, kv_len=kv_len, max_wg=max_wg)
+        torch.cuda.synchronize()
+        assert sync.tolist() == [0, 0, 0, 0], sync.tolist()  # counters reset, no poll timed out
+        ref_a = _attn_ref(q, kc, vc, slot, torch.tensor([kvl or p_ + 1]), nh, nkv, hd)
+        assert rel_err(att, ref_a) < 1e-2, p_
+        assert rel_err(out, resid.float() + ref_a @ w.float().T) < 1e-2, p_
+        # the two-launch path: same attention bits, the GEMV's reduction order
+        att2, out2 = torch.zeros_like(att), resid.clone()
+        po, pl = torch.zeros(nh * hd, device=DEV), torch.zeros(nh, device=DEV)
+        h.attn(q, kc, vc, slot, pos, 1, nh, nkv, hd, 1, po, pl, att2, kv_len=kv_len)
+        assert rel_err(att, att2.float()) < 1e-3, p_
+        print(f"pos {p_}: fused attention bitwise equal to the small-grid kernel: {torch.equal(att, att2)}")
+        h.gemv(att2, wp, 1, N, K, h.EPI_RESID, h.make_epi(out=out2, resid=out2, ldo=N, ldr=N))
+        assert rel_err(out, out2.float()) < 4e-3, p_
+
+
+def test_attn_oproj_graph_replay_and_unsupported():
+    """The fused kernel replayed from a hipGraph (its counters reset in-kernel; replays with a
+    moving position give the eager results), and False for a shape it has no instantiation for
+    (GQA group 8: the caller falls back to two launches)."""
+    h = hip()
+    nh, nkv, hd, N, T = 32, 32, 128, 4096, 512
+    K = nh * hd
+    g = torch.Generator(device=DEV).manual_seed(5)
+    q = _rnd(1, K, gen=g)
+    kc, vc = _rnd(1, nkv, T, hd, gen=g), _rnd(1, nkv, T, hd, gen=g)
+    wp = packing.pack_b(_rnd(N, K, scale=K ** -0.5, gen=g))
+    sync = torch.zeros(4, dtype=torch.int32, device=DEV)
+    slot = torch.zeros(1, dtype=torch.int32, device=DEV)
+    pos = torch.zeros(1, dtype=torch.int32, device=DEV)
+    resid = _rnd(1, N, gen=g)
+    out = torch.zeros(1, N, dtype=torch.bfloat16, device=DEV)
+    att = torch.zeros(1, K, dtype=torch.bfloat16, device=DEV)
+    ep = h.make_epi(out=out, resid=resid, ldo=N, ldr=N)
+    eager = []
+    for p_ in (10, 200, 511):
+        pos.fill_(p_)
+        h.attn_oproj(q, kc, vc, slot, pos, nh, nkv, hd, att, wp, N, ep, sync)
+        eager.append(out.clone())
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(graph, stream=s):
+            h.attn_oproj(q, kc, vc, slot, pos, nh, nkv, hd, att, wp, N, ep, sync)
+    torch.cuda.current_stream().wait_stream(s)
+    for _ in range(2):
+        for p_, e in zip((10, 200, 511), eager):
+            pos.fill_(p_)
+            out.zero_()
+            graph.replay()
+            torch.cuda.synchronize()
+            assert torch.equal(out, e), p_
+            assert sync.tolist() == [0, 0, 0, 0]
+    ep2 = h.make_epi(out=out, resid=resid, ldo=N, ldr=N)
+    q8 = _rnd(1, 16 * hd, gen=g)
+    kc8 = _rnd(1, 2, T, hd, gen=g)
+    assert not h.attn_oproj(q8, kc8, kc8, slot, pos, 16, 2, hd, torch.zeros(1, 16 * hd, dtype=torch.bfloat16,
+                            device=DEV), packing.pack_b(_rnd(N, 16 * hd, gen=g)), N, ep2, sync)
+
+
 def test_embed_and_rmsnorm():
     h = hip()
     V, H = 1000, 4096
