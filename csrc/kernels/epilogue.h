@@ -64,10 +64,11 @@ LSA_DEVICE float epi_act(const EpiArgs& ep, float v) { return ep.act == 1 ? gelu
 // of the RoPE partner column n ^ 8 (same row). The packed q/k row order within a head is
 //   tile tt (16 columns): columns 0..7 -> dims 8tt..8tt+7, columns 8..15 -> dims hd/2+8tt..
 // so a rotate_half partner pair always lives in one 16-wide tile (see ops/packing.py).
-LSA_DEVICE void epi_qkv_store(const EpiArgs& ep, int m, int n, float v, float vp) {
+// ``p`` / ``slot_m``: the row's position and cache slot (ep.pos[m], ep.slot[m]), passed in so a
+// caller can request them early.
+LSA_DEVICE void epi_qkv_store(const EpiArgs& ep, int m, int n, float v, float vp, int p, int slot_m) {
   const int hd = ep.head_dim, sh = __builtin_ctz((unsigned)hd);  // power of two (host-checked)
   const int qs = ep.n_heads << sh, ks = ep.n_kv << sh;
-  const int p = ep.pos[m];
   if (p < 0 || p >= ep.t_max) return;  // never write outside the static cache
   if (ep.cos_t == nullptr) {  // no RoPE: natural column order [q | k | v]
     const int isk = n >= qs, isv = n >= qs + ks;
@@ -76,7 +77,7 @@ LSA_DEVICE void epi_qkv_store(const EpiArgs& ep, int m, int n, float v, float vp
     if (!isk) {
       ep.out[(size_t)m * ep.ldo + c0] = f2bf(v);
     } else {
-      const size_t base = ((size_t)ep.slot[m] * ep.n_kv + head) * ep.t_max + p;
+      const size_t base = ((size_t)slot_m * ep.n_kv + head) * ep.t_max + p;
       (isv ? ep.v_cache : ep.k_cache)[base * hd + dim] = f2bf(v);
     }
     return;
@@ -95,13 +96,13 @@ LSA_DEVICE void epi_qkv_store(const EpiArgs& ep, int m, int n, float v, float vp
     if (isq) {
       ep.out[(size_t)m * ep.ldo + head * hd + dim] = f2bf(r);
     } else {
-      const size_t base = ((size_t)ep.slot[m] * ep.n_kv + head) * ep.t_max + p;
+      const size_t base = ((size_t)slot_m * ep.n_kv + head) * ep.t_max + p;
       ep.k_cache[base * hd + dim] = f2bf(r);
     }
   } else {
     const int c0 = n - qs - ks;
     const int head = c0 >> sh, dim = c0 & (hd - 1);
-    const size_t base = ((size_t)ep.slot[m] * ep.n_kv + head) * ep.t_max + p;
+    const size_t base = ((size_t)slot_m * ep.n_kv + head) * ep.t_max + p;
     ep.v_cache[base * hd + dim] = f2bf(v);
   }
 }

@@ -195,7 +195,8 @@ __global__ __launch_bounds__(GTHR) void gemm_packed_kernel(const bf16_raw* __res
           const int col = (ntile0 + tn) * 16 + n;
           if (EPI == EPI_QKV) {
             const float vp = __shfl_xor(v, 8, 64);
-            if (gm < M) epi_qkv_store(ep, gm, col, v + epi_bias(ep, col), vp + epi_bias(ep, col ^ 8));
+            if (gm < M)
+              epi_qkv_store(ep, gm, col, v + epi_bias(ep, col), vp + epi_bias(ep, col ^ 8), ep.pos[gm], ep.slot[gm]);
           } else if (gm < M) {
             if (EPI == EPI_STORE)
               ep.out[(size_t)gm * ep.ldo + col] = f2bf(epi_act(ep, v + epi_bias(ep, col)));

@@ -53,6 +53,26 @@ __global__ __launch_bounds__(NW * 64) void gemv_packed_kernel(
   }
   if (EPI == EPI_ARGMAX && tid < MR) s_key[tid] = 0ull;
 
+  // Epilogue inputs that do not depend on the result (the residual, the row's cache position and
+  // slot), requested before the weight stream so their latency hides under it instead of
+  // following it (profiles/r6_gemv_epi_prefetch.md). Only where each thread finishes at most one
+  // element (e = tid: every batch-1..16 config with TN * 256 <= NTHR); else loaded in the epilogue.
+  constexpr bool PRE = (EPI == EPI_RESID || EPI == EPI_QKV) && TN * MR * 16 <= NTHR;
+  // The loads are unconditional (indices clamped into range) and converted only where used: a
+  // guarded load made hipcc wait for it (vmcnt(0)) before the main loop.
+  bf16_raw pre_r = 0;
+  int pre_p = 0, pre_s = 0;
+  if constexpr (PRE) {
+    const bool in = tid < TN * MR * 16 && ((tid >> 4) % MR) < M;
+    const int mm = in ? (tid >> 4) % MR : 0, col = (nt0 + (in ? tid / (MR * 16) : 0)) * 16 + (tid & 15);
+    if (EPI == EPI_RESID) {
+      pre_r = ep.resid[(size_t)mm * ep.ldr + col];
+    } else {
+      pre_p = ep.pos[mm];
+      pre_s = ep.slot[mm];
+    }
+  }
+
   f32x4_t acc[MB][TN];
   float ss[MB];
 #pragma unroll
@@ -175,9 +195,11 @@ __global__ __launch_bounds__(NW * 64) void gemv_packed_kernel(
       if (EPI == EPI_STORE) {
         ep.out[(size_t)mm * ep.ldo + col] = f2bf(epi_act(ep, v + epi_bias(ep, col)));
       } else if (EPI == EPI_RESID) {
-        ep.out[(size_t)mm * ep.ldo + col] = f2bf(bf2f(ep.resid[(size_t)mm * ep.ldr + col]) + v + epi_bias(ep, col));
+        const float rv = bf2f(PRE ? pre_r : ep.resid[(size_t)mm * ep.ldr + col]);
+        ep.out[(size_t)mm * ep.ldo + col] = f2bf(rv + v + epi_bias(ep, col));
       } else if (EPI == EPI_QKV) {
-        epi_qkv_store(ep, mm, col, v + epi_bias(ep, col), rsum(t, mm, n ^ 8) * r + epi_bias(ep, col ^ 8));
+        epi_qkv_store(ep, mm, col, v + epi_bias(ep, col), rsum(t, mm, n ^ 8) * r + epi_bias(ep, col ^ 8),
+                      PRE ? pre_p : ep.pos[mm], PRE ? pre_s : ep.slot[mm]);
       } else if (EPI == EPI_ARGMAX) {
         atomicMax(&s_key[mm], argmax_key(v + epi_bias(ep, col), (unsigned)(col + ep.col_offset)));
       }

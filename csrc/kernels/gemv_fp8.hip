@@ -184,7 +184,8 @@ __global__ __launch_bounds__(NW * 64) void gemv_fp8_kernel(
       } else if (EPI == EPI_RESID) {
         ep.out[(size_t)mm * ep.ldo + col] = f2bf(bf2f(ep.resid[(size_t)mm * ep.ldr + col]) + v + epi_bias(ep, col));
       } else if (EPI == EPI_QKV) {
-        epi_qkv_store(ep, mm, col, v + epi_bias(ep, col), rsum(t, mm, n ^ 8) * r + epi_bias(ep, col ^ 8));
+        epi_qkv_store(ep, mm, col, v + epi_bias(ep, col), rsum(t, mm, n ^ 8) * r + epi_bias(ep, col ^ 8), ep.pos[mm],
+                      ep.slot[mm]);
       } else if (EPI == EPI_ARGMAX) {
         atomicMax(&s_key[mm], argmax_key(v + epi_bias(ep, col), (unsigned)(col + ep.col_offset)));
       }

@@ -607,6 +607,7 @@ class NodeController:
             serving.clear()
         if self._abort_timer is not None:
             self._abort_timer.cancel()
+            self._abort_timer.join(timeout=5)  # its thread has exited before the phase changes
         dropped = lost is not None or self._aborted
         if dropped:
             with self._submit_lock:  # no submit can slip in between the phase change and the sweep
