@@ -128,18 +128,19 @@ LSA_DEVICE void st16x(void* p, u32x4_t v) {
   }
 }
 
+// ``p`` / ``slot_m``: the row's position and cache slot (ep.pos[m], ep.slot[m]), passed in so a
+// caller can request them early (gemv_coop.hip).
 template <bool WT = false>
-LSA_DEVICE void epi_qkv_row16(const EpiArgs& ep, int m, int c0, const float* v) {
+LSA_DEVICE void epi_qkv_row16p(const EpiArgs& ep, int m, int c0, const float* v, int p, int slot_m) {
   const int hd = ep.head_dim, sh = __builtin_ctz((unsigned)hd);
   const int qs = ep.n_heads << sh, ks = ep.n_kv << sh;
-  const int p = ep.pos[m];
   if (p < 0 || p >= ep.t_max) return;  // never write outside the static cache
   const int sec = c0 < qs ? 0 : (c0 < qs + ks ? 1 : 2);
   const int cs0 = c0 - (sec == 0 ? 0 : (sec == 1 ? qs : qs + ks));
   const int head = cs0 >> sh, c = cs0 & (hd - 1);
   bf16_raw* dst = sec == 0 ? ep.out + (size_t)m * ep.ldo + ((size_t)head << sh)
                            : (sec == 1 ? ep.k_cache : ep.v_cache) +
-                                 ((((size_t)ep.slot[m] * ep.n_kv + head) * ep.t_max + p) << sh);
+                                 ((((size_t)slot_m * ep.n_kv + head) * ep.t_max + p) << sh);
   if (ep.cos_t == nullptr || sec == 2) {  // v (or no RoPE): natural order, 16 contiguous dims
     st16x<WT>(dst + c, pack8(v));
     st16x<WT>(dst + c + 8, pack8(v + 8));
@@ -161,6 +162,26 @@ LSA_DEVICE void epi_qkv_row16(const EpiArgs& ep, int m, int c0, const float* v) 
   }
   st16x<WT>(dst + fi0, pack8(lo));
   st16x<WT>(dst + half + fi0, pack8(hi));
+}
+
+template <bool WT = false>
+LSA_DEVICE void epi_qkv_row16(const EpiArgs& ep, int m, int c0, const float* v) {
+  epi_qkv_row16p<WT>(ep, m, c0, v, ep.pos[m], ep.slot[m]);
+}
+
+// out[m][c0 .. c0+16) = resid (16 bf16 already loaded as two 16-B words) + v
+LSA_DEVICE void epi_resid_row16(const EpiArgs& ep, int m, int c0, const float* v, u32x4_t r0, u32x4_t r1) {
+  float a[8], b[8];
+  unpack8(r0, a);
+  unpack8(r1, b);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    a[j] += v[j];
+    b[j] += v[j + 8];
+  }
+  bf16_raw* o = ep.out + (size_t)m * ep.ldo + c0;
+  st16(o, pack8(a));
+  st16(o + 8, pack8(b));
 }
 
 // Adds the bias (if any) to v in place.
@@ -189,17 +210,7 @@ LSA_DEVICE void epi_row16(const EpiArgs& ep, int m, int c0, float* v) {
     st16(o + 8, pack8(v + 8));
   } else if (EPI == EPI_RESID) {
     const bf16_raw* rr = ep.resid + (size_t)m * ep.ldr + c0;
-    float a[8], b[8];
-    unpack8(ld16(rr), a);
-    unpack8(ld16(rr + 8), b);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      a[j] += v[j];
-      b[j] += v[j + 8];
-    }
-    bf16_raw* o = ep.out + (size_t)m * ep.ldo + c0;
-    st16(o, pack8(a));
-    st16(o + 8, pack8(b));
+    epi_resid_row16(ep, m, c0, v, ld16(rr), ld16(rr + 8));
   }
 }
 

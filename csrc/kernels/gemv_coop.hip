@@ -157,6 +157,24 @@ __global__ __launch_bounds__(NW * KW * 64) void gemv_coop_kernel(
 #pragma unroll
   for (int i = 0; i < LPT; ++i) ss[i] = 0.f;
 
+  // Epilogue inputs that do not depend on the result, requested early so their round trip hides
+  // under other work instead of following the reduction (profiles/r6_gemv_epi_prefetch.md):
+  // QKV: the rows' pos / slot here (2 VGPRs per row); RESID: the residual after the main loop
+  // (8 VGPRs per row, beside the split hand-off). Thread tid finishes rows e = tid + i * NTHR,
+  // i < EPT; the loads are unconditional with clamped indices (a guarded load made hipcc wait).
+  constexpr int EPT = (TG * MR + NTHR - 1) / NTHR;
+  constexpr bool PRE_R = EPI == EPI_RESID, PRE_Q = EPI == EPI_QKV;
+  u32x4_t pre_r[PRE_R ? EPT : 1][2];
+  int pre_p[PRE_Q ? EPT : 1], pre_s[PRE_Q ? EPT : 1];
+  if constexpr (PRE_Q) {
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {
+      const int e = tid + i * NTHR, mm = e % MR < M ? e % MR : 0;
+      pre_p[i] = ep.pos[mm];
+      pre_s[i] = ep.slot[mm];
+    }
+  }
+
   struct AV { u32x4_t v[KW][LPT]; };
   auto load_a = [&](int c) -> AV {
     AV a;
@@ -303,6 +321,16 @@ __global__ __launch_bounds__(NW * KW * 64) void gemv_coop_kernel(
       for (int q = 0; q < TNW; ++q) t += acc[rb][q][0] + acc[rb][q][1] + acc[rb][q][2] + acc[rb][q][3];
     if (t == 1.2345f) ep.out[tid] = 0;  // keep the loop live
     return;
+  }
+  if constexpr (PRE_R) {
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {
+      const int e = tid + i * NTHR;
+      const bool in = e < tcnt * MR && e % MR < M;
+      const bf16_raw* rr = ep.resid + (size_t)(in ? e % MR : 0) * ep.ldr + (tlo + (in ? e / MR : 0)) * 16;
+      pre_r[i][0] = ld16(rr);
+      pre_r[i][1] = ld16(rr + 8);
+    }
   }
   if constexpr (KW > 1) {
     // k-groups 1..KW-1 hand their partial tiles to group 0 (fragment-native, 16 B per lane)
@@ -468,8 +496,12 @@ __global__ __launch_bounds__(NW * KW * 64) void gemv_coop_kernel(
       st16(o + 8, pack8(gg + 8));
     }
   } else {
-    // one thread per finished 16-column tile row (epilogue.h epi_row16)
-    for (int e = tid; e < tcnt * MR; e += NTHR) {
+    // one thread per finished 16-column tile row (epilogue.h epi_row16); rows e = tid + i * NTHR
+    // (static i: the prefetched inputs stay in registers)
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {
+      const int e = tid + i * NTHR;
+      if (e >= tcnt * MR) break;
       const int t = e / MR, mm = e % MR;
       if (mm >= M) continue;
       if constexpr (LSA_COOP_ABLATE == 4) {
@@ -496,6 +528,12 @@ __global__ __launch_bounds__(NW * KW * 64) void gemv_coop_kernel(
 #pragma unroll
         for (int j = 0; j < 16; ++j) t += v[j];
         if (t == 1.2345f) ep.out[mm] = 0;
+      } else if constexpr (PRE_R) {
+        epi_bias16(ep, c0, v);
+        epi_resid_row16(ep, mm, c0, v, pre_r[i][0], pre_r[i][1]);
+      } else if constexpr (PRE_Q) {
+        epi_bias16(ep, c0, v);
+        epi_qkv_row16p(ep, mm, c0, v, pre_p[i], pre_s[i]);
       } else {
         epi_row16<EPI>(ep, mm, c0, v);
       }
