@@ -129,8 +129,13 @@ def profile_stage_costs(cfg: LlamaConfig, source, device, batch: int = 1, contex
     mid1, midn = decode_ms("mid", 1), decode_ms("mid", n)
     first_n, full_n = decode_ms("first", n), decode_ms("full", n)
     p1, pn = prefill_ms(1), prefill_ms(n)
-    layer = max(0.0, (midn - mid1) / (n - 1))
-    lp = max(0.0, (pn - p1) / (n - 1))
+    # per-layer cost from the 1- vs n-layer difference; a host whose speed drifted between the two
+    # measurements can make that difference <= 0, and a zero layer cost would make the planner
+    # treat layers as free: then the n-layer time split evenly over its layers (an upper bound)
+    layer = (midn - mid1) / (n - 1)
+    layer = layer if layer > 0 else midn / n
+    lp = (pn - p1) / (n - 1)
+    lp = lp if lp > 0 else pn / n
     out = {
         "batch": batch, "context": context, "profiled_layers": n, "prefill_len": prefill_len,
         "device": str(dev), "graph": gpu,
