@@ -29,13 +29,18 @@ def _rnd(*shape, scale=1.0):
 @pytest.mark.parametrize("bn", [128, 192, 256])
 @pytest.mark.parametrize("grid", [256, 37])
 def test_gemm_wr_store(M, N, K, bn, grid):
-    """K = 320 / 64 / 2816 leave a partial last group of K-steps (the ring holds 4)."""
+    """K = 320 / 64 / 2816 leave a partial last group of K-steps (the ring holds 4). A width that
+    does not tile N is refused on the host before anything launches (output left untouched)."""
     h = hip()
-    if N % bn:
-        pytest.skip("N not a multiple of bn")
     a = _rnd(M, K)
     w = _rnd(N, K, scale=0.02)
     out = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=DEV)
+    if N % bn:
+        with pytest.raises(ValueError, match="does not tile"):
+            h.gemm_wr(a, packing.pack_b(w), M, N, K, h.EPI_STORE, h.make_epi(out=out, ldo=N), bn=bn, grid=grid)
+        torch.cuda.synchronize()
+        assert torch.isnan(out.float()).all()
+        return
     h.gemm_wr(a, packing.pack_b(w), M, N, K, h.EPI_STORE, h.make_epi(out=out, ldo=N), bn=bn, grid=grid)
     assert rel_err(out, a.float() @ w.float().T) < 8e-3
 
