@@ -538,17 +538,19 @@ class NodeController:
             elif cmd == "abort_pipeline":
                 # the master lost a rank of this torchrun world (MasterNode.failover): rank 0 stops
                 # scheduling, every rank drops its pipeline and waits for a chain re-deployment
-                first = not self._aborted
-                self._aborted = True
+                with self._abort_lock:
+                    # the timer exists BEFORE _aborted is set: the serving loop returns on
+                    # _aborted and must find the timer to cancel it (it reads it under this lock)
+                    if not self._aborted and serving.is_set():
+                        # a rank still inside an RCCL op with the dead peer after the grace period
+                        # cannot see a closed connection (gloo can): abort its communicators so the
+                        # op fails instead of waiting for the watchdog
+                        t = threading.Timer(self.ABORT_GRACE_S, self._abort_groups, args=(serving,))
+                        t.daemon = True
+                        t.start()
+                        self._abort_timer = t
+                    self._aborted = True
                 self._pong(msg)
-                if first:
-                    # a rank still inside an RCCL op with the dead peer after the grace period
-                    # cannot see a closed connection (gloo can): abort its communicators so the
-                    # op fails instead of waiting for the watchdog
-                    t = threading.Timer(self.ABORT_GRACE_S, self._abort_groups, args=(serving,))
-                    t.daemon = True
-                    self._abort_timer = t
-                    t.start()
             elif cmd == "replan" or (msg.get("mode") == "pipeline" and "stages" in msg):
                 # live re-shard of the deployed pipeline (reference hot re-config, node_worker.py
                 # :445-474): rank 0 owns the command stream, so the new split is applied there,
@@ -605,9 +607,10 @@ class NodeController:
             lost = repr(e)
         with self._abort_lock:  # no communicator abort may start once serve() has returned
             serving.clear()
-        if self._abort_timer is not None:
-            self._abort_timer.cancel()
-            self._abort_timer.join(timeout=5)  # its thread has exited before the phase changes
+            timer = self._abort_timer  # set, if ever, together with _aborted (same lock)
+        if timer is not None:
+            timer.cancel()
+            timer.join(timeout=5)  # its thread has exited before the phase changes
         dropped = lost is not None or self._aborted
         if dropped:
             with self._submit_lock:  # no submit can slip in between the phase change and the sweep

@@ -11,6 +11,7 @@ if ROOT not in sys.path:
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a ROCm GPU (MI355X) and the built HIP library")
     config.addinivalue_line("markers", "slow: long-running test")
+    config.addinivalue_line("markers", "multigpu: needs >= 2 GPUs (skipped on a 1-GPU box); run after the rest")
 
 
 def _has_gpu() -> bool:
@@ -22,6 +23,8 @@ def _has_gpu() -> bool:
 
 
 def pytest_collection_modifyitems(config, items):
+    # multi-GPU cases last: under -x a failure there cannot hide the single-GPU results
+    items.sort(key=lambda it: "multigpu" in it.keywords)  # stable: the rest keep their order
     if _has_gpu():
         return
     skip = pytest.mark.skip(reason="no GPU in this environment")

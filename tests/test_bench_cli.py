@@ -46,6 +46,16 @@ def test_bench_cli_spawns_ranks(n):
     assert line["config"]["microbatches"] == n  # bench default: one stream -> M = stages
 
 
+def test_bench_cli_two_ranks_match_one_and_prove_placement():
+    """The CPU rehearsal of tests/test_multigpu_gpu.py: the same placement checks and the same
+    token comparison, over gloo (every rank its own process, so its own "device")."""
+    from bench_checks import check_placement
+    one = _run_bench("--gpus", "1", "--model", "tiny", *COMMON)
+    two = _run_bench("--gpus", "2", "--model", "tiny", *COMMON)
+    check_placement(two, 2, "gloo")
+    assert two["tokens_mb0_sha16"] == one["tokens_mb0_sha16"]
+
+
 def test_bench_cli_rank_failure_is_reported():
     """A failing rank must make the launcher exit non-zero (the driver must not see a number)."""
     env = dict(os.environ, OMP_NUM_THREADS="1")
