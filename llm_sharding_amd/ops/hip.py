@@ -16,7 +16,7 @@ import functools
 import json
 import os
 from contextlib import contextmanager
-from typing import Optional, Tuple
+from typing import Optional
 
 import torch
 

@@ -21,11 +21,10 @@ On a CPU device the same engine runs plain torch ops on unpacked weights (the
 """
 from __future__ import annotations
 
-import math
 import os
 from contextlib import contextmanager
 from dataclasses import dataclass
-from typing import Callable, Optional
+from typing import Optional
 
 import torch
 import torch.nn.functional as F

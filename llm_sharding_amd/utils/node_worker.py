@@ -54,9 +54,9 @@ from ..models.rope import full_cos_sin
 from ..models.tokenizer import load_tokenizer
 from ..parallel import protocol
 from ..parallel.communicator import Again, Communicator
-from ..parallel.transport import PullSocket, PushSocket, local_ip, parse_addr
+from ..parallel.transport import PullSocket, PushSocket, local_ip
 from ..runtime.engine import DecodeGraph, ShardFolderSource, StageEngine, WeightSource
-from .forwarding_utils import build_position_ids
+from .forwarding_utils import build_position_ids  # noqa: F401 - re-exported as in the reference module
 
 
 def _log(msg: str) -> None:

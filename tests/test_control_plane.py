@@ -12,7 +12,7 @@ import torch
 from llm_sharding_amd.models import weights as W
 from llm_sharding_amd.models.reference import ReferenceLlama
 from llm_sharding_amd.parallel import protocol
-from llm_sharding_amd.parallel.communicator import Communicator, reset_local_transport
+from llm_sharding_amd.parallel.communicator import reset_local_transport
 from llm_sharding_amd.parallel.transport import Again, PullSocket, PushSocket
 from llm_sharding_amd.utils.config_sender import ConfigSender
 from llm_sharding_amd.utils.node_worker import NodeController, NodeWorker, send_shutdown, send_user_request

@@ -2,7 +2,6 @@
 import json
 import os
 
-import pytest
 import torch
 
 from llm_sharding_amd.config import LlamaConfig, get_preset, llama2_7b, llama32_3b, tiny

@@ -34,7 +34,6 @@ import pytest
 import torch
 
 from llm_sharding_amd.config import get_preset
-from llm_sharding_amd.models import weights as W
 from llm_sharding_amd.models.reference import ReferenceLlama
 from llm_sharding_amd.runtime.engine import DecodeGraph, RandomSource, StageEngine
 

@@ -5,7 +5,7 @@ import os
 import pytest
 import torch
 
-from llm_sharding_amd.config import LlamaConfig, tiny
+from llm_sharding_amd.config import tiny
 from llm_sharding_amd.models import weights as W
 from llm_sharding_amd.models.reference import LAYER_KEYS, ReferenceLlama
 from llm_sharding_amd.runtime.engine import ShardFolderSource, StageEngine
