@@ -406,6 +406,8 @@ def main():
             line["ttft_error"] = f"{type(e).__name__}: {e}"[:200]
     if a.extras and a.gpus == 1 and a.device == "cuda" and not a.stage_layers:
         line["extra"] = extra_runs(a.extras, a)
+    from llm_sharding_amd.utils.runtime_config import knobs_in_effect
+    line["knobs"] = knobs_in_effect()  # LSA_* switches set for this run ({} = the product defaults)
     if res.get("tokens_mb0"):  # parity digest across layouts (same prompts -> same tokens)
         import hashlib
         line["tokens_mb0_sha16"] = hashlib.sha256(json.dumps(res["tokens_mb0"]).encode()).hexdigest()[:16]

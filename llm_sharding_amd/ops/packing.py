@@ -353,5 +353,3 @@ def gemv_config(n_tiles: int, rows: int, need_even: bool = False, k: int = 4096)
     return best
 
 
-def pick_tn(n_tiles: int, need_even: bool = False, rows: int = 1, k: int = 4096) -> int:
-    return gemv_config(n_tiles, rows, need_even, k)[0]

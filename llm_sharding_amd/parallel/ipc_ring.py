@@ -285,29 +285,3 @@ class IpcRingP2P:
         for p in self._own:
             L.lsa_ipc_free(p)
         self._opened, self._own = [], []
-
-
-class HybridP2P:
-    """Messages that fit a ring slot go through ``ipc`` (IpcRingP2P), larger ones (the prompt
-    prefill's hidden states) through ``fallback`` (DistP2P / RCCL). Both ends decide by the
-    message's byte count only (:meth:`IpcRingP2P.fits`), so each channel stays FIFO per edge."""
-
-    graph_capturable = True  # what fits the ring (every decode message) is graph-capturable
-
-    def __init__(self, ipc: IpcRingP2P, fallback):
-        self.ipc, self.fallback = ipc, fallback
-
-    def fits(self, t: torch.Tensor) -> bool:
-        return self.ipc.fits(t)
-
-    def isend(self, t: torch.Tensor, dst: int):
-        return self.ipc.isend(t, dst) if self.ipc.fits(t) else self.fallback.isend(t, dst)
-
-    def recv(self, t: torch.Tensor, src: int) -> None:
-        if self.ipc.fits(t):
-            self.ipc.recv(t, src)
-        else:
-            self.fallback.recv(t, src)
-
-    def check(self) -> None:
-        self.ipc.check()

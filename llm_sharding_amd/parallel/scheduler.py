@@ -219,16 +219,6 @@ def stage_memory(cfg: LlamaConfig, n_layers: int, *, slots: int, max_seq: int, p
             "total": float(w + kv + scratch + io)}
 
 
-def even_split(n_layers: int, n_stages: int) -> list:
-    base, extra = divmod(n_layers, n_stages)
-    out, s = [], 0
-    for k in range(n_stages):
-        e = s + base + (1 if k < extra else 0)
-        out.append((s, e))
-        s = e
-    return out
-
-
 def build_chain_configs(plan: Plan, ingress_stage: int = 0) -> list:
     """ConfigSender payloads (reference schema, config_sender.py:33-40) for a ring chain."""
     n = len(plan.stages)
