@@ -445,7 +445,8 @@ def default_sk_workspace(device=None) -> SkWorkspace:
 N_CU = 256
 
 
-SK_TUNING_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_sk_tuning.json")
+SK_TUNING_FILE = os.environ.get("LSA_GEMM_SK_TUNING") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                                     "gemm_sk_tuning.json")
 _SK_TUNED = None
 _SK_PARTIAL = None
 

@@ -51,6 +51,7 @@ KNOBS = {
     "LSA_PREFLIGHT_FAULT": ("env", "diagnostic", "", "fault injection: 'a->b' drops the preflight message of edge a->b"),
     "LSA_SK_ABLATE": ("define", "diagnostic", "0", "gemm_sk ablation builds (scripts/sk_ablate.py)"),
     "LSA_COOP_ABLATE": ("define", "diagnostic", "0", "coop GEMV ablation builds"),
+    "LSA_GEMM_SK_TUNING": ("env", "diagnostic", "", "path of a gemm_sk tuning table to use instead of ops/gemm_sk_tuning.json (A/B runs)"),
     "LSA_GEMV_TUNING": ("env", "diagnostic", "", "path of a decode-GEMV tuning table to use instead of ops/gemv_tuning.json (A/B runs)"),
     "LSA_STREAM_ABLATE": ("define", "diagnostic", "0", "gemv_stream probe ablation builds (scripts/probes/build_gemv_stream.sh)"),
     "LSA_GEMM_STAMPS": ("define", "diagnostic", "", "gemm_sk per-phase s_memrealtime stamps"),
